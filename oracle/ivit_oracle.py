@@ -1,0 +1,412 @@
+"""CPU oracle for the IntentNetViT hot path — TEST INFRASTRUCTURE ONLY.
+
+A plain PyTorch-fp32 / numpy restatement of the reference algorithm, used by
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg as the checker and CPU baseline. The product (the HIP path in
+``visiontransformer-intention-prediction_amd/``) never imports this file.
+
+Pinning: every function here is checked against golden vectors produced by
+running the reference's OWN ``model_vit.py`` / ``heads.py`` / ``loss.py`` /
+``utils.py`` (``oracle/make_golden.py``; fixtures in ``tests/golden/``).
+Third-party pieces that are absent from this image (timm ViT, torchvision
+``nms``/``sigmoid_focal_loss``, shapely/GEOS) are restated from their
+published algorithms; the timm ViT restatement is additionally cross-checked
+against ``transformers.ViTModel`` (an independent implementation) inside the
+golden generator. See DESIGN.md §Oracle.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+# constants.py:18-25 (ANCHOR_CONFIGS_PAPER), :28-39 (grid / offsets), :72-77
+ANCHOR_CONFIGS = [(2.0, 4.5, 0.0), (2.0, 4.5, math.pi / 2), (2.5, 2.5, 0.0), (1.5, 9.0, 0.0), (4.0, 2.0, 0.0)]
+VOXEL = 0.2
+DOMINANT = (0, 6, 7)  # iteration order of the reference's set({0, 7, 6}) for small ints
+
+
+# --------------------------------------------------------------------------------------
+# ViT stream (timm VisionTransformer.forward_features semantics, model_vit.py:64,71,119)
+# --------------------------------------------------------------------------------------
+def vit_forward_features(sd, prefix, x, num_heads, depth, drop_path_scales=None, eps=1e-6):
+    """timm ``forward_features``: PatchEmbed conv k=s=patch → cat CLS → +pos_embed →
+    ``depth`` pre-norm blocks (LN eps 1e-6, MHSA, exact-erf GELU MLP) → final LN.
+
+    ``drop_path_scales``: optional list (per block) of (attn_scale[B], mlp_scale[B])
+    standing in for timm DropPath's per-sample Bernoulli/keep_prob factors.
+    """
+    w = sd[prefix + "patch_embed.proj.weight"]
+    p = w.shape[-1]
+    t = F.conv2d(x, w, sd[prefix + "patch_embed.proj.bias"], stride=p)
+    B, D = t.shape[0], t.shape[1]
+    t = t.flatten(2).transpose(1, 2)
+    cls = sd[prefix + "cls_token"].expand(B, -1, -1)
+    t = torch.cat([cls, t], dim=1) + sd[prefix + "pos_embed"]
+    N = t.shape[1]
+    hd = D // num_heads
+    for i in range(depth):
+        b = f"{prefix}blocks.{i}."
+        h = F.layer_norm(t, (D,), sd[b + "norm1.weight"], sd[b + "norm1.bias"], eps)
+        qkv = F.linear(h, sd[b + "attn.qkv.weight"], sd[b + "attn.qkv.bias"])
+        q, k, v = qkv.reshape(B, N, 3, num_heads, hd).permute(2, 0, 3, 1, 4).unbind(0)
+        s = (q @ k.transpose(-2, -1)) * (hd ** -0.5)
+        a = torch.softmax(s, dim=-1) @ v
+        a = a.transpose(1, 2).reshape(B, N, D)
+        a = F.linear(a, sd[b + "attn.proj.weight"], sd[b + "attn.proj.bias"])
+        if drop_path_scales is not None:
+            a = a * drop_path_scales[i][0].view(B, 1, 1)
+        t = t + a
+        h = F.layer_norm(t, (D,), sd[b + "norm2.weight"], sd[b + "norm2.bias"], eps)
+        h = F.gelu(F.linear(h, sd[b + "mlp.fc1.weight"], sd[b + "mlp.fc1.bias"]))
+        h = F.linear(h, sd[b + "mlp.fc2.weight"], sd[b + "mlp.fc2.bias"])
+        if drop_path_scales is not None:
+            h = h * drop_path_scales[i][1].view(B, 1, 1)
+        t = t + h
+    return F.layer_norm(t, (D,), sd[prefix + "norm.weight"], sd[prefix + "norm.bias"], eps)
+
+
+def _stream(sd, name, x, num_heads, depth, dps):
+    """model_vit.py:116-122 (_process_stream): drop CLS, adapter LN(eps 1e-5)→Linear→GELU,
+    tokens → (B, C, Hf, Wf) with token n = gy*Wf + gx."""
+    pre = f"backbone.vit_{name}."
+    tok = vit_forward_features(sd, pre, x, num_heads, depth, dps)[:, 1:]
+    a = f"backbone.adapter_{name}."
+    D = tok.shape[-1]
+    y = F.layer_norm(tok, (D,), sd[a + "0.weight"], sd[a + "0.bias"], 1e-5)
+    y = F.gelu(F.linear(y, sd[a + "1.weight"], sd[a + "1.bias"]))
+    p = sd[pre + "patch_embed.proj.weight"].shape[-1]
+    Hf, Wf = x.shape[2] // p, x.shape[3] // p
+    B, Nn, C = y.shape
+    return y.permute(0, 2, 1).contiguous().view(B, C, Hf, Wf)
+
+
+def _bn(x, sd, p, training, momentum=0.1):
+    return F.batch_norm(x, sd[p + "running_mean"], sd[p + "running_var"], sd[p + "weight"], sd[p + "bias"],
+                        training=training, momentum=momentum, eps=1e-5)
+
+
+def fusion_forward(sd, x, layers=2, training=True):
+    """model_vit.py:19-34 BasicBlock ×layers (+1×1 downsample on block 0), :125-132."""
+    for li in range(layers):
+        p = f"backbone.fusion_block.{li}."
+        idn = x
+        o = F.relu(_bn(F.conv2d(x, sd[p + "conv1.weight"], padding=1), sd, p + "bn1.", training))
+        o = _bn(F.conv2d(o, sd[p + "conv2.weight"], padding=1), sd, p + "bn2.", training)
+        if (p + "downsample.0.weight") in sd:
+            idn = _bn(F.conv2d(x, sd[p + "downsample.0.weight"]), sd, p + "downsample.1.", training)
+        x = F.relu(o + idn)
+    return x
+
+
+def heads_forward(sd, feat, num_anchors=5, num_classes=8):
+    """heads.py:18-25,39-43 + model_vit.py:181-184: conv3x3 + view/permute → flat anchors."""
+    B = feat.shape[0]
+    d = F.conv2d(feat, sd["det_head.conv.weight"], sd["det_head.conv.bias"], padding=1)
+    Hf, Wf = d.shape[2:]
+    d = d.view(B, num_anchors, 7, Hf, Wf).permute(0, 3, 4, 1, 2).contiguous()
+    it = F.conv2d(feat, sd["intention_head.conv.weight"], sd["intention_head.conv.bias"], padding=1)
+    it = it.view(B, num_anchors, num_classes, Hf, Wf).permute(0, 3, 4, 1, 2).contiguous()
+    return d[..., 0].reshape(B, -1, 1), d[..., 1:].reshape(B, -1, 6), it.reshape(B, -1, num_classes)
+
+
+def intentnet_forward(sd, lidar, map_bev, cfg, training=False, drop_path_scales=None):
+    """IntentNetViT.forward (model_vit.py:179-185) → (cls (B,A·HW,1), box (B,A·HW,6), intent)."""
+    from oracle.weights import VIT_ARCH
+    al, am = VIT_ARCH[cfg["vit_lidar"]], VIT_ARCH[cfg["vit_map"]]
+    depth_l = cfg.get("depth") or al["depth"]
+    depth_m = cfg.get("depth") or am["depth"]
+    dl = dm = None
+    if drop_path_scales is not None:
+        dl, dm = drop_path_scales
+    fl = _stream(sd, "lidar", lidar, al["num_heads"], depth_l, dl)
+    fm = _stream(sd, "map", map_bev, am["num_heads"], depth_m, dm)
+    feat = fusion_forward(sd, torch.cat([fl, fm], dim=1), cfg["layers"], training)
+    return heads_forward(sd, feat, cfg["num_anchors"], cfg["num_classes"])
+
+
+# --------------------------------------------------------------------------------------
+# Geometry (utils.py)
+# --------------------------------------------------------------------------------------
+def generate_anchors(bev_h=400, bev_w=720, stride=8, configs=ANCHOR_CONFIGS, voxel=VOXEL, off_x=None, off_y=None):
+    """utils.py:519-562 — (Hf·Wf·A, 5) [cx, cy, w, l, yaw], location-major / anchor-minor.
+    Offsets default to the constants.py:38-39 values of the *base* grid (400×720)."""
+    off_x = 720 / 2.0 if off_x is None else off_x
+    off_y = 400 * 3.0 / 4.0 if off_y is None else off_y
+    fh, fw = bev_h // stride, bev_w // stride
+    gy, gx = torch.meshgrid(torch.arange(fh), torch.arange(fw), indexing="ij")
+    px = gx * stride + stride / 2.0
+    py = gy * stride + stride / 2.0
+    ey = (px - off_x) * voxel
+    ex = (off_y - py) * voxel
+    centers = torch.stack([ex, ey], dim=-1).reshape(-1, 2)
+    per = []
+    for (w, l, r) in configs:
+        dims = torch.tensor([w, l, r], dtype=torch.float32).unsqueeze(0).repeat(centers.shape[0], 1)
+        per.append(torch.cat([centers, dims], dim=1))
+    return torch.stack(per, dim=0).transpose(0, 1).reshape(-1, 5)
+
+
+def axis_aligned_iou(b1, b2):
+    """utils.py:276-292 (cols 0..3 only; eps 1e-7 on the union)."""
+    def corners(b):
+        return torch.stack([b[:, 0] - b[:, 2] / 2, b[:, 1] - b[:, 3] / 2,
+                            b[:, 0] + b[:, 2] / 2, b[:, 1] + b[:, 3] / 2], dim=1)
+    c1, c2 = corners(b1), corners(b2)
+    ix1 = torch.maximum(c1[:, None, 0], c2[None, :, 0])
+    iy1 = torch.maximum(c1[:, None, 1], c2[None, :, 1])
+    ix2 = torch.minimum(c1[:, None, 2], c2[None, :, 2])
+    iy2 = torch.minimum(c1[:, None, 3], c2[None, :, 3])
+    inter = torch.clamp(ix2 - ix1, min=0) * torch.clamp(iy2 - iy1, min=0)
+    a1 = b1[:, 2] * b1[:, 3]
+    a2 = b2[:, 2] * b2[:, 3]
+    return inter / ((a1[:, None] + a2[None, :] - inter) + 1e-7)
+
+
+def decode_boxes(rel, anchors):
+    """utils.py:227-257."""
+    if rel.shape[0] == 0:
+        return torch.empty((0, 5))
+    ax, ay, aw, al, ah = anchors.unbind(1)
+    dx, dy, dw, dl, ds, dc = rel.unbind(1)
+    yaw = ah + torch.atan2(ds, dc)
+    yaw = torch.atan2(torch.sin(yaw), torch.cos(yaw))
+    return torch.stack([dx * aw + ax, dy * al + ay, torch.exp(dw) * aw, torch.exp(dl) * al, yaw], dim=-1)
+
+
+def nms_corners_numpy(x1, y1, x2, y2, scores, thr=0.2):
+    """torchvision CPU ``nms`` (published C++ kernel ``nms_kernel_impl``) on x1y1x2y2:
+    stable descending sort; f32 areas/IoU; suppress j if IoU > thr with the f32 IoU
+    promoted to double. Returns kept indices (int64) in score order."""
+    x1, y1, x2, y2 = [np.asarray(v, np.float32) for v in (x1, y1, x2, y2)]
+    s = np.asarray(scores, dtype=np.float32)
+    n = s.shape[0]
+    if n == 0:
+        return np.zeros((0,), np.int64)
+    areas = (x2 - x1) * (y2 - y1)
+    order = np.argsort(-s, kind="stable")
+    sup = np.zeros(n, bool)
+    keep = []
+    zero = np.float32(0)
+    for pos in range(n):
+        i = order[pos]
+        if sup[i]:
+            continue
+        keep.append(i)
+        rest = order[pos + 1:]
+        rest = rest[~sup[rest]]
+        if rest.size == 0:
+            continue
+        w = np.maximum(zero, np.minimum(x2[i], x2[rest]) - np.maximum(x1[i], x1[rest]))
+        h = np.maximum(zero, np.minimum(y2[i], y2[rest]) - np.maximum(y1[i], y1[rest]))
+        inter = w * h
+        ovr = inter / ((areas[i] + areas[rest]) - inter)
+        sup[rest[ovr.astype(np.float64) > float(thr)]] = True
+    return np.asarray(keep, dtype=np.int64)
+
+
+def nms_numpy(boxes_xywha, scores, thr=0.2):
+    """utils.py:259-274 (apply_nms): axis-aligned corners cx∓w/2, cy∓l/2 (yaw ignored) →
+    ``nms_corners_numpy``."""
+    b = np.asarray(boxes_xywha, dtype=np.float32)
+    if b.shape[0] == 0:
+        return np.zeros((0,), np.int64)
+    half = np.float32(2)
+    return nms_corners_numpy(b[:, 0] - b[:, 2] / half, b[:, 1] - b[:, 3] / half,
+                             b[:, 0] + b[:, 2] / half, b[:, 1] + b[:, 3] / half, scores, thr)
+
+
+def _rect_corners(box):
+    """utils.py:295-332 — local corners [-w/2,-l/2],[w/2,-l/2],[w/2,l/2],[-w/2,l/2] rotated by yaw."""
+    cx, cy, w, l, a = [float(v) for v in box]
+    hw, hl = w / 2.0, l / 2.0
+    loc = np.array([[-hw, -hl], [hw, -hl], [hw, hl], [-hw, hl]], dtype=np.float64)
+    c, s = np.cos(a), np.sin(a)
+    R = np.array([[c, -s], [s, c]])
+    return loc @ R.T + np.array([cx, cy])
+
+
+def _poly_area(P):
+    if len(P) < 3:
+        return 0.0
+    x, y = P[:, 0], P[:, 1]
+    return 0.5 * abs(float(np.dot(x, np.roll(y, -1)) - np.dot(y, np.roll(x, -1))))
+
+
+def _ccw(P):
+    x, y = P[:, 0], P[:, 1]
+    sgn = float(np.dot(x, np.roll(y, -1)) - np.dot(y, np.roll(x, -1)))
+    return P if sgn >= 0 else P[::-1]
+
+
+def convex_clip(P, Q):
+    """Sutherland–Hodgman clip of convex polygon P by convex polygon Q (float64)."""
+    P, Q = _ccw(P), _ccw(Q)
+    out = [tuple(p) for p in P]
+    for i in range(len(Q)):
+        if not out:
+            break
+        a, b = Q[i], Q[(i + 1) % len(Q)]
+        inp, out = out, []
+        ex, ey = b[0] - a[0], b[1] - a[1]
+
+        def side(p):
+            return ex * (p[1] - a[1]) - ey * (p[0] - a[0])
+        for j in range(len(inp)):
+            cur, prv = inp[j], inp[j - 1]
+            sc, sp = side(cur), side(prv)
+            if sc >= 0:
+                if sp < 0:
+                    t = sp / (sp - sc)
+                    out.append((prv[0] + t * (cur[0] - prv[0]), prv[1] + t * (cur[1] - prv[1])))
+                out.append(cur)
+            elif sp >= 0:
+                t = sp / (sp - sc)
+                out.append((prv[0] + t * (cur[0] - prv[0]), prv[1] + t * (cur[1] - prv[1])))
+    return np.array(out, dtype=np.float64).reshape(-1, 2)
+
+
+def rotated_iou_numpy(b1, b2):
+    """utils.py:335-392: area<1e-6 → 0; inter ≤ 1e-7 → 0; union ≤ 1e-6 → 0; output f32.
+    GEOS intersection restated as convex clipping in float64 (inputs are rectangles)."""
+    b1 = np.asarray(b1, np.float32)
+    b2 = np.asarray(b2, np.float32)
+    out = np.zeros((b1.shape[0], b2.shape[0]), np.float32)
+    P1 = [_rect_corners(b) for b in b1]
+    P2 = [_rect_corners(b) for b in b2]
+    A1 = [_poly_area(p) for p in P1]
+    A2 = [_poly_area(p) for p in P2]
+    for i in range(len(P1)):
+        if A1[i] < 1e-6:
+            continue
+        for j in range(len(P2)):
+            if A2[j] < 1e-6:
+                continue
+            inter = _poly_area(convex_clip(P1[i], P2[j]))
+            if inter > 1e-7:
+                u = A1[i] + A2[j] - inter
+                if u > 1e-6:
+                    out[i, j] = inter / u
+    return out
+
+
+# --------------------------------------------------------------------------------------
+# Loss (loss.py)
+# --------------------------------------------------------------------------------------
+def sigmoid_focal_loss(x, t, alpha=0.25, gamma=2.0):
+    """torchvision.ops.sigmoid_focal_loss (published Python source), reduction='none'."""
+    p = torch.sigmoid(x)
+    ce = F.binary_cross_entropy_with_logits(x, t, reduction="none")
+    p_t = p * t + (1 - p) * (1 - t)
+    loss = ce * ((1 - p_t) ** gamma)
+    if alpha >= 0:
+        loss = (alpha * t + (1 - alpha) * (1 - t)) * loss
+    return loss
+
+
+def assign_targets(anchors, gt_list, pos_thr=0.6, neg_thr=0.45, iou_fn=axis_aligned_iou):
+    """loss.py:58-126 — per-sample IoU assignment, force-match and delta encoding."""
+    B, NA = len(gt_list), anchors.shape[0]
+    cls_t = torch.full((B, NA), -1, dtype=torch.long)
+    box_t = torch.zeros((B, NA, 6))
+    int_t = torch.full((B, NA), -1, dtype=torch.long)
+    for b in range(B):
+        g = gt_list[b]
+        if not isinstance(g, dict) or "boxes_xywha" not in g or "intentions" not in g or g["boxes_xywha"].shape[0] == 0:
+            cls_t[b, :] = 0
+            continue
+        boxes, ints = g["boxes_xywha"].float(), g["intentions"].long()
+        iou = iou_fn(anchors, boxes)
+        mx, arg = iou.max(dim=1)
+        cls_t[b, mx < neg_thr] = 0
+        pos = mx >= pos_thr
+        cls_t[b, pos] = 1
+        _, best_anchor = iou.max(dim=0)
+        for gi in range(boxes.shape[0]):
+            ai = best_anchor[gi]
+            if not pos[ai] and iou[ai, gi] >= neg_thr:
+                pos[ai] = True
+                cls_t[b, ai] = 1
+        fin = cls_t[b] == 1
+        idx = torch.where(fin)[0]
+        if idx.numel():
+            a, gbx = anchors[idx], boxes[arg[fin]]
+            eps = 1e-6
+            box_t[b, idx] = torch.stack([
+                (gbx[:, 0] - a[:, 0]) / (a[:, 2] + eps), (gbx[:, 1] - a[:, 1]) / (a[:, 3] + eps),
+                torch.log(gbx[:, 2] / (a[:, 2] + eps) + eps), torch.log(gbx[:, 3] / (a[:, 3] + eps) + eps),
+                torch.sin(gbx[:, 4] - a[:, 4]), torch.cos(gbx[:, 4] - a[:, 4])], dim=1)
+            int_t[b, idx] = ints[arg[fin]]
+    return cls_t, box_t, int_t
+
+
+def detection_loss(cls_logits, box_preds, intent_logits, anchors, gt_list, *, downsampling=True,
+                   keep=None, keep_prob=0.15, dominant=DOMINANT, class_weights=None, alpha=0.25, gamma=2.0,
+                   beta=1.0 / 9.0, w_cls=1.0, w_box=1.0, w_int=0.5, iou_fn=axis_aligned_iou):
+    """loss.py:58-206. ``keep``: optional (B, NA) float 0/1 per-anchor keep mask applied to
+    dominant-class positives (the product's device-RNG formulation); ``None`` reproduces
+    the reference's global-RNG ``torch.rand`` draws in dominant-class order."""
+    cls_t, box_t, int_t = assign_targets(anchors, gt_list, iou_fn=iou_fn)
+    ct, bt, it = cls_t.reshape(-1), box_t.reshape(-1, 6), int_t.reshape(-1)
+    cl = cls_logits.reshape(-1, 1)
+    valid, pos = ct >= 0, ct == 1
+    num_pos = pos.sum()
+    cls_loss = torch.tensor(0.0)
+    if valid.any():
+        cls_loss = sigmoid_focal_loss(cl[valid], ct[valid].float().unsqueeze(1), alpha, gamma).sum() / max(1, num_pos)
+    box_loss = torch.tensor(0.0)
+    int_loss = torch.tensor(0.0)
+    if num_pos > 0:
+        box_loss = F.smooth_l1_loss(box_preds.reshape(-1, 6)[pos], bt[pos], beta=beta, reduction="sum") / max(1, num_pos)
+        il = intent_logits.reshape(-1, intent_logits.shape[-1])[pos]
+        itp = it[pos]
+        ce = F.cross_entropy(il, itp, weight=None if downsampling else class_weights, reduction="none")
+        if downsampling:
+            with torch.no_grad():
+                m = torch.ones_like(itp, dtype=torch.float32)
+                if keep is not None:
+                    kf = keep.reshape(-1)[pos].float()
+                    for d in dominant:
+                        sel = itp == d
+                        m[sel] = kf[sel]
+                else:
+                    for d in dominant:
+                        sel = itp == d
+                        if sel.any():
+                            m[sel] = (torch.rand(int(sel.sum().item())) < keep_prob).float()
+            int_loss = (ce * m).sum() / max(1, m.sum())
+        else:
+            int_loss = ce.sum() / max(1, itp.numel())
+    total = w_cls * cls_loss + w_box * box_loss + w_int * int_loss
+    if torch.isnan(total).any() or torch.isinf(total).any():
+        z = torch.tensor(0.0)
+        return {"loss": torch.tensor(0.0, requires_grad=True), "cls_loss": z, "box_loss": z,
+                "intent_loss": z, "num_pos_anchors": int(num_pos)}
+    return {"loss": total, "cls_loss": cls_loss.detach(), "box_loss": box_loss.detach(),
+            "intent_loss": int_loss.detach(), "num_pos_anchors": int(num_pos)}
+
+
+# --------------------------------------------------------------------------------------
+# Synthetic inputs (BASELINE.md "CPU baseline plan"; SURVEY.md §8(d) synthetic inputs)
+# --------------------------------------------------------------------------------------
+def synthetic_batch(B, img_size=(400, 720), lidar_ch=290, map_ch=9, seed=1234, G=20, grid_scale=1.0,
+                    box_region=None):
+    """lidar ~ U[0,1), map ~ Bernoulli(0.1), G boxes per sample. ``box_region`` =
+    (xmin, xmax, ymin, ymax) overrides the metric box-centre range."""
+    g = torch.Generator().manual_seed(seed)
+    H, W = img_size
+    lidar = torch.rand((B, lidar_ch, H, W), generator=g)
+    mp = (torch.rand((B, map_ch, H, W), generator=g) < 0.1).float()
+    if box_region is None:
+        box_region = (-20.0 * grid_scale, 60.0 * grid_scale, -72.0 * grid_scale, 72.0 * grid_scale)
+    x0, x1, y0, y1 = box_region
+    gts = []
+    for _ in range(B):
+        u = torch.rand((G, 5), generator=g)
+        boxes = torch.stack([x0 + (x1 - x0) * u[:, 0], y0 + (y1 - y0) * u[:, 1], 1.5 + 1.5 * u[:, 2],
+                             3.5 + 3.0 * u[:, 3], -math.pi + 2 * math.pi * u[:, 4]], dim=1)
+        ints = torch.randint(0, 8, (G,), generator=g)
+        gts.append({"boxes_xywha": boxes.float(), "intentions": ints.long()})
+    return lidar, mp, gts

@@ -1,0 +1,216 @@
+"""Generate golden vectors from the reference's OWN code (run HERE only).
+
+    cd /root/repo && python -m oracle.make_golden
+
+Imports ``model_vit``, ``heads``, ``loss``, ``utils``, ``constants`` from
+/root/reference through ``oracle/refshim.py`` stand-ins, feeds them seeded
+inputs and the ``oracle/weights.py`` filler, and writes small ``.npz``
+fixtures (inputs as seeds + checksums, outputs as arrays / strided samples)
+into ``tests/golden/``. The reference never travels to the GPU box: only these
+data files do.
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+
+from oracle import ivit_oracle as O  # noqa: E402
+from oracle import refshim  # noqa: E402
+from oracle.weights import make_state_dict, model_cfg, state_checksum  # noqa: E402
+
+OUT = os.path.join(REPO, "tests", "golden")
+SMALL_IMG = (32, 48)
+N_SAMPLE = 64
+
+
+def _sample(t):
+    f = t.detach().reshape(-1).double()
+    stride = max(1, f.numel() // N_SAMPLE)
+    s = f[::stride][:N_SAMPLE].numpy()
+    out = np.full(N_SAMPLE, np.nan)
+    out[: s.size] = s
+    return out, stride
+
+
+def small_gt(seed=4321):
+    """GT boxes inside the 32×48 grid's anchor footprint (x∈[54,60], y∈[-72,-62])."""
+    g = torch.Generator().manual_seed(seed)
+    gts = []
+    for G in (6, 4):
+        u = torch.rand((G, 5), generator=g)
+        boxes = torch.stack([54.0 + 6.0 * u[:, 0], -72.0 + 10.0 * u[:, 1], 1.5 + 1.5 * u[:, 2],
+                             3.5 + 3.0 * u[:, 3], -math.pi + 2 * math.pi * u[:, 4]], 1).float()
+        gts.append({"boxes_xywha": boxes, "intentions": torch.randint(0, 8, (G,), generator=g)})
+    return gts
+
+
+def gen_model_small():
+    import loss as ref_loss
+    import model_vit as ref_model
+    import utils as ref_utils
+    cfg = model_cfg(img_size=SMALL_IMG)
+    sd = make_state_dict(cfg, seed=0)
+    lidar, mp, _ = O.synthetic_batch(2, SMALL_IMG, seed=1234)
+    gts = small_gt()
+    anchors = ref_utils.generate_anchors(SMALL_IMG[0], SMALL_IMG[1], 8)
+    bcfg = {"img_size": SMALL_IMG, "lidar_input_channels": 290, "map_input_channels": 9,
+            "drop_path_rate_lidar": 0.0, "drop_path_rate_map": 0.0}
+    m = ref_model.IntentNetViT(backbone_cfg=dict(bcfg))
+    m.load_state_dict(refshim.timm_to_hf_state(sd), strict=True)
+    rec = {"cfg": json.dumps(cfg), "w_checksum": state_checksum(sd),
+           "lidar_sum": float(lidar.double().sum()), "map_sum": float(mp.double().sum()),
+           "anchors": anchors.numpy()}
+    for i, g in enumerate(gts):
+        rec[f"gt{i}_boxes"] = g["boxes_xywha"].numpy()
+        rec[f"gt{i}_ints"] = g["intentions"].numpy()
+    m.eval()
+    with torch.no_grad():
+        c, b, it = m(lidar, mp)
+    rec.update(eval_cls=c.numpy(), eval_box=b.numpy(), eval_int=it.numpy())
+    # train mode, DropPath 0, BN batch statistics, downsampling off
+    m.train()
+    c, b, it = m(lidar, mp)
+    lf = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False)
+    d = lf(c, b, it, anchors, gts)
+    d["loss"].backward()
+    rec.update(train_cls=c.detach().numpy(), train_box=b.detach().numpy(), train_int=it.detach().numpy(),
+               train_loss=np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]),
+                                    float(d["intent_loss"]), float(d["num_pos_anchors"])]))
+    grads = refshim.hf_grads_to_timm({k: p.grad for k, p in m.named_parameters() if p.grad is not None})
+    names = sorted(grads)
+    samples, strides = zip(*[_sample(grads[k]) for k in names])
+    rec.update(grad_names=np.array(names), grad_sum=np.array([float(grads[k].double().sum()) for k in names]),
+               grad_abssum=np.array([float(grads[k].double().abs().sum()) for k in names]),
+               grad_samples=np.stack(samples), grad_strides=np.array(strides))
+    bn = {k: v for k, v in m.state_dict().items() if "running_" in k}
+    rec.update(bn_names=np.array(sorted(bn)), bn_values=np.stack([bn[k].numpy() for k in sorted(bn)]))
+    # downsampling on: the reference's own torch.rand draws under a fixed global seed
+    with torch.no_grad():
+        torch.manual_seed(77)
+        d2 = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=True)(c, b, it, anchors, gts)
+    rec["train_loss_ds"] = np.array([float(d2["loss"]), float(d2["cls_loss"]), float(d2["box_loss"]),
+                                     float(d2["intent_loss"]), float(d2["num_pos_anchors"])])
+    np.savez_compressed(os.path.join(OUT, "model_small.npz"), **rec)
+    print("model_small: loss", rec["train_loss"], "ds", rec["train_loss_ds"])
+
+
+def gen_geometry():
+    import loss as ref_loss
+    import utils as ref_utils
+    rec = {}
+    anchors = ref_utils.generate_anchors(400, 720, 8)
+    rec["anchors"] = anchors.numpy()
+    # --- full-size loss on seeded random head outputs ---
+    g = torch.Generator().manual_seed(99)
+    B, NA = 2, anchors.shape[0]
+    cls = torch.randn((B, NA, 1), generator=g)
+    box = 0.5 * torch.randn((B, NA, 6), generator=g)
+    it = torch.randn((B, NA, 8), generator=g)
+    rec["logits_seed"] = np.array([99])
+    rec["logits_sums"] = np.array([float(cls.double().sum()), float(box.double().sum()), float(it.double().sum())])
+    _, _, gts = O.synthetic_batch(B, seed=2024, G=20)
+    # sample 1: GT centred exactly on anchors (ties between yaw-0 / yaw-90 anchors, force-match)
+    sel = torch.tensor([5, 4005, 11117, 20000, 22499]) // 5
+    a0 = anchors[sel * 5]
+    gts[1]["boxes_xywha"] = torch.cat([gts[1]["boxes_xywha"][:15],
+                                       torch.stack([a0[:, 0], a0[:, 1], torch.full((5,), 2.0),
+                                                    torch.full((5,), 4.5), torch.zeros(5)], 1)])
+    for i, gg in enumerate(gts):
+        rec[f"gt{i}_boxes"] = gg["boxes_xywha"].numpy()
+        rec[f"gt{i}_ints"] = gg["intentions"].numpy()
+    iou = ref_utils.compute_axis_aligned_iou(anchors, gts[0]["boxes_xywha"])
+    mx, arg = iou.max(dim=1)
+    _, arg0 = iou.max(dim=0)
+    rec.update(iou_max=mx.numpy(), iou_arg=arg.numpy(), iou_arg0=arg0.numpy(), iou_sample=iou[::97].numpy())
+    lf = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False)
+    d = lf(cls, box, it, anchors, gts)
+    rec["loss_full"] = np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]),
+                                 float(d["intent_loss"]), float(d["num_pos_anchors"])])
+    torch.manual_seed(5)
+    d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=True)(cls, box, it, anchors, gts)
+    rec["loss_full_ds"] = np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]),
+                                    float(d["intent_loss"]), float(d["num_pos_anchors"])])
+    # empty / malformed GT → all anchors negative
+    d = lf(cls, box, it, anchors, [{"boxes_xywha": torch.zeros((0, 5)), "intentions": torch.zeros((0,), dtype=torch.long)}, {}])
+    rec["loss_empty"] = np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]),
+                                  float(d["intent_loss"]), float(d["num_pos_anchors"])])
+    # --- decode ---
+    g = torch.Generator().manual_seed(7)
+    idx = torch.randperm(NA, generator=g)[:1000]
+    rel = 0.5 * torch.randn((1000, 6), generator=g)
+    rec.update(dec_idx=idx.numpy(), dec_rel=rel.numpy(),
+               dec_out=ref_utils.decode_box_predictions(rel, anchors[idx]).numpy())
+    # --- NMS (apply_nms) cases ---
+    cases = []
+    g = torch.Generator().manual_seed(11)
+    rel = 0.1 * torch.randn((NA, 6), generator=g)
+    rel[:, 4:] = torch.randn((NA, 2), generator=g)
+    boxes = ref_utils.decode_box_predictions(rel, anchors)
+    scores = torch.sigmoid(0.5 * torch.randn(NA, generator=g))
+    cases.append((boxes, scores))                                      # full 22500, eval-like
+    cases.append((boxes[:3000], torch.round(scores[:3000] * 16) / 16))  # heavy score ties
+    s1 = torch.full((3000,), 0.5)
+    cases.append((boxes[:3000], s1))                                   # all equal scores
+    ex = torch.tensor([[0.5, 0.5, 1.0, 1.0, 0.0], [0.5, 0.1, 1.0, 0.2, 0.0], [0.5, 0.9, 1.0, 0.2, 0.3],
+                       [0.1, 0.5, 0.2, 1.0, 0.0], [3.0, 3.0, 1.0, 1.0, 0.0], [3.0, 3.0, 1.0, 1.0, 0.0],
+                       [0.5, 0.5, 0.0, 1.0, 0.0]], dtype=torch.float32)
+    cases.append((ex, torch.tensor([0.9, 0.8, 0.7, 0.6, 0.5, 0.5, 0.95])))  # IoU == 0.2f, dup, zero-area
+    cases.append((torch.zeros((0, 5)), torch.zeros(0)))                # empty
+    off = [0]
+    keeps = []
+    for i, (bx, sc) in enumerate(cases):
+        rec[f"nms{i}_boxes"] = bx.numpy()
+        rec[f"nms{i}_scores"] = sc.numpy()
+        k = ref_utils.apply_nms(bx, sc, 0.2).numpy()
+        rec[f"nms{i}_keep"] = k
+        keeps.append(k.size)
+    rec["nms_cases"] = np.array([len(cases)])
+    # --- rotated IoU ---
+    g = torch.Generator().manual_seed(13)
+    b1 = torch.stack([10 * torch.rand(48, generator=g), 10 * torch.rand(48, generator=g),
+                      0.5 + 3 * torch.rand(48, generator=g), 0.5 + 6 * torch.rand(48, generator=g),
+                      -math.pi + 2 * math.pi * torch.rand(48, generator=g)], 1)
+    b2 = b1[torch.randperm(48, generator=g)[:24]].clone()
+    b2[:, :2] += 0.7 * torch.randn((24, 2), generator=g)
+    b2[:, 4] += 0.3 * torch.randn(24, generator=g)
+    b1[3, 2] = 0.0                                                    # degenerate box → 0 row
+    rec.update(rot_b1=b1.numpy(), rot_b2=b2.numpy(), rot_iou=ref_utils.compute_rotated_iou(b1, b2).numpy())
+    np.savez_compressed(os.path.join(OUT, "geometry.npz"), **rec)
+    print("geometry: loss", rec["loss_full"], "ds", rec["loss_full_ds"], "nms keeps", keeps)
+
+
+def cross_check_vit():
+    """HF ViTModel (stand-in) vs the oracle's timm restatement, 12 blocks, real widths."""
+    cfg = model_cfg(img_size=SMALL_IMG)
+    sd = make_state_dict(cfg, seed=0)
+    vit = refshim.HFTimmViT("vit_small_patch8_224", in_chans=9, img_size=SMALL_IMG)
+    pre = "backbone.vit_map."
+    vit.load_state_dict({k[len(pre + "hf."):]: v for k, v in refshim.timm_to_hf_state(sd).items()
+                         if k.startswith(pre + "hf.")} | {}, strict=False)
+    hf_sd = {("hf." + k[len(pre + "hf."):]): v for k, v in refshim.timm_to_hf_state(sd).items() if k.startswith(pre + "hf.")}
+    vit.load_state_dict(hf_sd, strict=True)
+    _, mp, _ = O.synthetic_batch(2, SMALL_IMG, seed=1234)
+    with torch.no_grad():
+        a = vit.forward_features(mp)
+        b = O.vit_forward_features(sd, pre, mp, 6, 12)
+    err = float((a - b).abs().max())
+    print("HF vs oracle ViT max abs diff", err)
+    assert err < 1e-4, err
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    refshim.install()
+    torch.set_num_threads(8)
+    cross_check_vit()
+    gen_model_small()
+    gen_geometry()

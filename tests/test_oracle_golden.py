@@ -1,0 +1,136 @@
+"""Pin the CPU oracle against golden vectors produced by the reference's own code
+(``oracle/make_golden.py``). CPU only."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import ivit_oracle as O
+from oracle.weights import make_state_dict, state_checksum
+
+
+def _gts(z, n):
+    return [{"boxes_xywha": torch.from_numpy(z[f"gt{i}_boxes"]), "intentions": torch.from_numpy(z[f"gt{i}_ints"])}
+            for i in range(n)]
+
+
+@pytest.fixture(scope="module")
+def small():
+    z = golden("model_small.npz")
+    cfg = json.loads(str(z["cfg"]))
+    cfg["img_size"] = tuple(cfg["img_size"])
+    sd = make_state_dict(cfg, seed=0)
+    lidar, mp, _ = O.synthetic_batch(2, cfg["img_size"], seed=1234)
+    return z, cfg, sd, lidar, mp
+
+
+def test_inputs_regenerate(small):
+    z, cfg, sd, lidar, mp = small
+    assert abs(state_checksum(sd) - float(z["w_checksum"])) < 1e-6 * abs(float(z["w_checksum"]))
+    assert float(lidar.double().sum()) == pytest.approx(float(z["lidar_sum"]), rel=1e-12)
+    assert float(mp.double().sum()) == pytest.approx(float(z["map_sum"]), rel=1e-12)
+
+
+def test_anchors_bitexact():
+    z = golden("geometry.npz")
+    assert np.array_equal(O.generate_anchors(400, 720, 8).numpy(), z["anchors"])
+    zs = golden("model_small.npz")
+    assert np.array_equal(O.generate_anchors(32, 48, 8).numpy(), zs["anchors"])
+
+
+def test_forward_eval(small):
+    z, cfg, sd, lidar, mp = small
+    sd = {k: v.clone() for k, v in sd.items()}
+    with torch.no_grad():
+        c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=False)
+    for got, key in ((c, "eval_cls"), (b, "eval_box"), (i, "eval_int")):
+        ref = z[key]
+        assert got.shape == ref.shape
+        np.testing.assert_allclose(got.numpy(), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_train_forward_loss_grads(small):
+    z, cfg, sd, lidar, mp = small
+    sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v.clone())
+          for k, v in sd.items()}
+    c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=True)
+    np.testing.assert_allclose(c.detach().numpy(), z["train_cls"], rtol=1e-4, atol=1e-4)
+    anchors = torch.from_numpy(z["anchors"])
+    gts = _gts(z, 2)
+    d = O.detection_loss(c, b, i, anchors, gts, downsampling=False)
+    got = np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]),
+                    d["num_pos_anchors"]])
+    np.testing.assert_allclose(got, z["train_loss"], rtol=1e-5)
+    d["loss"].backward()
+    for name, gs, gas, smp, st in zip(z["grad_names"], z["grad_sum"], z["grad_abssum"], z["grad_samples"],
+                                      z["grad_strides"]):
+        g = sd[str(name)].grad
+        assert g is not None, name
+        assert float(g.double().abs().sum()) == pytest.approx(gas, rel=1e-3, abs=1e-6), name
+        s = g.reshape(-1).double()[:: int(st)][:64].numpy()
+        m = ~np.isnan(smp)
+        np.testing.assert_allclose(s, smp[m][: s.size], rtol=2e-3, atol=2e-5 * max(1.0, np.abs(smp[m]).max()),
+                                   err_msg=str(name))
+    for name, val in zip(z["bn_names"], z["bn_values"]):
+        np.testing.assert_allclose(sd[str(name)].numpy(), val, rtol=1e-4, atol=1e-5)
+    with torch.no_grad():
+        torch.manual_seed(77)
+        d2 = O.detection_loss(c, b, i, anchors, gts, downsampling=True)
+    got = np.array([float(d2["loss"]), float(d2["cls_loss"]), float(d2["box_loss"]), float(d2["intent_loss"]),
+                    d2["num_pos_anchors"]])
+    np.testing.assert_allclose(got, z["train_loss_ds"], rtol=1e-5)
+
+
+def _logits(z, NA):
+    g = torch.Generator().manual_seed(int(z["logits_seed"][0]))
+    cls = torch.randn((2, NA, 1), generator=g)
+    box = 0.5 * torch.randn((2, NA, 6), generator=g)
+    it = torch.randn((2, NA, 8), generator=g)
+    sums = [float(t.double().sum()) for t in (cls, box, it)]
+    np.testing.assert_allclose(sums, z["logits_sums"], rtol=1e-12)
+    return cls, box, it
+
+
+def test_full_size_assignment_and_loss():
+    z = golden("geometry.npz")
+    anchors = torch.from_numpy(z["anchors"])
+    gts = _gts(z, 2)
+    iou = O.axis_aligned_iou(anchors, gts[0]["boxes_xywha"])
+    mx, arg = iou.max(dim=1)
+    assert np.array_equal(mx.numpy(), z["iou_max"]) and np.array_equal(arg.numpy(), z["iou_arg"])
+    assert np.array_equal(iou.max(dim=0)[1].numpy(), z["iou_arg0"])
+    cls, box, it = _logits(z, anchors.shape[0])
+    d = O.detection_loss(cls, box, it, anchors, gts, downsampling=False)
+    got = [float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]), d["num_pos_anchors"]]
+    np.testing.assert_allclose(got, z["loss_full"], rtol=1e-5)
+    torch.manual_seed(5)
+    d = O.detection_loss(cls, box, it, anchors, gts, downsampling=True)
+    got = [float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]), d["num_pos_anchors"]]
+    np.testing.assert_allclose(got, z["loss_full_ds"], rtol=1e-5)
+    empty = [{"boxes_xywha": torch.zeros((0, 5)), "intentions": torch.zeros((0,), dtype=torch.long)}, {}]
+    d = O.detection_loss(cls, box, it, anchors, empty, downsampling=False)
+    got = [float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]), d["num_pos_anchors"]]
+    np.testing.assert_allclose(got, z["loss_empty"], rtol=1e-5)
+
+
+def test_decode():
+    z = golden("geometry.npz")
+    anchors = torch.from_numpy(z["anchors"])
+    out = O.decode_boxes(torch.from_numpy(z["dec_rel"]), anchors[torch.from_numpy(z["dec_idx"])])
+    np.testing.assert_array_equal(out.numpy(), z["dec_out"])
+
+
+def test_nms_keep_bitexact():
+    z = golden("geometry.npz")
+    for i in range(int(z["nms_cases"][0])):
+        keep = O.nms_numpy(z[f"nms{i}_boxes"], z[f"nms{i}_scores"], 0.2)
+        assert np.array_equal(keep, z[f"nms{i}_keep"]), i
+
+
+def test_rotated_iou():
+    z = golden("geometry.npz")
+    got = O.rotated_iou_numpy(z["rot_b1"], z["rot_b2"])
+    np.testing.assert_allclose(got, z["rot_iou"], atol=1e-6)
+    assert np.all(got[3] == 0)
