@@ -1,0 +1,199 @@
+"""Headline benchmark: IntentNetViT training step (fwd + loss + bwd + AdamW) on synthetic
+BEV tensors of the constants.py grid — BASELINE.json metric "BEV samples/sec (fwd+bwd)
+IntentNetViT at 1/2/4/8 MI355X; attn MFMA util %", config 2 (bf16, batch 8 per GPU) at
+N=1 and config 3 (DDP over RCCL) for N>1.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(HERE, "visiontransformer-intention-prediction_amd")
+sys.path.insert(0, PKG)
+
+PEAK_BF16_TFLOPS = 2516.6  # 256 CU x 2.4 GHz x 4096 dense bf16 flop/clk (MI355X_MICROARCH.md)
+
+
+def step_flops(B, H, W, depth=12, D=384, C_l=290, C_m=9, planes=512, A=5, K=8, adapter=192):
+    """Algorithmic fwd+bwd FLOPs of one train step (2*MAC; bwd = 2 x fwd except patch-embed dgrad)."""
+    Np = (H // 8) * (W // 8)
+    N = Np + 1
+    per_block = 2 * N * D * (3 * D) + 2 * N * D * D + 2 * 2 * N * D * 4 * D + 2 * 2 * N * N * D
+    vit = 2 * depth * per_block
+    patch = 2 * Np * D * 64 * (C_l + C_m)
+    adapters = 2 * 2 * Np * D * adapter
+    cin = 2 * adapter
+    fusion = 2 * Np * planes * (9 * cin + 9 * planes + cin + 9 * planes + 9 * planes)
+    heads = 2 * Np * 9 * planes * A * (7 + K)
+    fwd = vit + patch + adapters + fusion + heads
+    return B * (3 * fwd - patch), B * (3 * vit)
+
+
+def attn_fwd_flops(B, N, H, Dh=64):
+    return 4.0 * B * H * N * N * Dh
+
+
+def cpu_baseline(seconds_budget=25.0):
+    """The CPU oracle's train step (B=1, full grid, f32) on this host's cores."""
+    sys.path.insert(0, HERE)
+    from oracle import ivit_oracle as O
+    from oracle.weights import make_state_dict, model_cfg
+    torch.set_num_threads(max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
+    cfg = model_cfg()
+    sd = {k: (v.requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
+          for k, v in make_state_dict(cfg, seed=0).items()}
+    opt = torch.optim.AdamW([v for v in sd.values() if v.requires_grad], lr=1e-4, weight_decay=1e-4)
+    lidar, mp, gts = O.synthetic_batch(1, seed=1234)
+    anchors = O.generate_anchors()
+
+    def step():
+        opt.zero_grad()
+        c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=True)
+        d = O.detection_loss(c, b, i, anchors, gts, downsampling=True)
+        d["loss"].backward()
+        opt.step()
+
+    t0 = time.time()
+    step()  # warm-up
+    warm = time.time() - t0
+    n = max(1, min(3, int(seconds_budget / max(warm, 1e-3))))
+    ts = []
+    for _ in range(n):
+        t0 = time.time()
+        step()
+        ts.append(time.time() - t0)
+    med = sorted(ts)[len(ts) // 2]
+    return {"value": 1.0 / med, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle f32 train step (fwd+loss+bwd+AdamW), B=1, 400x720, median of {n} after 1 warm-up",
+            "step_s": med}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch (BASELINE config 2/3: 8)")
+    ap.add_argument("--grid", type=str, default="400x720")
+    ap.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--bucket-mb", type=int, default=64)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import loss as L
+    import model_vit
+    import ops
+    import utils
+    from optim import FusedAdamW
+
+    H, W = (int(v) for v in args.grid.split("x"))
+    B = args.batch
+    cd = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(0)
+    model = model_vit.IntentNetViT(backbone_cfg={"img_size": (H, W)}).to(dev).set_compute_dtype(cd).train()
+    net = model
+    if world > 1:
+        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
+                                                        gradient_as_bucket_view=True, broadcast_buffers=False)
+    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    lf = L.DetectionIntentionLoss(use_rotated_iou=False, apply_intention_downsampling=True)
+    anchors = utils.generate_anchors(H, W, 8, device=dev)
+    g = torch.Generator().manual_seed(1234 + rank)
+    lidar = torch.rand((B, 290, H, W), generator=g).to(dev)
+    mp = (torch.rand((B, 9, H, W), generator=g) < 0.1).float().to(dev)
+    sc = H / 400.0
+    gts = []
+    for _ in range(B):
+        u = torch.rand((20, 5), generator=g)
+        boxes = torch.stack([-20 * sc + 80 * sc * u[:, 0], -72 * sc + 144 * sc * u[:, 1], 1.5 + 1.5 * u[:, 2],
+                             3.5 + 3.0 * u[:, 3], -math.pi + 2 * math.pi * u[:, 4]], 1)
+        gts.append({"boxes_xywha": boxes, "intentions": torch.randint(0, 8, (20,), generator=g)})
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        c, b, i = net(lidar, mp)
+        d = lf(c, b, i, anchors, gts)
+        d["loss"].backward()
+        opt.step()
+        return d
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ops.KernelTimer.enabled = {"attn_fwd"}
+    ops.KernelTimer.records = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        d = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    attn_ms = ops.KernelTimer.mean_ms("attn_fwd")
+    ops.KernelTimer.enabled = set()
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t)
+    loss_v = float(d["loss"])
+    gb = B * world
+    value = gb * args.steps / el
+    ms = el / args.steps * 1e3
+    fl_step, fl_vit = step_flops(B, H, W)
+    N = (H // 8) * (W // 8) + 1
+    afl = attn_fwd_flops(B, N, 6)
+    achieved = afl / (attn_ms * 1e-3) / 1e12
+    peak = PEAK_BF16_TFLOPS if cd == torch.bfloat16 else 157.3
+    out = {
+        "metric": "BEV samples/sec (fwd+bwd) IntentNetViT at 1/2/4/8 MI355X; attn MFMA util %",
+        "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.dtype, "data": "synthetic (random BEV rasters U[0,1)/Bernoulli(0.1), 20 random GT/sample; "
+                                     "random-init weights)",
+        "config": {"workload": f"IntentNetViT train step (fwd+loss+bwd+AdamW), {args.dtype}, {H}x{W}, "
+                               f"batch {B}/GPU", "global_batch": gb, "per_gpu_batch": B, "grid": [H, W],
+                   "tokens_per_stream": N, "parallelism": f"dp{world}"},
+        "roofline": {"kernel": "attn_fwd_bf16_kernel (ivit_attn_fwd)", "bound": "mfma",
+                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "per_launch": f"4*B*H*N^2*64 = {afl:.4g} flop (B={B}, H=6, N={N}); {attn_ms:.4f} ms avg over "
+                                   f"{len(ops.KernelTimer.records.get('attn_fwd', []))} launches (HIP events)"},
+        "step_mfma": {"achieved": round(fl_step * world / el * args.steps / 1e12 / world, 2), "unit": "TFLOP/s/GPU",
+                      "frac": round(fl_step / (el / args.steps) / 1e12 / peak, 4),
+                      "flops_per_step_per_gpu": fl_step},
+        "loss": loss_v,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

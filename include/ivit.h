@@ -1,0 +1,162 @@
+/* libivit_hip — C ABI of the MI355X-native IntentNetViT hot path (gfx950 / CDNA4).
+ *
+ * Every entry point is stream-ordered and stateless: buffers are caller-owned device
+ * pointers (PyTorch caching allocator on the Python side), sizes are plain integers,
+ * the stream is a hipStream_t passed as void*. Return value: 0 on success, <0 for bad
+ * arguments (message in ivit_last_error()), >0 for a hipError_t from the launch.
+ * dtype selects the compute path: IVIT_F32 (exact f32 MFMA; the parity path) or
+ * IVIT_BF16 (bf16 MFMA, f32 accumulation; the throughput path).
+ *
+ * Each function names the reference interface (file:line under the reference repo) whose
+ * arithmetic it implements; the Python host layer mirrors those interfaces.
+ */
+#ifndef IVIT_H
+#define IVIT_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IVIT_OK 0
+#define IVIT_ERR_ARG (-1)
+#define IVIT_ERR_UNSUPPORTED (-2)
+
+#define IVIT_F32 0
+#define IVIT_BF16 1
+
+#define IVIT_ACT_NONE 0
+#define IVIT_ACT_GELU 1
+#define IVIT_ACT_RELU 2
+
+const char* ivit_version(void);
+const char* ivit_last_error(void);
+
+/* ---- Linear layers: timm Attention.qkv/proj, Mlp.fc1/fc2 (reached from model_vit.py:64,71,119)
+ *      and the adapters nn.Linear(384,192) (model_vit.py:82-83).                              */
+/* Y[M,N] = act(X[M,K] W[N,K]^T + b)  (Ypre: optional pre-activation copy), or, when resid != 0,
+ * Y(f32) = resid + row_scale[m / rows_per_scale] * (X W^T + b)   (residual + DropPath, timm Block). */
+int ivit_linear_fwd(int dtype, const void* X, long ldx, const void* W, const float* bias, long M, long N, long K,
+                    int act, void* Y, long ldy, int y_dtype, void* Ypre, const float* resid, long ldr,
+                    const float* row_scale, long rows_per_scale, void* stream);
+/* dX[M,K] = dY[M,N] W[N,K]  (optionally * gelu'(pre[M,K])). */
+int ivit_linear_dgrad(int dtype, const void* dY, long lddy, const void* W, long M, long N, long K, void* dX,
+                      long lddx, int dx_dtype, const void* gelu_pre, long ldpre, void* stream);
+/* dW[N,K] (+)= dY^T X ; dbias[N] (+)= colsum(dY). f32 outputs; split-K through `work`. */
+long ivit_linear_wgrad_workspace(long M, long N, long K);
+int ivit_linear_wgrad(int dtype, const void* dY, long lddy, const void* X, long ldx, long M, long N, long K,
+                      float* dW, float* dbias, int accumulate, void* work, long work_bytes, void* stream);
+
+/* ---- timm PatchEmbed (Conv2d k=s=8) + CLS concat + pos_embed (model_vit.py:64,71 → timm). */
+int ivit_patch_embed_fwd(int dtype, const float* img, long B, long C, long H, long W, const void* Wt,
+                         const float* bias, const float* pos, const float* cls, long D, float* out, void* stream);
+long ivit_patch_embed_wgrad_workspace(long B, long C, long H, long W, long D);
+int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* img, long B, long C, long H, long W, long D,
+                           float* dW, float* dbias, float* dpos, float* dcls, int accumulate, void* work,
+                           long work_bytes, void* stream);
+
+/* ---- k x k stride-1 "same" convolution on NHWC maps (BasicBlock conv3x3/conv1x1,
+ *      model_vit.py:12-17; DetectionHead/IntentionHead conv, heads.py:16,37).
+ *      Weights packed [Cout][k][k][Cin] (see ivit_pack_conv_weight).                           */
+int ivit_conv_fwd(int dtype, const void* X, long B, long H, long W, long Cin, const void* Wp, const float* bias,
+                  long Cout, long ks, void* Y, long ldy, int y_dtype, void* stream);
+int ivit_conv_dgrad(int dtype, const void* dY, long lddy, long B, long H, long W, long Cout, const void* Wp,
+                    long Cin, long ks, void* dX, int dx_dtype, void* stream);
+long ivit_conv_wgrad_workspace(long B, long H, long W, long Cin, long Cout, long ks);
+int ivit_conv_wgrad(int dtype, const void* dY, long lddy, const void* X, long B, long H, long W, long Cin,
+                    long Cout, long ks, float* dWp, float* dbias, int accumulate, void* work, long work_bytes,
+                    void* stream);
+/* torch [Cout][Cin][k][k] f32  ->  packed [Cout_pad][k][k][Cin] (dtype), rows >= Cout zeroed. */
+int ivit_pack_conv_weight(int dtype, const float* w, long Cout, long Cin, long ks, long Cout_pad, void* out,
+                          void* stream);
+/* packed f32 gradient [Cout_pad][k][k][Cin] -> torch layout [Cout][Cin][k][k] (+= if accumulate). */
+int ivit_unpack_conv_grad(const float* gp, long Cout, long Cin, long ks, float* out, int accumulate, void* stream);
+
+/* ---- Multi-head self-attention core: timm Attention -> F.scaled_dot_product_attention
+ *      (softmax(Q K^T / sqrt(Dh)) V, no mask, no dropout). qkv: [B, N, 3, H, Dh] rows of 3*H*Dh;
+ *      out: [B, N, H*Dh]; lse: [B, H, N] f32 (natural-log-sum-exp of the scaled scores).        */
+long ivit_attn_workspace(int dtype, long B, long N, long H, long Dh, int backward);
+int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H, long Dh, void* out, float* lse, void* work,
+                  long work_bytes, void* stream);
+int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse, long B, long N,
+                  long H, long Dh, void* dqkv, void* work, long work_bytes, void* stream);
+
+/* ---- LayerNorm over the last dim D (timm norm1/norm2/norm eps 1e-6; adapters eps 1e-5).
+ *      Input rows r -> (r / rpb) * rstride + roff + r % rpb (rpb = 0: identity) of X (f32).    */
+int ivit_layernorm_fwd(const float* X, long ldx, long rpb, long rstride, long roff, long M, long D,
+                       const float* gamma, const float* beta, float eps, void* Y, long ldy, int y_dtype,
+                       float* mean, float* rstd, void* stream);
+/* dX(f32) = dres + LN_bwd(dY);  dXs = dtype(dX * row_scale[m / rows_per_scale]) if non-null;
+ * dgamma/dbeta (+)= column sums. work >= ivit_layernorm_bwd_workspace(M, D). dX may alias dres.
+ * X, dres and dX use the row map; dY (lddy) and dXs ([M, D] contiguous) use plain rows.      */
+long ivit_layernorm_bwd_workspace(long M, long D);
+int ivit_layernorm_bwd(const float* X, long ldx, long rpb, long rstride, long roff, long M, long D,
+                       const float* gamma, const float* mean, const float* rstd, const void* dY, long lddy,
+                       int dy_dtype, const float* dres, float* dX, long lddx, void* dXs, int dxs_dtype,
+                       const float* row_scale, long rows_per_scale, float* dgamma, float* dbeta, int accumulate,
+                       void* work, long work_bytes, void* stream);
+
+/* ---- BatchNorm2d (train: batch statistics, biased var for normalisation, unbiased for the
+ *      running update, momentum 0.1, eps 1e-5) on NHWC [M, C] maps (model_vit.py:24-31). */
+long ivit_bn_workspace(long M, long C);
+int ivit_bn_stats(const void* X, int x_dtype, long M, long C, float* mean, float* invstd, float* run_mean,
+                  float* run_var, float momentum, float eps, void* work, long work_bytes, void* stream);
+/* Y = [relu]( (X - mean) * invstd * g + b  [+ R] ), Y/R in y_dtype. */
+int ivit_bn_apply(const void* X, int x_dtype, long M, long C, const float* mean, const float* invstd,
+                  const float* g, const float* b, const void* R, int relu, void* Y, int y_dtype, void* stream);
+/* Backward of Y = relu?(BN(X) + R): dYin masked by (Y > 0) if relu; dR = masked dY;
+ * dX = invstd*g*(dy - mean(dy) - xhat*mean(dy*xhat)); dg, db (+)= sums. */
+int ivit_bn_bwd(const void* X, int x_dtype, const void* Y, int y_dtype, const void* dY, int dy_dtype, long M, long C,
+                const float* mean, const float* invstd, const float* g, int relu, void* dX, int dx_dtype, void* dR,
+                float* dg, float* db, int accumulate, void* work, long work_bytes, void* stream);
+
+/* ---- Small kernels: casts, column sums, token scatter, AdamW ---------------------------- */
+int ivit_cast(const void* x, int x_dtype, void* y, int y_dtype, long n, void* stream);
+/* out = (a [+ b]) [* gelu'(pre)] [* row_scale[i / (cols * rows_per_scale)]] elementwise over n values. */
+int ivit_add_act_grad(const void* a, int a_dtype, const void* b, int b_dtype, const void* pre, int pre_dtype,
+                      const float* row_scale, long row_elems, void* out, int out_dtype, long n, void* stream);
+int ivit_colsum(const void* X, int x_dtype, long ld, long rpb, long rstride, long roff, long M, long N, float* out,
+                int accumulate, void* work, long work_bytes, void* stream);
+long ivit_colsum_workspace(long M, long N);
+/* Adapter output tokens [B*Np, C] -> slice [.., coff:coff+C] of an NHWC map with ld channels. */
+int ivit_copy_cols(const void* src, long lds, void* dst, long ldd, long rows, long cols, int dtype, void* stream);
+/* Head output [M, ldh] (det A*7 cols, then intent A*K cols) -> cls [M*A], box [M*A, 6], intent [M*A, K]. */
+int ivit_split_heads(const float* h, long ldh, long M, long A, long K, float* cls, float* box, float* intent,
+                     void* stream);
+int ivit_merge_heads_grad(const float* dcls, const float* dbox, const float* dint, long M, long A, long K,
+                          void* dh, long ldh, int dh_dtype, void* stream);
+/* torch.optim.AdamW (foreach semantics) over n_tensors tensors given by device pointer tables. */
+int ivit_adamw(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
+               void* const* exp_avg_sq, const long* sizes, long max_size, float lr, float beta1, float beta2,
+               float eps, float weight_decay, float bc1, float bc2_sqrt, void* stream);
+
+/* ---- Detection / intention loss (loss.py:58-206): assignment + focal + Smooth-L1 + CE. ----- */
+/* gt: [B, Gmax, 5] f32 padded, ngt[B] int32, gint[B, Gmax] int32. keep: [B, NA] f32 0/1 (dominant
+ * intent keep mask) or null. stats (f32[8]): focal_sum, box_sum, ce_sum, num_pos, keep_sum, loss,
+ * cls_loss, box_loss, intent_loss (written). Per-anchor targets go to tgt (int32 [B, NA]). */
+long ivit_det_loss_workspace(long B, long NA, long Gmax);
+int ivit_det_loss_fwd(const float* cls, const float* box, const float* intent, const float* anchors, long B,
+                      long NA, long K, const float* gt, const int* ngt, const int* gint, long Gmax,
+                      const float* keep, unsigned dominant_mask, int downsampling, const float* class_w,
+                      float pos_thr, float neg_thr, float alpha, float gamma, float beta, float w_cls,
+                      float w_box, float w_int, int use_rotated, float* stats, void* work, long work_bytes,
+                      void* stream);
+int ivit_det_loss_bwd(const float* cls, const float* box, const float* intent, long B, long NA, long K,
+                      const float* keep, unsigned dominant_mask, int downsampling, const float* class_w,
+                      float alpha, float gamma, float beta, float w_cls, float w_box, float w_int,
+                      const float* stats, const float* grad_loss, float* dcls, float* dbox, float* dintent,
+                      void* work, long work_bytes, void* stream);
+
+/* ---- Geometry (utils.py) ----------------------------------------------------------------- */
+int ivit_generate_anchors(long bev_h, long bev_w, long stride, const float* cfgs, long A, float voxel, float off_x,
+                          float off_y, float* out, void* stream);
+int ivit_axis_iou(const float* b1, long n1, const float* b2, long n2, float* out, void* stream);
+int ivit_rotated_iou(const float* b1, long n1, const float* b2, long n2, float* out, void* stream);
+int ivit_decode_boxes(const float* rel, const float* anchors, const long* idx, long n, float* out, void* stream);
+/* torchvision CPU nms semantics, bit-exact: keep (int64, score order), count (int64[1]). */
+long ivit_nms_workspace(long n);
+int ivit_nms(const float* boxes_xywha, const float* scores, long n, double iou_thr, long* keep, long* count,
+             void* work, long work_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IVIT_H */

@@ -1,0 +1,196 @@
+"""End-to-end parity of the HIP IntentNetViT (the product path) against the golden vectors
+from the reference's own code and against the CPU oracle. f32 path: within 1e-3 rel
+(north_star); bf16 path: bf16-appropriate tolerances; NMS indices bit-exact."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle import ivit_oracle as O
+from oracle.weights import make_state_dict, model_cfg
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model(cfg, cd=torch.float32, dp=0.0):
+    import model_vit
+    m = model_vit.IntentNetViT(backbone_cfg={"img_size": tuple(cfg["img_size"]), "drop_path_rate_lidar": dp,
+                                             "drop_path_rate_map": dp})
+    m.load_state_dict(make_state_dict(cfg, seed=0), strict=True)
+    return m.to(DEV).set_compute_dtype(cd)
+
+
+def _rel(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+def _gts(z, n):
+    return [{"boxes_xywha": torch.from_numpy(z[f"gt{i}_boxes"]), "intentions": torch.from_numpy(z[f"gt{i}_ints"])}
+            for i in range(n)]
+
+
+@pytest.fixture(scope="module")
+def small():
+    z = golden("model_small.npz")
+    cfg = json.loads(str(z["cfg"]))
+    cfg["img_size"] = tuple(cfg["img_size"])
+    lidar, mp, _ = O.synthetic_batch(2, cfg["img_size"], seed=1234)
+    return z, cfg, lidar, mp
+
+
+def test_small_eval_vs_golden(small):
+    z, cfg, lidar, mp = small
+    m = _model(cfg).eval()
+    with torch.no_grad():
+        c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    assert _rel(c, z["eval_cls"]) < 1e-3 and _rel(b, z["eval_box"]) < 1e-3 and _rel(i, z["eval_int"]) < 1e-3
+
+
+def test_small_train_loss_grads_vs_golden(small):
+    import loss as L
+    import utils
+    z, cfg, lidar, mp = small
+    m = _model(cfg).train()
+    c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    assert _rel(c.detach(), z["train_cls"]) < 1e-3
+    anchors = utils.generate_anchors(*cfg["img_size"], 8)
+    assert np.array_equal(anchors.cpu().numpy(), z["anchors"])
+    lf = L.DetectionIntentionLoss(apply_intention_downsampling=False)
+    d = lf(c, b, i, anchors, _gts(z, 2))
+    got = [float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]),
+           float(d["num_pos_anchors"])]
+    np.testing.assert_allclose(got, z["train_loss"], rtol=1e-3)
+    d["loss"].backward()
+    sd = dict(m.named_parameters())
+    for name, gas, smp, st in zip(z["grad_names"], z["grad_abssum"], z["grad_samples"], z["grad_strides"]):
+        g = sd[str(name)].grad
+        assert g is not None, name
+        assert float(g.double().abs().sum()) == pytest.approx(gas, rel=1e-3, abs=1e-6), name
+        s = g.reshape(-1).double()[:: int(st)][:64].cpu().numpy()
+        ref = smp[~np.isnan(smp)][: s.size]
+        assert np.abs(s - ref).max() <= 1e-3 * max(np.abs(ref).max(), 1e-6) + 1e-7, name
+    bufs = dict(m.named_buffers())
+    for name, val in zip(z["bn_names"], z["bn_values"]):
+        np.testing.assert_allclose(bufs[str(name)].cpu().numpy(), val, rtol=1e-4, atol=1e-5)
+
+
+def test_loss_full_size_vs_golden():
+    import loss as L
+    import utils
+    z = golden("geometry.npz")
+    anchors = utils.generate_anchors(400, 720, 8)
+    g = torch.Generator().manual_seed(int(z["logits_seed"][0]))
+    NA = anchors.shape[0]
+    cls = torch.randn((2, NA, 1), generator=g)
+    box = 0.5 * torch.randn((2, NA, 6), generator=g)
+    it = torch.randn((2, NA, 8), generator=g)
+    gts = _gts(z, 2)
+    d = L.DetectionIntentionLoss(apply_intention_downsampling=False)(cls.to(DEV), box.to(DEV), it.to(DEV), anchors,
+                                                                      gts)
+    got = [float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]),
+           float(d["num_pos_anchors"])]
+    np.testing.assert_allclose(got, z["loss_full"], rtol=2e-5)
+    empty = [{"boxes_xywha": torch.zeros((0, 5)), "intentions": torch.zeros((0,), dtype=torch.long)}, {}]
+    d = L.DetectionIntentionLoss(apply_intention_downsampling=False)(cls.to(DEV), box.to(DEV), it.to(DEV), anchors,
+                                                                      empty)
+    got = [float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]),
+           float(d["num_pos_anchors"])]
+    np.testing.assert_allclose(got, z["loss_empty"], rtol=2e-5)
+
+
+@pytest.mark.parametrize("downsampling", [False, True])
+def test_loss_grads_vs_oracle(downsampling):
+    import loss as L
+    import utils
+    z = golden("geometry.npz")
+    anchors = utils.generate_anchors(400, 720, 8)
+    NA = anchors.shape[0]
+    g = torch.Generator().manual_seed(21)
+    cls = torch.randn((2, NA, 1), generator=g)
+    box = 0.5 * torch.randn((2, NA, 6), generator=g)
+    it = torch.randn((2, NA, 8), generator=g)
+    keep = (torch.rand((2, NA), generator=g) < 0.15).float()
+    gts = _gts(z, 2)
+    ts = [t.clone().to(DEV).requires_grad_(True) for t in (cls, box, it)]
+    d = L.DetectionIntentionLoss(apply_intention_downsampling=downsampling)(*ts, anchors, gts, intent_keep=keep)
+    d["loss"].backward()
+    rs = [t.clone().double().requires_grad_(True) for t in (cls, box, it)]
+    ref = O.detection_loss(*rs, anchors.cpu().double(), [{k: v.double() if v.is_floating_point() else v
+                                                          for k, v in gg.items()} for gg in gts],
+                           downsampling=downsampling, keep=keep)
+    ref["loss"].backward()
+    assert float(d["loss"]) == pytest.approx(float(ref["loss"]), rel=1e-5)
+    for a, r in zip(ts, rs):
+        assert _rel(a.grad, r.grad) < 1e-4
+
+
+def test_medium_grid_fp32_vs_oracle():
+    """80x120 grid (N=151 tokens: attention tails, 2 q-blocks) — HIP f32 vs CPU oracle, fwd + grads."""
+    cfg = model_cfg(img_size=(80, 120))
+    lidar, mp, gts = O.synthetic_batch(2, (80, 120), seed=5, box_region=(35.0, 60.0, -72.0, -48.0))
+    m = _model(cfg).train()
+    c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v.clone())
+          for k, v in make_state_dict(cfg, seed=0).items()}
+    rc, rb, ri = O.intentnet_forward(sd, lidar, mp, cfg, training=True)
+    assert _rel(c.detach(), rc.detach()) < 1e-3 and _rel(i.detach(), ri.detach()) < 1e-3
+    g = torch.Generator().manual_seed(9)
+    wc, wb, wi = torch.randn(rc.shape, generator=g), torch.randn(rb.shape, generator=g), torch.randn(ri.shape, generator=g)
+    ((c * wc.to(DEV)).sum() + (b * wb.to(DEV)).sum() + (i * wi.to(DEV)).sum()).backward()
+    ((rc * wc).sum() + (rb * wb).sum() + (ri * wi).sum()).backward()
+    params = dict(m.named_parameters())
+    worst = 0.0
+    for k, p in params.items():
+        r = _rel(p.grad, sd[k].grad)
+        worst = max(worst, r)
+        assert r < 1e-3, (k, r)
+
+
+def test_bf16_path_close_to_fp32(small):
+    z, cfg, lidar, mp = small
+    m32 = _model(cfg).eval()
+    m16 = _model(cfg, torch.bfloat16).eval()
+    with torch.no_grad():
+        a = m32(lidar.to(DEV), mp.to(DEV))
+        b = m16(lidar.to(DEV), mp.to(DEV))
+    for x, y in zip(a, b):
+        assert _rel(y, x) < 6e-2
+
+
+def test_full_grid_bf16_train_step_finite():
+    """constants.py grid, B=2, bf16 forward + loss + backward + fused AdamW: finite, parameters move."""
+    import loss as L
+    import utils
+    from optim import FusedAdamW
+    cfg = model_cfg()
+    m = _model(cfg, torch.bfloat16, dp=0.1).train()
+    lidar, mp, gts = O.synthetic_batch(2, seed=1234)
+    anchors = utils.generate_anchors()
+    opt = FusedAdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    lf = L.DetectionIntentionLoss()
+    w0 = m.det_head.conv.weight.detach().clone()
+    c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    d = lf(c, b, i, anchors, gts)
+    d["loss"].backward()
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(d["loss"]).item()
+    for n, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all().item(), n
+    assert not torch.equal(w0, m.det_head.conv.weight.detach())
+
+
+def test_full_grid_fp32_forward_vs_oracle():
+    cfg = model_cfg()
+    lidar, mp, _ = O.synthetic_batch(1, seed=1234)
+    m = _model(cfg).eval()
+    with torch.no_grad():
+        c, b, i = m(lidar.to(DEV), mp.to(DEV))
+        sd = make_state_dict(cfg, seed=0)
+        rc, rb, ri = O.intentnet_forward(sd, lidar, mp, cfg, training=False)
+    assert _rel(c, rc) < 1e-3 and _rel(b, rb) < 1e-3 and _rel(i, ri) < 1e-3

@@ -1,0 +1,248 @@
+"""Per-kernel parity on the MI355X: each HIP op (through the C ABI) against a CPU f64/f32
+reference of the same op. f32 path: rel 1e-5-ish (exact-f32 MFMA); bf16 path: bf16 tolerance."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+def _lin_case(M, N, K, dtype):
+    x = torch.randn(M, K)
+    w = torch.randn(N, K) / math.sqrt(K)
+    b = torch.randn(N) * 0.1
+    return x, w, b
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 200, 136), (1000, 1152, 384), (77, 64, 1536)])
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_linear_fwd_dgrad_wgrad(M, N, K, cd):
+    import ops
+    from _lib import ACT_GELU, BF16, F32
+    cdt = BF16 if cd == torch.bfloat16 else F32
+    x, w, b = _lin_case(M, N, K, cd)
+    xd, wd, bd = ops.cast(x.to(DEV), cd), ops.cast(w.to(DEV), cd), b.to(DEV)
+    ref = x.double() @ w.double().T + b.double()
+    y, _ = ops.linear_fwd(xd, wd, bd, cdt, out_dtype=torch.float32)
+    tol = 1e-5 if cdt == F32 else 2e-2
+    assert _rel(y, ref) < tol
+    a, pre = ops.linear_fwd(xd, wd, bd, cdt, act=ACT_GELU, want_pre=True)
+    assert _rel(pre.float(), ref) < tol
+    assert _rel(a.float(), F.gelu(ref)) < max(tol, 1e-5) * 2
+    r = torch.randn(M, N).to(DEV)
+    s = torch.tensor([0.5, 2.0]).to(DEV)
+    yr, _ = ops.linear_fwd(xd, wd, bd, cdt, resid=r, row_scale=s, rps=(M + 1) // 2)
+    sc = torch.where(torch.arange(M) < (M + 1) // 2, 0.5, 2.0).double()[:, None]
+    assert _rel(yr, r.cpu().double() + sc * ref) < tol
+    dy = torch.randn(M, N)
+    dyd = ops.cast(dy.to(DEV), cd)
+    dx = ops.linear_dgrad(dyd, wd, cdt, torch.float32)
+    assert _rel(dx, dy.double() @ w.double()) < tol
+    dxg = ops.linear_dgrad(dyd, wd, cdt, torch.float32, gelu_pre=ops.cast(pre, cd) if cd == torch.float32 else pre)
+    hp = pre.float().cpu().double().requires_grad_(True)
+    F.gelu(hp).backward(dy.double() @ w.double())
+    assert _rel(dxg, hp.grad) < tol * 2
+    dw, db = ops.linear_wgrad(dyd, xd, cdt)
+    assert _rel(dw, dy.double().T @ x.double()) < tol
+    assert _rel(db, dy.double().sum(0)) < tol
+
+
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_layernorm(cd):
+    import ops
+    M, D = 513, 384
+    x = torch.randn(M, D) * 2 + 0.5
+    g, b = 1 + 0.1 * torch.randn(D), 0.1 * torch.randn(D)
+    y, m, r = ops.layernorm_fwd(x.to(DEV), g.to(DEV), b.to(DEV), 1e-6, cd)
+    xr = x.double().requires_grad_(True)
+    gr, br = g.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = F.layer_norm(xr, (D,), gr, br, 1e-6)
+    assert _rel(y.float(), ref.detach()) < (2e-6 if cd == torch.float32 else 1e-2)
+    dy = torch.randn(M, D)
+    dres = torch.randn(M, D)
+    ref.backward(dy.double())
+    s = torch.tensor([0.5]).to(DEV)
+    dx, dxs, dg, dbb = ops.layernorm_bwd(x.to(DEV), g.to(DEV), m, r, dy.to(DEV), dres=dres.to(DEV).clone(),
+                                         xs_dtype=cd, row_scale=s, rps=M)
+    assert _rel(dx, xr.grad + dres.double()) < 1e-5
+    assert _rel(dxs.float(), 0.5 * (xr.grad + dres.double())) < (1e-5 if cd == torch.float32 else 1e-2)
+    assert _rel(dg, gr.grad) < 1e-5 and _rel(dbb, br.grad) < 1e-5
+
+
+def _attn_ref(qkv, B, N, H):
+    q, k, v = qkv.double().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-1, -2)) / 8.0
+    p = torch.softmax(s, -1)
+    return (p @ v).transpose(1, 2).reshape(B * N, H * 64), torch.logsumexp(s, -1)
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 257, 2), (1, 4501, 6), (1, 64, 1)])
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_attention(B, N, H, cd):
+    import ops
+    from _lib import BF16, F32
+    cdt = BF16 if cd == torch.bfloat16 else F32
+    qkv = torch.randn(B * N, 3 * H * 64)
+    q = ops.cast(qkv.to(DEV), cd)
+    o, lse = ops.attn_fwd(q, B, N, H, cdt)
+    qr = q.float().cpu().double().requires_grad_(True)
+    oref, lref = _attn_ref(qr, B, N, H)
+    tol = 1e-5 if cdt == F32 else 2e-2
+    assert _rel(o.float(), oref.detach()) < tol
+    assert _rel(lse, lref.detach()) < 1e-5
+    do = torch.randn(B * N, H * 64)
+    dod = ops.cast(do.to(DEV), cd)
+    oref.backward(dod.float().cpu().double())
+    dq = ops.attn_bwd(q, o, dod, lse, B, N, H, cdt)
+    g = qr.grad.reshape(B * N, 3, H * 64)
+    d = dq.float().cpu().reshape(B * N, 3, H * 64)
+    for i in range(3):
+        assert _rel(d[:, i], g[:, i]) < (1e-4 if cdt == F32 else 3e-2), ("qkv"[i], _rel(d[:, i], g[:, i]))
+
+
+@pytest.mark.parametrize("k", [1, 3])
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_conv_nhwc(k, cd):
+    import ops
+    from _lib import BF16, F32
+    cdt = BF16 if cd == torch.bfloat16 else F32
+    B, H, W, Cin, Cout = 2, 7, 9, 48, 40
+    x = torch.randn(B, Cin, H, W)
+    w = torch.randn(Cout, Cin, k, k) / math.sqrt(Cin * k * k)
+    bias = torch.randn(Cout) * 0.1
+    xh = ops.cast(x.permute(0, 2, 3, 1).reshape(-1, Cin).contiguous().to(DEV), cd)
+    wp = ops.pack_conv(w.to(DEV), cdt)
+    y = ops.conv_fwd(xh, B, H, W, wp, bias.to(DEV), cdt, torch.float32)
+    xr = xh.float().cpu().reshape(B, H, W, Cin).permute(0, 3, 1, 2).double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    ref = F.conv2d(xr, wr, bias.double(), padding=k // 2)
+    tol = 1e-5 if cdt == F32 else 2e-2
+    assert _rel(y.reshape(B, H, W, Cout).permute(0, 3, 1, 2), ref.detach()) < tol
+    dy = torch.randn(B, Cout, H, W)
+    dyh = ops.cast(dy.permute(0, 2, 3, 1).reshape(-1, Cout).contiguous().to(DEV), cd)
+    ref.backward(dyh.float().cpu().reshape(B, H, W, Cout).permute(0, 3, 1, 2).double())
+    dx = ops.conv_dgrad(dyh, B, H, W, wp, cdt, torch.float32)
+    assert _rel(dx.reshape(B, H, W, Cin).permute(0, 3, 1, 2), xr.grad) < tol
+    gp, db = ops.conv_wgrad(dyh, xh, B, H, W, Cin, Cout, k, cdt, want_bias=True)
+    assert _rel(ops.unpack_conv_grad(gp, Cout, Cin, k), wr.grad) < tol
+    assert _rel(db, dyh.float().cpu().double().sum(0)) < tol
+
+
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_patch_embed(cd):
+    import ops
+    from _lib import BF16, F32
+    cdt = BF16 if cd == torch.bfloat16 else F32
+    B, C, H, W, D = 2, 20, 32, 48, 64
+    img = torch.rand(B, C, H, W)
+    w = torch.randn(D, C, 8, 8) / math.sqrt(C * 64)
+    b, pos, cls = 0.1 * torch.randn(D), 0.02 * torch.randn(1, 25, D), 0.02 * torch.randn(1, 1, D)
+    params = [t.to(DEV).requires_grad_(True) for t in (w, b, pos, cls)]
+    out = ops.PatchEmbedFn.apply(img.to(DEV), *params, cdt)
+    wr, br, pr, cr = [t.double().requires_grad_(True) for t in (w, b, pos, cls)]
+    t = F.conv2d(img.double(), wr, br, stride=8).flatten(2).transpose(1, 2)
+    ref = torch.cat([cr.expand(B, -1, -1), t], 1) + pr
+    tol = 1e-5 if cdt == F32 else 2e-2
+    assert _rel(out.reshape(B, 25, D), ref.detach()) < tol
+    g = torch.randn(B, 25, D)
+    out.backward(g.reshape(B * 25, D).to(DEV))
+    ref.backward(g.double())
+    for p, r in zip(params, (wr, br, pr, cr)):
+        assert _rel(p.grad, r.grad) < tol
+
+
+def test_batchnorm_train():
+    import ops
+    M, C = 1000, 96
+    x = torch.randn(M, C) * 3 + 1
+    g, b = 1 + 0.1 * torch.randn(C), 0.1 * torch.randn(C)
+    rm, rv = torch.zeros(C), torch.ones(C)
+    rmd, rvd = rm.to(DEV).clone(), rv.to(DEV).clone()
+    res = torch.randn(M, C)
+    st = ops.bn_forward(x.to(DEV), g.to(DEV), b.to(DEV), rmd, rvd, True)
+    y = ops.bn_apply(x.to(DEV), st, g.to(DEV), b.to(DEV), torch.float32, resid=res.to(DEV), relu=True)
+    xr = x.double().requires_grad_(True)
+    gr, br = g.double().requires_grad_(True), b.double().requires_grad_(True)
+    rr = res.double().requires_grad_(True)
+    rm2, rv2 = rm.double().clone(), rv.double().clone()
+    ref = F.relu(F.batch_norm(xr, rm2, rv2, gr, br, training=True) + rr)
+    assert _rel(y, ref.detach()) < 1e-5
+    assert _rel(rmd, rm2) < 1e-5 and _rel(rvd, rv2) < 1e-5
+    dy = torch.randn(M, C)
+    ref.backward(dy.double())
+    dx, dr, dg, db = ops.bn_backward(x.to(DEV), y, dy.to(DEV), st, g.to(DEV), True, torch.float32, want_dr=True)
+    assert _rel(dx, xr.grad) < 1e-4 and _rel(dr, rr.grad) < 1e-5
+    assert _rel(dg, gr.grad) < 1e-4 and _rel(db, br.grad) < 1e-5
+
+
+def test_adamw_matches_torch():
+    from optim import FusedAdamW
+    ps = [torch.randn(1000), torch.randn(37, 5)]
+    gs = [[torch.randn_like(p) for p in ps] for _ in range(3)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    dev = [p.clone().to(DEV).requires_grad_(True) for p in ps]
+    o1 = torch.optim.AdamW(ref, lr=1e-3, weight_decay=1e-2)
+    o2 = FusedAdamW(dev, lr=1e-3, weight_decay=1e-2)
+    for step in gs:
+        for p, q, g in zip(ref, dev, step):
+            p.grad = g.clone()
+            q.grad = g.clone().to(DEV)
+        o1.step()
+        o2.step()
+    for p, q in zip(ref, dev):
+        assert _rel(q.detach(), p.detach()) < 1e-6
+
+
+def test_geometry_golden():
+    from conftest import golden
+    import utils
+    z = golden("geometry.npz")
+    a = utils.generate_anchors(400, 720, 8)
+    assert np.array_equal(a.cpu().numpy(), z["anchors"])
+    out = utils.decode_box_predictions(torch.from_numpy(z["dec_rel"]).to(DEV),
+                                       a[torch.from_numpy(z["dec_idx"]).to(DEV)])
+    np.testing.assert_allclose(out.cpu().numpy(), z["dec_out"], rtol=1e-6, atol=1e-6)
+    r = utils.compute_rotated_iou(torch.from_numpy(z["rot_b1"]).to(DEV), torch.from_numpy(z["rot_b2"]).to(DEV))
+    np.testing.assert_allclose(r.cpu().numpy(), z["rot_iou"], atol=1e-6)
+    gt0 = torch.from_numpy(z["gt0_boxes"]).to(DEV)
+    iou = utils.compute_axis_aligned_iou(a, gt0)
+    mx, arg = iou.max(dim=1)
+    assert np.array_equal(mx.cpu().numpy(), z["iou_max"])
+
+
+def test_nms_bitexact_golden():
+    from conftest import golden
+    import utils
+    z = golden("geometry.npz")
+    for i in range(int(z["nms_cases"][0])):
+        keep = utils.apply_nms(torch.from_numpy(z[f"nms{i}_boxes"]).to(DEV), torch.from_numpy(z[f"nms{i}_scores"]).to(DEV),
+                               0.2)
+        assert np.array_equal(keep.cpu().numpy(), z[f"nms{i}_keep"]), i
+
+
+def test_nms_random_vs_oracle():
+    from oracle import ivit_oracle as O
+    import utils
+    g = torch.Generator().manual_seed(3)
+    for n in (1, 63, 64, 65, 500, 4097):
+        b = torch.stack([10 * torch.rand(n, generator=g), 10 * torch.rand(n, generator=g),
+                         0.5 + 2 * torch.rand(n, generator=g), 0.5 + 2 * torch.rand(n, generator=g),
+                         torch.zeros(n)], 1)
+        s = torch.round(torch.rand(n, generator=g) * 8) / 8
+        keep = utils.apply_nms(b.to(DEV), s.to(DEV), 0.2).cpu().numpy()
+        assert np.array_equal(keep, O.nms_numpy(b.numpy(), s.numpy(), 0.2)), n

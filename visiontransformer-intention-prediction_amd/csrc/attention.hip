@@ -1,0 +1,565 @@
+// Multi-head self-attention core (timm Attention -> F.scaled_dot_product_attention,
+// reached from model_vit.py:64,71,119): O = softmax(Q K^T * Dh^-0.5) V per (batch, head).
+//
+// bf16 path: flash-style kernels, never materialising N x N.
+//   forward : S^T = K Q^T (keys in registers, query on the lane) so the online-softmax
+//             max/sum of a query are lane-local (+1 cross-half swap); O^T += V^T P^T takes
+//             P^T straight from the S^T accumulator (no LDS round trip) and V^T by the
+//             CDNA4 transposing LDS read.
+//   backward: dQ kernel (query block, sweep keys) and dK/dV kernel (key block, sweep
+//             queries); both recompute P from the saved LSE. No atomics.
+// f32 path (parity): exact-f32 MFMA GEMMs through the generic engine with the score
+//             matrix materialised in the workspace, plus row-softmax kernels.
+#include "gemm_engine.h"
+
+using namespace ivit;
+
+namespace {
+
+constexpr int AQ = 128;  // queries per workgroup (4 waves x 32)
+constexpr int AK = 64;   // keys per tile
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float NEG_BIG = -1.0e30f;
+
+// tile image: 64 rows x 64 bf16 (128-B rows), chunk swizzle swz128 (see gemm_engine.h)
+IVIT_DEV int t_off(int r, int c) { return r * 128 + ((c ^ swz128(r)) << 4); }
+
+// Load a 64 x 64 bf16 tile (rows r0.., cols c0.. of a row-major matrix with row stride ld)
+// into registers: 512 16-B chunks, 2 per thread. Rows >= nrows are zero.
+IVIT_DEV void tile_gload(const bf16* base, long ld, int r0, int nrows, int tid, uint4 (&r)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = tid + 256 * i, row = idx >> 3, ch = idx & 7;
+    r[i] = (r0 + row < nrows) ? *(const uint4*)(base + (long)(r0 + row) * ld + ch * 8) : make_uint4(0, 0, 0, 0);
+  }
+}
+IVIT_DEV void tile_sstore(char* img, int tid, const uint4 (&r)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = tid + 256 * i;
+    *(uint4*)(img + t_off(idx >> 3, idx & 7)) = r[i];
+  }
+}
+
+// 32x32x16 operand from a [row = reduction index][col] tile image by transposing reads,
+// with the k order an f32 32x32 accumulator uses when fed back as an operand
+// (element j of lane-half h <-> reduction row rb + 8(j>>2) + 4h + (j&3); cdna_hip_programming.md §3).
+IVIT_DEV bf16x8 tr_acc_order(const char* img, int rb, int colbase, int lane) {
+  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = colbase + 16 * (G & 1) + 4 * p;
+  const int r0 = rb + 4 * (G >> 1) + q;
+  const int c = col >> 3, e = (col & 7) * 2;
+  union { s16x4 s[2]; bf16x8 v; } u;
+  u.s[0] = ds_tr(img + t_off(r0, c) + e);
+  u.s[1] = ds_tr(img + t_off(r0 + 8, c) + e);
+  return u.v;
+}
+
+// Pack accumulator registers 8s..8s+7 (f32) into a bf16x8 operand.
+IVIT_DEV bf16x8 pack_acc(const f32x16& a, int s) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (bf16)a[8 * s + j];
+  return v;
+}
+
+// Register operand: lane l holds row (l&31), k = 16s + 8(l>>5) .. +7 of a 64-wide row.
+IVIT_DEV void load_row_frags(const bf16* rowp, bool valid, int lane, bf16x8 (&f)[4]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    Pack8 p;
+    p.u = valid ? *(const uint4*)(rowp + 16 * s + 8 * (lane >> 5)) : make_uint4(0, 0, 0, 0);
+    f[s] = p.v;
+  }
+}
+
+IVIT_DEV f32x16 zero16() {
+  f32x16 a;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) a[r] = 0.f;
+  return a;
+}
+
+// ------------------------------------------------------------------------- forward (bf16)
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16* __restrict__ qkv, int N, int H,
+                                                               bf16* __restrict__ out, float* __restrict__ lse,
+                                                               float c2) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int q = blockIdx.x * AQ + wv * 32 + (lane & 31);
+
+  bf16x8 qf[4];
+  load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
+
+  f32x16 o0 = zero16(), o1 = zero16();
+  float m = NEG_BIG, l = 0.f;
+  const int nt = (N + AK - 1) / AK;
+  uint4 rk[2], rv[2];
+  tile_gload(Kb, ld, 0, N, tid, rk);
+  tile_gload(Vb, ld, 0, N, tid, rv);
+  tile_sstore(smem[0][0], tid, rk);
+  tile_sstore(smem[0][1], tid, rv);
+  __syncthreads();
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) {
+      tile_gload(Kb, ld, (kt + 1) * AK, N, tid, rk);
+      tile_gload(Vb, ld, (kt + 1) * AK, N, tid, rv);
+    }
+    const char* kimg = smem[cur][0];
+    const char* vimg = smem[cur][1];
+    f32x16 s[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      s[t] = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+        s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s[t], 0, 0, 0);
+      }
+    }
+    // scale into the log2 domain, mask keys >= N, row max over this tile
+    float mx = NEG_BIG;
+    const int kbase = kt * AK;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const float v = key < N ? s[t][r] * c2 : NEG_BIG;
+        s[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(s[t][r] - mn);
+        s[t][r] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = mn;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack_acc(s[t], ss);
+        const int rb = 32 * t + 16 * ss;
+        const bf16x8 va0 = tr_acc_order(vimg, rb, 0, lane);
+        const bf16x8 va1 = tr_acc_order(vimg, rb, 32, lane);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, pb, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, pb, o1, 0, 0, 0);
+      }
+    if (kt + 1 < nt) {
+      tile_sstore(smem[cur ^ 1][0], tid, rk);
+      tile_sstore(smem[cur ^ 1][1], tid, rv);
+    }
+    __syncthreads();
+  }
+  if (q < N) {
+    const float inv = 1.f / l;
+    bf16* orow = out + ((long)b * N + q) * D + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      Pack4 a, c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a.h[j] = (bf16)(o0[4 * g + j] * inv);
+        c.h[j] = (bf16)(o1[4 * g + j] * inv);
+      }
+      const int d = 8 * g + 4 * hl;  // rows (r&3) + 8(r>>2) + 4h of O^T
+      *(uint2*)(orow + d) = a.u;
+      *(uint2*)(orow + 32 + d) = c.u;
+    }
+    if (hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
+  }
+}
+
+// delta[z][q] = sum_d dO[q][d] O[q][d]   (one thread per (b, n, h) row of 64)
+template <typename T>
+__global__ void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__ dout, long B, int N, int H,
+                                  float* __restrict__ delta) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * N * H) return;
+  const int D = H * 64;
+  const long bn = i / H;
+  const int h = (int)(i - bn * H);
+  const T* a = o + bn * D + h * 64;
+  const T* g = dout + bn * D + h * 64;
+  float s = 0.f;
+#pragma unroll 8
+  for (int d = 0; d < 64; ++d) s += to_f32(a[d]) * to_f32(g[d]);
+  const long b = bn / N, n = bn - b * N;
+  delta[(b * H + h) * N + n] = s;
+}
+
+// ------------------------------------------------------------------------- dQ (bf16)
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16_kernel(const bf16* __restrict__ qkv,
+                                                                  const bf16* __restrict__ dout,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ delta, int N, int H,
+                                                                  bf16* __restrict__ dqkv, float c2, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int q = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  const bool qv = q < N;
+  bf16x8 qf[4], gf[4];
+  load_row_frags(Qb + (long)q * ld, qv, lane, qf);
+  load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
+  const float lse2 = qv ? lse[(long)z * N + q] * LOG2E : 1e30f;
+  const float dlt = qv ? delta[(long)z * N + q] : 0.f;
+
+  f32x16 a0 = zero16(), a1 = zero16();  // dQ[q][d]: col d, rows q
+  const int nt = (N + AK - 1) / AK;
+  uint4 rk[2], rv[2];
+  tile_gload(Kb, ld, 0, N, tid, rk);
+  tile_gload(Vb, ld, 0, N, tid, rv);
+  tile_sstore(smem[0][0], tid, rk);
+  tile_sstore(smem[0][1], tid, rv);
+  __syncthreads();
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) {
+      tile_gload(Kb, ld, (kt + 1) * AK, N, tid, rk);
+      tile_gload(Vb, ld, (kt + 1) * AK, N, tid, rv);
+    }
+    const char* kimg = smem[cur][0];
+    const char* vimg = smem[cur][1];
+    const int kbase = kt * AK;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 s = zero16(), dp = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+        const bf16x8 va = *(const bf16x8*)(vimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, gf[ks], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const float p = key < N ? exp2f(s[r] * c2 - lse2) : 0.f;
+        s[r] = p * (dp[r] - dlt);  // dS^T[key][q]
+      }
+      // dQ[q][d] += dS[q][key] K[key][d]  (X = dS^T as the A operand)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 xa = pack_acc(s, ss);
+        const int rb = 32 * t + 16 * ss;
+        const bf16x8 kb0 = tr_acc_order(kimg, rb, 0, lane);
+        const bf16x8 kb1 = tr_acc_order(kimg, rb, 32, lane);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, kb0, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, kb1, a1, 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nt) {
+      tile_sstore(smem[cur ^ 1][0], tid, rk);
+      tile_sstore(smem[cur ^ 1][1], tid, rv);
+    }
+    __syncthreads();
+  }
+  // a0/a1: rows = q within this wave's 32, col = d
+  const int qw = blockIdx.x * AQ + wv * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qq = qw + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    if (qq < N) {
+      bf16* row = dqkv + ((long)b * N + qq) * ld + h * 64;
+      row[lane & 31] = (bf16)(a0[r] * scale);
+      row[32 + (lane & 31)] = (bf16)(a1[r] * scale);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- dK, dV (bf16)
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* __restrict__ qkv,
+                                                                   const bf16* __restrict__ dout,
+                                                                   const float* __restrict__ lse,
+                                                                   const float* __restrict__ delta, int N, int H,
+                                                                   bf16* __restrict__ dqkv, float c2, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][Q|dO]
+  __shared__ float srow[2][2][AK];                                  // [stage][lse2|delta]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const bf16* Gb = dout + (long)b * N * D + h * 64;
+  const float* L = lse + (long)z * N;
+  const float* Dl = delta + (long)z * N;
+  const int key = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  bf16x8 kf[4], vf[4];
+  load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
+  load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
+
+  f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();  // [key][d]: col d, rows key
+  const int nt = (N + AK - 1) / AK;
+  uint4 rq[2], rg[2];
+  float rl = 0.f, rd = 0.f;
+  auto rows_load = [&](int q0) {
+    if (tid < AK) {
+      const int qq = q0 + tid;
+      rl = qq < N ? L[qq] * LOG2E : 1e30f;
+      rd = qq < N ? Dl[qq] : 0.f;
+    }
+  };
+  tile_gload(Qb, ld, 0, N, tid, rq);
+  tile_gload(Gb, D, 0, N, tid, rg);
+  rows_load(0);
+  tile_sstore(smem[0][0], tid, rq);
+  tile_sstore(smem[0][1], tid, rg);
+  if (tid < AK) { srow[0][0][tid] = rl; srow[0][1][tid] = rd; }
+  __syncthreads();
+  for (int qt = 0; qt < nt; ++qt) {
+    const int cur = qt & 1;
+    if (qt + 1 < nt) {
+      tile_gload(Qb, ld, (qt + 1) * AK, N, tid, rq);
+      tile_gload(Gb, D, (qt + 1) * AK, N, tid, rg);
+      rows_load((qt + 1) * AK);
+    }
+    const char* qimg = smem[cur][0];
+    const char* gimg = smem[cur][1];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x16 s = zero16(), dp = zero16();  // [q][key]: col key (lane), rows q
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 qa = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+        const bf16x8 ga = *(const bf16x8*)(gimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[ks], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int qi = 32 * t + 8 * g + 4 * hl;  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j
+        const float4 l4 = *(const float4*)&srow[cur][0][qi];
+        const float4 d4 = *(const float4*)&srow[cur][1][qi];
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = exp2f(s[4 * g + j] * c2 - lv[j]);
+          s[4 * g + j] = p;                               // P[q][key]
+          dp[4 * g + j] = p * (dp[4 * g + j] - dv[j]);    // dS[q][key]
+        }
+      }
+      // dV[key][d] += P^T dO ; dK[key][d] += dS^T Q   (X = P / dS as the A operand)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int rb = 32 * t + 16 * ss;
+        const bf16x8 pa = pack_acc(s, ss);
+        const bf16x8 g0 = tr_acc_order(gimg, rb, 0, lane);
+        const bf16x8 g1 = tr_acc_order(gimg, rb, 32, lane);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, g0, dv0, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, g1, dv1, 0, 0, 0);
+        const bf16x8 da = pack_acc(dp, ss);
+        const bf16x8 q0 = tr_acc_order(qimg, rb, 0, lane);
+        const bf16x8 q1 = tr_acc_order(qimg, rb, 32, lane);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, q0, dk0, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, q1, dk1, 0, 0, 0);
+      }
+    }
+    if (qt + 1 < nt) {
+      tile_sstore(smem[cur ^ 1][0], tid, rq);
+      tile_sstore(smem[cur ^ 1][1], tid, rg);
+      if (tid < AK) { srow[cur ^ 1][0][tid] = rl; srow[cur ^ 1][1][tid] = rd; }
+    }
+    __syncthreads();
+  }
+  const int kw = blockIdx.x * AQ + wv * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    if (kk < N) {
+      bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
+      row[D + (lane & 31)] = (bf16)(dk0[r] * scale);
+      row[D + 32 + (lane & 31)] = (bf16)(dk1[r] * scale);
+      row[2 * D + (lane & 31)] = (bf16)dv0[r];
+      row[2 * D + 32 + (lane & 31)] = (bf16)dv1[r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- f32 row kernels
+// S rows (already scaled) -> P = softmax, zero padding columns; lse = max + log(sum).
+__global__ void softmax_rows_kernel(float* __restrict__ S, long ldS, int N, float* __restrict__ lse) {
+  const long row = blockIdx.x;  // z * N + q
+  float* s = S + row * ldS;
+  __shared__ float red[4];
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < N; i += 256) mx = fmaxf(mx, s[i]);
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const float e = expf(s[i] - mx);
+    s[i] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  sum = red[0] + red[1] + red[2] + red[3];
+  const float inv = 1.f / sum;
+  for (int i = threadIdx.x; i < ldS; i += 256) s[i] = i < N ? s[i] * inv : 0.f;
+  if (threadIdx.x == 0) lse[row] = mx + logf(sum);
+}
+
+// P = exp(S - lse) (recompute in backward), zero padding.
+__global__ void prob_rows_kernel(float* __restrict__ S, long ldS, int N, const float* __restrict__ lse) {
+  const long row = blockIdx.x;
+  float* s = S + row * ldS;
+  const float l = lse[row];
+  for (int i = threadIdx.x; i < ldS; i += 256) s[i] = i < N ? expf(s[i] - l) : 0.f;
+}
+
+// dS = P * (dP - rowsum(P * dP)) in place of dP.
+__global__ void dsoftmax_rows_kernel(const float* __restrict__ P, float* __restrict__ dP, long ldS, int N) {
+  const long row = blockIdx.x;
+  const float* p = P + row * ldS;
+  float* g = dP + row * ldS;
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < N; i += 256) s += p[i] * g[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  s = red[0] + red[1] + red[2] + red[3];
+  for (int i = threadIdx.x; i < ldS; i += 256) g[i] = i < N ? p[i] * (g[i] - s) : 0.f;
+}
+
+long ld_scores(long N) { return (N + 7) / 8 * 8; }
+
+}  // namespace
+
+extern "C" long ivit_attn_workspace(int dtype, long B, long N, long H, long Dh, int backward) {
+  if (dtype == IVIT_BF16) return backward ? B * H * N * 4 : 0;
+  const long one = B * H * N * ld_scores(N) * 4;
+  return backward ? 2 * one : one;
+}
+
+extern "C" int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H, long Dh, void* out, float* lse,
+                             void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(Dh == 64, "ivit_attn_fwd: head dim must be 64 (got %ld)", Dh);
+  IVIT_CHECK_ARG(work_bytes >= ivit_attn_workspace(dtype, B, N, H, Dh, 0), "ivit_attn_fwd: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  const float scale = 1.0f / sqrtf((float)Dh);
+  if (B * N * H == 0) return 0;
+  if (dtype == IVIT_BF16) {
+    dim3 g(ivit_cdiv(N, AQ), B * H);
+    hipLaunchKernelGGL(attn_fwd_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H, (bf16*)out, lse,
+                       scale * LOG2E);
+    IVIT_LAUNCH_CHECK();
+    return 0;
+  }
+  const long D = H * Dh, ldq = 3 * D, ldS = ld_scores(N);
+  float* S = (float*)work;
+  const float* Q = (const float*)qkv;
+  // S = scale * Q K^T
+  LdDense<float> la{Q, ldq, (int)N, (int)Dh, 0, 0, 0, {H, N * ldq, Dh}};
+  LdDense<float> lb{Q + D, ldq, (int)N, (int)Dh, 0, 0, 0, {H, N * ldq, Dh}};
+  EpiStore<float> es{S, ldS, {1, N * ldS, 0}, nullptr, IVIT_ACT_NONE, nullptr, scale};
+  launch_gemm<true, true>(false, la, lb, es, (int)N, (int)N, (int)Dh, (int)(B * H), 1, st);
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3(B * H * N), dim3(256), 0, st, S, ldS, (int)N, lse);
+  // O = P V
+  LdDense<float> lp{S, ldS, (int)N, (int)ldS, 0, 0, 0, {1, N * ldS, 0}};
+  LdDense<float> lv{Q + 2 * D, ldq, (int)N, (int)Dh, 0, 0, 0, {H, N * ldq, Dh}};
+  EpiStore<float> eo{(float*)out, D, {H, N * D, Dh}, nullptr, IVIT_ACT_NONE, nullptr, 1.f};
+  launch_gemm<true, false>(false, lp, lv, eo, (int)N, (int)Dh, (int)ldS, (int)(B * H), 1, st);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse, long B,
+                             long N, long H, long Dh, void* dqkv, void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(Dh == 64, "ivit_attn_bwd: head dim must be 64 (got %ld)", Dh);
+  IVIT_CHECK_ARG(work_bytes >= ivit_attn_workspace(dtype, B, N, H, Dh, 1), "ivit_attn_bwd: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  const float scale = 1.0f / sqrtf((float)Dh);
+  if (B * N * H == 0) return 0;
+  const long D = H * Dh, ldq = 3 * D;
+  if (dtype == IVIT_BF16) {
+    float* delta = (float*)work;
+    hipLaunchKernelGGL(attn_delta_kernel<bf16>, dim3(ivit_cdiv(B * N * H, 256)), dim3(256), 0, st,
+                       (const bf16*)out, (const bf16*)dout, B, (int)N, (int)H, delta);
+    dim3 g(ivit_cdiv(N, AQ), B * H);
+    hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse, delta,
+                       (int)N, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    hipLaunchKernelGGL(attn_bwd_dkv_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse,
+                       delta, (int)N, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    IVIT_LAUNCH_CHECK();
+    return 0;
+  }
+  const long ldS = ld_scores(N), zs = N * ldS;
+  float* P = (float*)work;
+  float* dP = P + B * H * zs;
+  const float* Q = (const float*)qkv;
+  float* dq = (float*)dqkv;
+  const int Z = (int)(B * H);
+  const BatchOff qoff{H, N * ldq, Dh}, soff{1, zs, 0}, ooff{H, N * D, Dh};
+  // recompute P
+  {
+    LdDense<float> la{Q, ldq, (int)N, (int)Dh, 0, 0, 0, qoff};
+    LdDense<float> lb{Q + D, ldq, (int)N, (int)Dh, 0, 0, 0, qoff};
+    EpiStore<float> es{P, ldS, soff, nullptr, IVIT_ACT_NONE, nullptr, scale};
+    launch_gemm<true, true>(false, la, lb, es, (int)N, (int)N, (int)Dh, Z, 1, st);
+    hipLaunchKernelGGL(prob_rows_kernel, dim3(Z * N), dim3(256), 0, st, P, ldS, (int)N, lse);
+  }
+  // dV = P^T dO
+  {
+    LdDense<float> la{P, ldS, (int)N, (int)ldS, 0, 0, 0, soff};
+    LdDense<float> lb{(const float*)dout, D, (int)N, (int)Dh, 0, 0, 0, ooff};
+    EpiStore<float> e{dq + 2 * D, ldq, qoff, nullptr, IVIT_ACT_NONE, nullptr, 1.f};
+    launch_gemm<false, false>(false, la, lb, e, (int)N, (int)Dh, (int)N, Z, 1, st);
+  }
+  // dP = dO V^T ; dS
+  {
+    LdDense<float> la{(const float*)dout, D, (int)N, (int)Dh, 0, 0, 0, ooff};
+    LdDense<float> lb{Q + 2 * D, ldq, (int)N, (int)Dh, 0, 0, 0, qoff};
+    EpiStore<float> e{dP, ldS, soff, nullptr, IVIT_ACT_NONE, nullptr, 1.f};
+    launch_gemm<true, true>(false, la, lb, e, (int)N, (int)N, (int)Dh, Z, 1, st);
+    hipLaunchKernelGGL(dsoftmax_rows_kernel, dim3(Z * N), dim3(256), 0, st, P, dP, ldS, (int)N);
+  }
+  // dQ = scale * dS K ; dK = scale * dS^T Q
+  {
+    LdDense<float> la{dP, ldS, (int)N, (int)ldS, 0, 0, 0, soff};
+    LdDense<float> lb{Q + D, ldq, (int)N, (int)Dh, 0, 0, 0, qoff};
+    EpiStore<float> e{dq, ldq, qoff, nullptr, IVIT_ACT_NONE, nullptr, scale};
+    launch_gemm<true, false>(false, la, lb, e, (int)N, (int)Dh, (int)ldS, Z, 1, st);
+  }
+  {
+    LdDense<float> la{dP, ldS, (int)N, (int)ldS, 0, 0, 0, soff};
+    LdDense<float> lb{Q, ldq, (int)N, (int)Dh, 0, 0, 0, qoff};
+    EpiStore<float> e{dq + D, ldq, qoff, nullptr, IVIT_ACT_NONE, nullptr, scale};
+    launch_gemm<false, false>(false, la, lb, e, (int)N, (int)Dh, (int)N, Z, 1, st);
+  }
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,158 @@
+// Small bandwidth-bound kernels: dtype casts, column-slice copies, the head output split
+// (heads.py:18-25,39-43 view/permute + model_vit.py:181-184 reshape) and fused AdamW
+// (torch.optim.AdamW as used at train_vit.py:130).
+#include "ivit_common.h"
+
+namespace {
+
+IVIT_DEV float ldv(const void* p, int dt, long i) {
+  return dt == IVIT_BF16 ? bf2f(((const bf16*)p)[i]) : ((const float*)p)[i];
+}
+IVIT_DEV void stv(void* p, int dt, long i, float v) {
+  if (dt == IVIT_BF16) ((bf16*)p)[i] = f2bf(v);
+  else ((float*)p)[i] = v;
+}
+
+__global__ void cast_kernel(const void* x, int xdt, void* y, int ydt, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) stv(y, ydt, i, ldv(x, xdt, i));
+}
+
+__global__ void add_act_grad_kernel(const void* a, int adt, const void* b, int bdt, const void* pre, int pdt,
+                                    const float* rs, long re, void* out, int odt, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float v = ldv(a, adt, i);
+  if (b) v += ldv(b, bdt, i);
+  if (pre) v *= gelu_erf_grad(ldv(pre, pdt, i));
+  if (rs) v *= rs[i / re];
+  stv(out, odt, i, v);
+}
+
+__global__ void copy_cols_kernel(const void* src, long lds, void* dst, long ldd, long rows, long cols, int dt) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows * cols) return;
+  const long r = i / cols, c = i - r * cols;
+  stv(dst, dt, r * ldd + c, ldv(src, dt, r * lds + c));
+}
+
+// head row m (one BEV cell), anchor a: det channel a*7 + j (j=0 cls, 1..6 box),
+// intent channel A*7 + a*K + k.  Flat anchor index = m*A + a  (model_vit.py:183-184).
+__global__ void split_heads_kernel(const float* __restrict__ h, long ldh, long M, int A, int K, float* cls,
+                                   float* box, float* intent) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over M*A
+  if (i >= M * A) return;
+  const long m = i / A;
+  const int a = (int)(i - m * A);
+  const float* r = h + m * ldh;
+  cls[i] = r[a * 7];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) box[i * 6 + j] = r[a * 7 + 1 + j];
+  for (int k = 0; k < K; ++k) intent[i * K + k] = r[A * 7 + a * K + k];
+}
+
+__global__ void merge_heads_kernel(const float* dcls, const float* dbox, const float* dint, long M, int A, int K,
+                                   void* dh, long ldh, int dt) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;  // over M*ldh
+  if (i >= M * ldh) return;
+  const long m = i / ldh;
+  const int c = (int)(i - m * ldh);
+  float v = 0.f;
+  if (c < A * 7) {
+    const int a = c / 7, j = c - a * 7;
+    const long fa = m * A + a;
+    v = j == 0 ? (dcls ? dcls[fa] : 0.f) : (dbox ? dbox[fa * 6 + j - 1] : 0.f);
+  } else if (c < A * 7 + A * K) {
+    const int cc = c - A * 7, a = cc / K, k = cc - a * K;
+    v = dint ? dint[(m * A + a) * K + k] : 0.f;
+  }
+  stv(dh, dt, i, v);
+}
+
+// torch _multi_tensor_adamw (foreach=True, amsgrad=False, maximize=False):
+//   p *= 1 - lr*wd ; m = lerp(m, g, 1-b1) ; v = v*b2 + (1-b2) g^2
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+__global__ void adamw_kernel(void* const* params, void* const* grads, void* const* ms, void* const* vs,
+                             const long* sizes, float lr, float b1, float b2, float eps, float wd, float bc1,
+                             float bc2s) {
+  const int t = blockIdx.y;
+  const long n = sizes[t];
+  float* p = (float*)params[t];
+  const float* g = (const float*)grads[t];
+  float* m = (float*)ms[t];
+  float* v = (float*)vs[t];
+  const float step = lr / bc1;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    float pi = p[i] * (1.f - lr * wd);
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    const float den = sqrtf(vi) / bc2s + eps;
+    pi = pi - step * (mi / den);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+}  // namespace
+
+extern "C" int ivit_cast(const void* x, int x_dtype, void* y, int y_dtype, long n, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(cast_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), x, x_dtype, y, y_dtype,
+                     n);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_add_act_grad(const void* a, int a_dtype, const void* b, int b_dtype, const void* pre,
+                                 int pre_dtype, const float* row_scale, long row_elems, void* out, int out_dtype, long n,
+                                 void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(add_act_grad_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), a, a_dtype, b,
+                     b_dtype, pre, pre_dtype, row_scale, row_elems > 0 ? row_elems : 1, out, out_dtype, n);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_copy_cols(const void* src, long lds, void* dst, long ldd, long rows, long cols, int dtype,
+                              void* stream) {
+  if (rows * cols <= 0) return 0;
+  hipLaunchKernelGGL(copy_cols_kernel, dim3(ivit_cdiv(rows * cols, 256)), dim3(256), 0, ivit_stream(stream), src, lds,
+                     dst, ldd, rows, cols, dtype);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_split_heads(const float* h, long ldh, long M, long A, long K, float* cls, float* box,
+                                float* intent, void* stream) {
+  IVIT_CHECK_ARG(ldh >= A * 7 + A * K, "ivit_split_heads: ldh too small");
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(split_heads_kernel, dim3(ivit_cdiv(M * A, 256)), dim3(256), 0, ivit_stream(stream), h, ldh, M,
+                     (int)A, (int)K, cls, box, intent);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_merge_heads_grad(const float* dcls, const float* dbox, const float* dint, long M, long A, long K,
+                                     void* dh, long ldh, int dh_dtype, void* stream) {
+  if (M <= 0) return 0;
+  hipLaunchKernelGGL(merge_heads_kernel, dim3(ivit_cdiv(M * ldh, 256)), dim3(256), 0, ivit_stream(stream), dcls, dbox,
+                     dint, M, (int)A, (int)K, dh, ldh, dh_dtype);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_adamw(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
+                          void* const* exp_avg_sq, const long* sizes, long max_size, float lr, float beta1,
+                          float beta2, float eps, float weight_decay, float bc1, float bc2_sqrt, void* stream) {
+  if (n_tensors <= 0) return 0;
+  IVIT_CHECK_ARG(n_tensors < 65536, "ivit_adamw: too many tensors");
+  int gx = ivit_cdiv(max_size, 256);
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
+                     exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}

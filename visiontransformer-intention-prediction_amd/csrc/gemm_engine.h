@@ -1,0 +1,481 @@
+// Generic tiled MFMA GEMM engine for gfx950 with gather loaders and fused epilogues.
+//
+//   C[m, n] = sum_k A[m, k] * B[k, n]      (per batch z; optional split-K)
+//
+// Operands are "loaders": functors returning 8 bf16 (load8) or 4 f32 (load4) that are
+// contiguous along the loader's `c` argument. An operand is K-contiguous (LDS image
+// [rows=M or N][K], read with ds_read_b128) or MN-contiguous (image [K][M or N], read
+// with the CDNA4 transposing ds_read_b64_tr_b16). Gather loaders turn the patch
+// embedding and 3x3 convolutions into implicit GEMMs without an im2col buffer.
+//
+// bf16 path: 128x128x64 tile, 4 waves (2x2) x 64x64, v_mfma_f32_32x32x16_bf16.
+// f32  path: 128x128x16 tile, 4 waves (2x2) x 64x64, v_mfma_f32_32x32x2_f32 (exact f32).
+#pragma once
+#include "ivit_common.h"
+
+namespace ivit {
+
+constexpr int GBM = 128, GBN = 128;
+constexpr int GBK16 = 64;  // bf16 K tile
+constexpr int GBK32 = 16;  // f32 K tile
+
+// z -> element offset: (z / zdiv) * s1 + (z % zdiv) * s2
+struct BatchOff {
+  long zdiv = 1, s1 = 0, s2 = 0;
+  IVIT_DEV long at(int z) const { return (long)(z / zdiv) * s1 + (long)(z % zdiv) * s2; }
+};
+
+// ----------------------------------------------------------------------------- loaders
+// Dense matrix (optionally with a "row map" r -> (r / rpb) * rstride + roff + r % rpb,
+// used to skip CLS token rows). Element (r, c) at p[rowaddr(r) * ld + c]; zero if r >= R
+// or c >= C. C must be a multiple of 8 (bf16 chunks) / 4 (f32 chunks) — checked on host.
+template <typename S>
+struct LdDense {
+  static constexpr bool kRowFast = false;
+  const S* p; long ld; int R, C; long rpb, rstride, roff; BatchOff bo;
+  IVIT_DEV long row_addr(int r) const { return rpb ? (long)(r / rpb) * rstride + roff + r % rpb : (long)r; }
+  IVIT_DEV uint4 load8(int z, int r, int c) const {
+    if (r >= R || c >= C) return make_uint4(0, 0, 0, 0);
+    const S* q = p + bo.at(z) + row_addr(r) * ld + c;
+    if constexpr (sizeof(S) == 2) {
+      return *(const uint4*)q;
+    } else {
+      return f32x8_to_bf16x8(*(const float4*)q, *(const float4*)(q + 4));
+    }
+  }
+  IVIT_DEV float4 load4(int z, int r, int c) const {
+    if (r >= R || c >= C) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const S* q = p + bo.at(z) + row_addr(r) * ld + c;
+    if constexpr (sizeof(S) == 4) {
+      return *(const float4*)q;
+    } else {
+      Pack4 t; t.u = *(const uint2*)q;
+      return make_float4(bf2f(t.h[0]), bf2f(t.h[1]), bf2f(t.h[2]), bf2f(t.h[3]));
+    }
+  }
+};
+
+// Patch gather over an NCHW image (timm PatchEmbed conv k = s = P, P = 8):
+// r = m = b*Np + gy*Wp + gx ; c = kk = (ch*P + ky)*P + kx  (chunk of 8 = one kx row).
+template <typename S>
+struct LdPatch {
+  static constexpr bool kRowFast = true;  // consecutive patches are consecutive 32-B runs
+  const S* img; int Bn, Cin, H, W, Wp, Np; int R, C;
+  IVIT_DEV const S* addr(int r, int c) const {
+    const int b = r / Np, pi = r - b * Np, gy = pi / Wp, gx = pi - gy * Wp;
+    const int ch = c >> 6, ky = (c >> 3) & 7, kx = c & 7;
+    return img + (((long)b * Cin + ch) * H + gy * 8 + ky) * (long)W + gx * 8 + kx;
+  }
+  IVIT_DEV uint4 load8(int, int r, int c) const {
+    if (r >= R || c >= C) return make_uint4(0, 0, 0, 0);
+    const S* q = addr(r, c);
+    if constexpr (sizeof(S) == 2) return *(const uint4*)q;
+    else return f32x8_to_bf16x8(*(const float4*)q, *(const float4*)(q + 4));
+  }
+  IVIT_DEV float4 load4(int, int r, int c) const {
+    if (r >= R || c >= C) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const S* q = addr(r, c);
+    if constexpr (sizeof(S) == 4) return *(const float4*)q;
+    else {
+      Pack4 t; t.u = *(const uint2*)q;
+      return make_float4(bf2f(t.h[0]), bf2f(t.h[1]), bf2f(t.h[2]), bf2f(t.h[3]));
+    }
+  }
+};
+
+// k x k "same" convolution gather over an NHWC map (pad = k/2):
+// r = m = (b*H + y)*W + x ; c = kk = (ky*k + kx)*Cin + ci   (Cin % 8 == 0).
+// flip = true reads the spatially flipped tap (dgrad of the transposed conv).
+template <typename S>
+struct LdConv {
+  static constexpr bool kRowFast = false;
+  const S* x; int H, W, Cin, ks; int R, C; long ldc;  // ldc = channel stride of a pixel
+  IVIT_DEV bool at(int r, int c, long& off) const {
+    if (r >= R || c >= C) return false;
+    const int tap = c / Cin, ci = c - tap * Cin;
+    const int ky = tap / ks, kx = tap - ky * ks, pad = ks >> 1;
+    const int xw = r % W, t = r / W, y = t % H, b = t / H;
+    const int yy = y + ky - pad, xx = xw + kx - pad;
+    if (yy < 0 || yy >= H || xx < 0 || xx >= W) return false;
+    off = (((long)b * H + yy) * W + xx) * ldc + ci;
+    return true;
+  }
+  IVIT_DEV uint4 load8(int, int r, int c) const {
+    long off;
+    if (!at(r, c, off)) return make_uint4(0, 0, 0, 0);
+    const S* q = x + off;
+    if constexpr (sizeof(S) == 2) return *(const uint4*)q;
+    else return f32x8_to_bf16x8(*(const float4*)q, *(const float4*)(q + 4));
+  }
+  IVIT_DEV float4 load4(int, int r, int c) const {
+    long off;
+    if (!at(r, c, off)) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const S* q = x + off;
+    if constexpr (sizeof(S) == 4) return *(const float4*)q;
+    else {
+      Pack4 t; t.u = *(const uint2*)q;
+      return make_float4(bf2f(t.h[0]), bf2f(t.h[1]), bf2f(t.h[2]), bf2f(t.h[3]));
+    }
+  }
+};
+
+// Weights [Cout][ks][ks][Cin] read as the dgrad B operand: row r = (ky'*ks + kx')*Cout + co
+// (the flipped tap), col c = ci  ->  W[co][ks-1-ky'][ks-1-kx'][ci].
+template <typename S>
+struct LdConvWFlip {
+  static constexpr bool kRowFast = false;
+  const S* w; int Cout, Cin, ks; int R, C;
+  IVIT_DEV const S* addr(int r, int c) const {
+    const int tap = r / Cout, co = r - tap * Cout;
+    const int ky = tap / ks, kx = tap - ky * ks;
+    return w + (((long)co * ks + (ks - 1 - ky)) * ks + (ks - 1 - kx)) * Cin + c;
+  }
+  IVIT_DEV uint4 load8(int, int r, int c) const {
+    if (r >= R || c >= C) return make_uint4(0, 0, 0, 0);
+    const S* q = addr(r, c);
+    if constexpr (sizeof(S) == 2) return *(const uint4*)q;
+    else return f32x8_to_bf16x8(*(const float4*)q, *(const float4*)(q + 4));
+  }
+  IVIT_DEV float4 load4(int, int r, int c) const {
+    if (r >= R || c >= C) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const S* q = addr(r, c);
+    if constexpr (sizeof(S) == 4) return *(const float4*)q;
+    else {
+      Pack4 t; t.u = *(const uint2*)q;
+      return make_float4(bf2f(t.h[0]), bf2f(t.h[1]), bf2f(t.h[2]), bf2f(t.h[3]));
+    }
+  }
+};
+
+// ----------------------------------------------------------------------------- epilogues
+// apply(z, split, m, n, v) is called once per output element with m < M, n < N.
+template <typename O>
+struct EpiStore {  // out = act(alpha*acc + bias[n]); optional pre-activation copy
+  O* out; long ldo; BatchOff bo; const float* bias; int act; O* pre; float alpha;
+  IVIT_DEV void apply(int z, int, int m, int n, float v) const {
+    v = v * alpha + (bias ? bias[n] : 0.f);
+    const long o = bo.at(z) + (long)m * ldo + n;
+    if (pre) pre[o] = from_f32<O>(v);
+    if (act == IVIT_ACT_GELU) v = gelu_erf(v);
+    else if (act == IVIT_ACT_RELU) v = fmaxf(v, 0.f);
+    out[o] = from_f32<O>(v);
+  }
+};
+
+struct EpiResid {  // out(f32) = res + scale[m / rps] * (acc + bias[n])
+  float* out; long ldo; const float* res; long ldr; const float* bias; const float* scale; long rps;
+  IVIT_DEV void apply(int, int, int m, int n, float v) const {
+    v += bias ? bias[n] : 0.f;
+    if (scale) v *= scale[m / rps];
+    out[(long)m * ldo + n] = res[(long)m * ldr + n] + v;
+  }
+};
+
+template <typename O, typename P>
+struct EpiGeluGrad {  // out = acc * gelu'(pre)
+  O* out; long ldo; const P* pre; long ldp;
+  IVIT_DEV void apply(int, int, int m, int n, float v) const {
+    out[(long)m * ldo + n] = from_f32<O>(v * gelu_erf_grad(to_f32(pre[(long)m * ldp + n])));
+  }
+};
+
+struct EpiSlab {  // split-K partial slab [split][M][N] (f32)
+  float* slab; long M, N;
+  IVIT_DEV void apply(int, int split, int m, int n, float v) const { slab[((long)split * M + m) * N + n] = v; }
+};
+
+struct EpiPatch {  // token (b, 1 + p) of x(f32) = acc + bias[n] + pos[1 + p][n]
+  float* out; int Np, D; const float* bias; const float* pos;
+  IVIT_DEV void apply(int, int, int m, int n, float v) const {
+    const int b = m / Np, p = m - b * Np;
+    const long row = (long)b * (Np + 1) + 1 + p;
+    out[row * D + n] = v + bias[n] + pos[(long)(1 + p) * D + n];
+  }
+};
+
+// ----------------------------------------------------------------------------- LDS images
+// K-contiguous bf16 image: rows x 64 k (128-B rows); 16-B chunk c of row r stored at
+// chunk c ^ f(r), f a bijection of (r>>1)&7 chosen so that both the 32x32x16 row reads
+// (ds_read_b128 lane groups) and the transposed reads hit distinct bank slots.
+IVIT_DEV int swz128(int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 1) | ((r >> 2) & 1); }
+IVIT_DEV int kc_off(int r, int c) { return r * 128 + ((c ^ swz128(r)) << 4); }
+// MN-contiguous bf16 image: 64 k-rows x 128 columns (256-B rows); chunk c -> c ^ 4(r&3).
+IVIT_DEV int mn_off(int r, int c) { return r * 256 + ((c ^ ((r & 3) << 2)) << 4); }
+
+IVIT_DEV bf16x8 frag_kc(const char* img, int row, int chunk) {
+  return *(const bf16x8*)(img + kc_off(row, chunk));
+}
+
+IVIT_DEV s16x4 ds_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// 32x32x16 operand (lane l: row/col l&31, k = 8(l>>5) + j) from an MN-contiguous image:
+// two transposing reads of 4 k-rows each.
+IVIT_DEV bf16x8 frag_mn(const char* img, int kbase, int colbase, int lane) {
+  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = colbase + 16 * (G & 1) + 4 * p;
+  const int r0 = kbase + 8 * (G >> 1) + q;
+  const int c = col >> 3, e = (col & 7) * 2;
+  s16x4 lo = ds_tr(img + mn_off(r0, c) + e);
+  s16x4 hi = ds_tr(img + mn_off(r0 + 4, c) + e);
+  union { s16x4 s[2]; bf16x8 v; } u;
+  u.s[0] = lo; u.s[1] = hi;
+  return u.v;
+}
+
+// ----------------------------------------------------------------------------- bf16 kernel
+template <class LA, class LB, class EPI, bool A_KC, bool B_KC>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
+                                                         int tilesM, int tilesN, int splits, int kchunk) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][16384];  // [stage][A|B][image]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin / tilesN, tn = lin - tm * tilesN;
+  const int z = blockIdx.y / splits, split = blockIdx.y - z * splits;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nk = (kend - kbeg + GBK16 - 1) / GBK16;
+
+  uint4 ra[4], rb[4];
+  auto gload = [&](const auto& ld, bool kc, int o0, int k0, uint4* r) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 256 * i;
+      if (kc) {  // image rows = 128 (m/n), 8 chunks along k
+        int row, ch;
+        if (std::decay_t<decltype(ld)>::kRowFast) { row = idx & 127; ch = idx >> 7; }
+        else { row = idx >> 3; ch = idx & 7; }
+        const int kk = k0 + ch * 8;
+        r[i] = kk < kend ? ld.load8(z, o0 + row, kk) : make_uint4(0, 0, 0, 0);
+      } else {   // image rows = 64 (k), 16 chunks along m/n
+        int row, ch;
+        if (std::decay_t<decltype(ld)>::kRowFast) { row = idx & 63; ch = idx >> 6; }
+        else { row = idx >> 4; ch = idx & 15; }
+        const int kk = k0 + row;
+        r[i] = kk < kend ? ld.load8(z, kk, o0 + ch * 8) : make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto sstore = [&](char* img, bool kc, bool rowfast, const uint4* r) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 256 * i;
+      int off;
+      if (kc) {
+        int row, ch;
+        if (rowfast) { row = idx & 127; ch = idx >> 7; } else { row = idx >> 3; ch = idx & 7; }
+        off = kc_off(row, ch);
+      } else {
+        int row, ch;
+        if (rowfast) { row = idx & 63; ch = idx >> 6; } else { row = idx >> 4; ch = idx & 15; }
+        off = mn_off(row, ch);
+      }
+      *(uint4*)(img + off) = r[i];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) {
+    gload(la, A_KC, m0, kbeg, ra);
+    gload(lb, B_KC, n0, kbeg, rb);
+    sstore(smem[0][0], A_KC, LA::kRowFast, ra);
+    sstore(smem[0][1], B_KC, LB::kRowFast, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      gload(la, A_KC, m0, kbeg + (kt + 1) * GBK16, ra);
+      gload(lb, B_KC, n0, kbeg + (kt + 1) * GBK16, rb);
+    }
+    const char* ia = smem[cur][0];
+    const char* ib = smem[cur][1];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int rb0 = wm * 64 + 32 * i;
+        fa[i] = A_KC ? frag_kc(ia, rb0 + (lane & 31), 2 * t + (lane >> 5)) : frag_mn(ia, 16 * t, rb0, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cb0 = wn * 64 + 32 * j;
+        fb[j] = B_KC ? frag_kc(ib, cb0 + (lane & 31), 2 * t + (lane >> 5)) : frag_mn(ib, 16 * t, cb0, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      sstore(smem[cur ^ 1][0], A_KC, LA::kRowFast, ra);
+      sstore(smem[cur ^ 1][1], B_KC, LB::kRowFast, rb);
+    }
+    __syncthreads();
+  }
+  // C layout (32x32 f32): col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < M) epi.apply(z, split, m, n, acc[i][j][r]);
+      }
+    }
+}
+
+// ----------------------------------------------------------------------------- f32 kernel
+// K-contiguous f32 image [128][17] (row pad -> conflict-free ds_read_b32 column reads);
+// MN-contiguous f32 image [16][128].
+template <class LA, class LB, class EPI, bool A_KC, bool B_KC>
+__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
+                                                        int tilesM, int tilesN, int splits, int kchunk) {
+  constexpr int KCS = 17;                       // K-contig row stride (floats)
+  constexpr int IMG = 128 * KCS > 16 * 128 ? 128 * KCS : 16 * 128;
+  __shared__ __attribute__((aligned(16))) float smem[2][2][IMG];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin / tilesN, tn = lin - tm * tilesN;
+  const int z = blockIdx.y / splits, split = blockIdx.y - z * splits;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nk = (kend - kbeg + GBK32 - 1) / GBK32;
+
+  float4 ra[2], rb[2];
+  auto gload = [&](const auto& ld, bool kc, int o0, int k0, float4* r) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + 256 * i;
+      if (kc) {  // 128 rows x 4 chunks of 4 k
+        int row, ch;
+        if (std::decay_t<decltype(ld)>::kRowFast) { row = idx & 127; ch = idx >> 7; }
+        else { row = idx >> 2; ch = idx & 3; }
+        const int kk = k0 + ch * 4;
+        r[i] = kk < kend ? ld.load4(z, o0 + row, kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {   // 16 k-rows x 32 chunks of 4
+        int row, ch;
+        if (std::decay_t<decltype(ld)>::kRowFast) { row = idx & 15; ch = idx >> 4; }
+        else { row = idx >> 5; ch = idx & 31; }
+        const int kk = k0 + row;
+        r[i] = kk < kend ? ld.load4(z, kk, o0 + ch * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  auto sstore = [&](float* img, bool kc, bool rowfast, const float4* r) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + 256 * i;
+      if (kc) {
+        int row, ch;
+        if (rowfast) { row = idx & 127; ch = idx >> 7; } else { row = idx >> 2; ch = idx & 3; }
+        float* d = img + row * KCS + ch * 4;
+        d[0] = r[i].x; d[1] = r[i].y; d[2] = r[i].z; d[3] = r[i].w;
+      } else {
+        int row, ch;
+        if (rowfast) { row = idx & 15; ch = idx >> 4; } else { row = idx >> 5; ch = idx & 31; }
+        *(float4*)(img + row * 128 + ch * 4) = r[i];
+      }
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) {
+    gload(la, A_KC, m0, kbeg, ra);
+    gload(lb, B_KC, n0, kbeg, rb);
+    sstore(smem[0][0], A_KC, LA::kRowFast, ra);
+    sstore(smem[0][1], B_KC, LB::kRowFast, rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      gload(la, A_KC, m0, kbeg + (kt + 1) * GBK32, ra);
+      gload(lb, B_KC, n0, kbeg + (kt + 1) * GBK32, rb);
+    }
+    const float* ia = smem[cur][0];
+    const float* ib = smem[cur][1];
+    const int kq = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = 2 * s + kq;
+      float fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + 32 * i + (lane & 31);
+        fa[i] = A_KC ? ia[row * KCS + k] : ia[k * 128 + row];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wn * 64 + 32 * j + (lane & 31);
+        fb[j] = B_KC ? ib[col * KCS + k] : ib[k * 128 + col];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      sstore(smem[cur ^ 1][0], A_KC, LA::kRowFast, ra);
+      sstore(smem[cur ^ 1][1], B_KC, LB::kRowFast, rb);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + 32 * j + (lane & 31);
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < M) epi.apply(z, split, m, n, acc[i][j][r]);
+      }
+    }
+}
+
+// ----------------------------------------------------------------------------- launcher
+// dtype_bf16: which kernel. batch: number of z. splits: split-K factor (kchunk multiple
+// of the K tile). Grid: x = tiles (XCD-remapped), y = batch * splits.
+template <bool A_KC, bool B_KC, class LA, class LB, class EPI>
+int launch_gemm(bool bf16_path, const LA& la, const LB& lb, const EPI& epi, int M, int N, int K, int batch,
+                int splits, hipStream_t st) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  const int tilesM = ivit_cdiv(M, GBM), tilesN = ivit_cdiv(N, GBN);
+  const int bk = bf16_path ? GBK16 : GBK32;
+  if (splits < 1) splits = 1;
+  int kchunk = ivit_cdiv(ivit_cdiv(K, splits), bk) * bk;
+  if (kchunk <= 0) kchunk = bk;
+  dim3 grid(tilesM * tilesN, batch * splits);
+  if (bf16_path)
+    hipLaunchKernelGGL((gemm_bf16_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N, K,
+                       tilesM, tilesN, splits, kchunk);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N, K,
+                       tilesM, tilesN, splits, kchunk);
+  return 0;
+}
+
+}  // namespace ivit

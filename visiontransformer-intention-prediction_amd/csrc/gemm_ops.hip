@@ -1,0 +1,425 @@
+// C-ABI GEMM-shaped ops: linear fwd/dgrad/wgrad, patch embedding, NHWC convolutions.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "gemm_engine.h"
+
+using namespace ivit;
+
+static thread_local char g_err[512];
+void ivit_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+extern "C" const char* ivit_last_error(void) { return g_err; }
+extern "C" const char* ivit_version(void) { return "ivit-hip 0.1 gfx950"; }
+
+// ----------------------------------------------------------------------------- reductions
+// Sum split-K slabs: out[i] (+)= sum_s slab[s][i]
+__global__ void splitk_reduce_kernel(const float* __restrict__ slab, long n, int splits, float* __restrict__ out,
+                                     int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += slab[(long)k * n + i];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+// Column sums in two passes (deterministic): partial[chunk][col] then out[col].
+constexpr int CS_ROWS = 256;
+template <typename S>
+__global__ void colsum_partial_kernel(const S* __restrict__ X, long ld, long rpb, long rstride, long roff, long M,
+                                      long N, float* __restrict__ part) {
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ph = threadIdx.x >> 6;  // 4 row phases
+  const long r0 = (long)blockIdx.y * CS_ROWS;
+  float s = 0.f;
+  if (col < N) {
+    for (long r = r0 + ph; r < min(M, r0 + CS_ROWS); r += 4) {
+      const long row = rpb ? (r / rpb) * rstride + roff + r % rpb : r;
+      s += to_f32(X[row * ld + col]);
+    }
+  }
+  __shared__ float red[4][64];
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && col < N)
+    part[(long)blockIdx.y * N + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ void colsum_final_kernel(const float* __restrict__ part, long chunks, long N, float* __restrict__ out,
+                                    int accumulate) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (long k = 0; k < chunks; ++k) s += part[k * N + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+extern "C" long ivit_colsum_workspace(long M, long N) { return (long)ivit_cdiv(M, CS_ROWS) * N * 4; }
+
+extern "C" int ivit_colsum(const void* X, int x_dtype, long ld, long rpb, long rstride, long roff, long M, long N,
+                           float* out, int accumulate, void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(work_bytes >= ivit_colsum_workspace(M, N), "ivit_colsum: workspace too small");
+  if (M <= 0 || N <= 0) return 0;
+  hipStream_t st = ivit_stream(stream);
+  const int chunks = ivit_cdiv(M, CS_ROWS);
+  dim3 g(ivit_cdiv(N, 64), chunks);
+  if (x_dtype == IVIT_BF16)
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, g, dim3(256), 0, st, (const bf16*)X, ld, rpb, rstride, roff, M, N,
+                       (float*)work);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(256), 0, st, (const float*)X, ld, rpb, rstride, roff, M,
+                       N, (float*)work);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(ivit_cdiv(N, 256)), dim3(256), 0, st, (const float*)work, chunks, N,
+                     out, accumulate);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+static int splitk_choice(long tiles, long K, int bk) {
+  // aim for >= ~512 workgroups, each keeping >= 8 K-tiles of work
+  int s = 1;
+  while (tiles * s < 512 && K / ((long)bk * (s * 2)) >= 8) s *= 2;
+  return s;
+}
+
+// ----------------------------------------------------------------------------- linear
+template <typename S, typename O>
+static int linear_fwd_t(const void* X, long ldx, const void* W, const float* bias, long M, long N, long K, int act,
+                        void* Y, long ldy, void* Ypre, const float* resid, long ldr, const float* rs, long rps,
+                        hipStream_t st) {
+  const bool bf = sizeof(S) == 2;
+  LdDense<S> la{(const S*)X, ldx, (int)M, (int)K, 0, 0, 0, {}};
+  LdDense<S> lb{(const S*)W, K, (int)N, (int)K, 0, 0, 0, {}};
+  if (resid) {
+    EpiResid e{(float*)Y, ldy, resid, ldr, bias, rs, rps > 0 ? rps : 1};
+    return launch_gemm<true, true>(bf, la, lb, e, M, N, K, 1, 1, st);
+  }
+  EpiStore<O> e{(O*)Y, ldy, {}, bias, act, (O*)Ypre, 1.f};
+  return launch_gemm<true, true>(bf, la, lb, e, M, N, K, 1, 1, st);
+}
+
+extern "C" int ivit_linear_fwd(int dtype, const void* X, long ldx, const void* W, const float* bias, long M, long N,
+                               long K, int act, void* Y, long ldy, int y_dtype, void* Ypre, const float* resid, long ldr,
+                               const float* row_scale, long rows_per_scale, void* stream) {
+  IVIT_CHECK_ARG(K % 8 == 0 && ldx % 8 == 0, "ivit_linear_fwd: K and ldx must be multiples of 8");
+  IVIT_CHECK_ARG(!resid || y_dtype == IVIT_F32, "ivit_linear_fwd: residual output must be f32");
+  hipStream_t st = ivit_stream(stream);
+  int rc;
+  if (dtype == IVIT_BF16)
+    rc = y_dtype == IVIT_BF16
+             ? linear_fwd_t<bf16, bf16>(X, ldx, W, bias, M, N, K, act, Y, ldy, Ypre, resid, ldr, row_scale, rows_per_scale, st)
+             : linear_fwd_t<bf16, float>(X, ldx, W, bias, M, N, K, act, Y, ldy, Ypre, resid, ldr, row_scale, rows_per_scale, st);
+  else
+    rc = linear_fwd_t<float, float>(X, ldx, W, bias, M, N, K, act, Y, ldy, Ypre, resid, ldr, row_scale, rows_per_scale, st);
+  if (rc) return rc;
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename S, typename O>
+static int linear_dgrad_t(const void* dY, long lddy, const void* W, long M, long N, long K, void* dX, long lddx,
+                          const void* pre, long ldpre, hipStream_t st) {
+  const bool bf = sizeof(S) == 2;
+  LdDense<S> la{(const S*)dY, lddy, (int)M, (int)N, 0, 0, 0, {}};   // A[m][n], reduce over n
+  LdDense<S> lb{(const S*)W, K, (int)N, (int)K, 0, 0, 0, {}};       // B[n][k] MN-contiguous
+  if (pre) {
+    EpiGeluGrad<O, S> e{(O*)dX, lddx, (const S*)pre, ldpre};
+    return launch_gemm<true, false>(bf, la, lb, e, M, K, N, 1, 1, st);
+  }
+  EpiStore<O> e{(O*)dX, lddx, {}, nullptr, IVIT_ACT_NONE, nullptr, 1.f};
+  return launch_gemm<true, false>(bf, la, lb, e, M, K, N, 1, 1, st);
+}
+
+extern "C" int ivit_linear_dgrad(int dtype, const void* dY, long lddy, const void* W, long M, long N, long K, void* dX,
+                                 long lddx, int dx_dtype, const void* gelu_pre, long ldpre, void* stream) {
+  IVIT_CHECK_ARG(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0, "ivit_linear_dgrad: N, K, lddy must be multiples of 8");
+  hipStream_t st = ivit_stream(stream);
+  int rc;
+  if (dtype == IVIT_BF16)
+    rc = dx_dtype == IVIT_BF16 ? linear_dgrad_t<bf16, bf16>(dY, lddy, W, M, N, K, dX, lddx, gelu_pre, ldpre, st)
+                               : linear_dgrad_t<bf16, float>(dY, lddy, W, M, N, K, dX, lddx, gelu_pre, ldpre, st);
+  else
+    rc = linear_dgrad_t<float, float>(dY, lddy, W, M, N, K, dX, lddx, gelu_pre, ldpre, st);
+  if (rc) return rc;
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+static long wgrad_splits(long Mo, long No, long Kr, bool bf) {
+  const long tiles = (long)ivit_cdiv(Mo, GBM) * ivit_cdiv(No, GBN);
+  return splitk_choice(tiles, Kr, bf ? GBK16 : GBK32);
+}
+
+extern "C" long ivit_linear_wgrad_workspace(long M, long N, long K) {
+  const long s = wgrad_splits(N, K, M, true) > wgrad_splits(N, K, M, false) ? wgrad_splits(N, K, M, true)
+                                                                             : wgrad_splits(N, K, M, false);
+  return s * N * K * 4 + ivit_colsum_workspace(M, N);
+}
+
+template <typename S>
+static int linear_wgrad_t(const void* dY, long lddy, const void* X, long ldx, long M, long N, long K, float* slab,
+                          int splits, hipStream_t st) {
+  const bool bf = sizeof(S) == 2;
+  LdDense<S> la{(const S*)dY, lddy, (int)M, (int)N, 0, 0, 0, {}};  // A[n][m] (MN-contig), rows = m
+  LdDense<S> lb{(const S*)X, ldx, (int)M, (int)K, 0, 0, 0, {}};    // B[m][k] (MN-contig)
+  EpiSlab e{slab, N, K};
+  return launch_gemm<false, false>(bf, la, lb, e, N, K, M, 1, splits, st);
+}
+
+extern "C" int ivit_linear_wgrad(int dtype, const void* dY, long lddy, const void* X, long ldx, long M, long N,
+                                 long K, float* dW, float* dbias, int accumulate, void* work, long work_bytes,
+                                 void* stream) {
+  IVIT_CHECK_ARG(N % 8 == 0 && K % 8 == 0 && lddy % 8 == 0 && ldx % 8 == 0,
+                 "ivit_linear_wgrad: N, K, lddy, ldx must be multiples of 8");
+  IVIT_CHECK_ARG(work_bytes >= ivit_linear_wgrad_workspace(M, N, K), "ivit_linear_wgrad: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  const bool bf = dtype == IVIT_BF16;
+  const int splits = (int)wgrad_splits(N, K, M, bf);
+  float* slab = (float*)work;
+  int rc = bf ? linear_wgrad_t<bf16>(dY, lddy, X, ldx, M, N, K, slab, splits, st)
+              : linear_wgrad_t<float>(dY, lddy, X, ldx, M, N, K, slab, splits, st);
+  if (rc) return rc;
+  const long n = N * K;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dW, accumulate);
+  IVIT_LAUNCH_CHECK();
+  if (dbias) {
+    char* cw = (char*)work + (long)splits * N * K * 4;
+    rc = ivit_colsum(dY, dtype, lddy, 0, 0, 0, M, N, dbias, accumulate, cw, ivit_colsum_workspace(M, N), stream);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// ----------------------------------------------------------------------------- patch embedding
+__global__ void cls_rows_kernel(float* out, long B, long Ntok, long D, const float* cls, const float* pos) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * D) return;
+  const long b = i / D, d = i - b * D;
+  out[b * Ntok * D + d] = cls[d] + pos[d];
+}
+
+template <typename S>
+static int patch_fwd_t(const float* img, long B, long C, long H, long W, const void* Wt, const float* bias,
+                       const float* pos, long D, float* out, hipStream_t st) {
+  const bool bf = sizeof(S) == 2;
+  const int Wp = (int)(W / 8), Np = (int)((H / 8) * (W / 8));
+  LdPatch<float> la{img, (int)B, (int)C, (int)H, (int)W, Wp, Np, (int)(B * Np), (int)(C * 64)};
+  LdDense<S> lb{(const S*)Wt, C * 64, (int)D, (int)(C * 64), 0, 0, 0, {}};
+  EpiPatch e{out, Np, (int)D, bias, pos};
+  return launch_gemm<true, true>(bf, la, lb, e, (int)(B * Np), (int)D, (int)(C * 64), 1, 1, st);
+}
+
+extern "C" int ivit_patch_embed_fwd(int dtype, const float* img, long B, long C, long H, long W, const void* Wt,
+                                    const float* bias, const float* pos, const float* cls, long D, float* out,
+                                    void* stream) {
+  IVIT_CHECK_ARG(H % 8 == 0 && W % 8 == 0, "ivit_patch_embed_fwd: H, W must be multiples of the patch (8)");
+  hipStream_t st = ivit_stream(stream);
+  int rc = dtype == IVIT_BF16 ? patch_fwd_t<bf16>(img, B, C, H, W, Wt, bias, pos, D, out, st)
+                              : patch_fwd_t<float>(img, B, C, H, W, Wt, bias, pos, D, out, st);
+  if (rc) return rc;
+  const long Ntok = (H / 8) * (W / 8) + 1;
+  hipLaunchKernelGGL(cls_rows_kernel, dim3(ivit_cdiv(B * D, 256)), dim3(256), 0, st, out, B, Ntok, D, cls, pos);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+// dpos[t][d] (+)= sum_b dtok[b][t][d]; dcls = dpos[0] (before accumulation semantics: (+)=)
+template <typename S>
+__global__ void pos_grad_kernel(const S* __restrict__ dtok, long B, long Ntok, long D, float* dpos, float* dcls,
+                                int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Ntok * D) return;
+  float s = 0.f;
+  for (long b = 0; b < B; ++b) s += to_f32(dtok[b * Ntok * D + i]);
+  dpos[i] = accumulate ? dpos[i] + s : s;
+  if (i < D && dcls) dcls[i] = accumulate ? dcls[i] + s : s;
+}
+
+extern "C" long ivit_patch_embed_wgrad_workspace(long B, long C, long H, long W, long D) {
+  const long Np = (H / 8) * (W / 8);
+  long s = wgrad_splits(D, C * 64, B * Np, false);
+  const long s2 = wgrad_splits(D, C * 64, B * Np, true);
+  if (s2 > s) s = s2;
+  return s * D * C * 64 * 4 + ivit_colsum_workspace(B * Np, D);
+}
+
+template <typename S>
+static int patch_wgrad_t(const void* dtok, const float* img, long B, long C, long H, long W, long D, float* slab,
+                         int splits, hipStream_t st) {
+  const bool bf = sizeof(S) == 2;
+  const int Wp = (int)(W / 8), Np = (int)((H / 8) * (W / 8));
+  const long Ntok = Np + 1;
+  LdDense<S> la{(const S*)dtok, D, (int)(B * Np), (int)D, Np, Ntok, 1, {}};  // A[d][m] rows m -> token rows
+  LdPatch<float> lb{img, (int)B, (int)C, (int)H, (int)W, Wp, Np, (int)(B * Np), (int)(C * 64)};
+  EpiSlab e{slab, D, C * 64};
+  return launch_gemm<false, false>(bf, la, lb, e, (int)D, (int)(C * 64), (int)(B * Np), 1, splits, st);
+}
+
+extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* img, long B, long C, long H, long W,
+                                      long D, float* dW, float* dbias, float* dpos, float* dcls, int accumulate,
+                                      void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(work_bytes >= ivit_patch_embed_wgrad_workspace(B, C, H, W, D), "patch wgrad: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  const bool bf = dtype == IVIT_BF16;
+  const long Np = (H / 8) * (W / 8), Ntok = Np + 1;
+  const int splits = (int)wgrad_splits(D, C * 64, B * Np, bf);
+  float* slab = (float*)work;
+  int rc = bf ? patch_wgrad_t<bf16>(dtok, img, B, C, H, W, D, slab, splits, st)
+              : patch_wgrad_t<float>(dtok, img, B, C, H, W, D, slab, splits, st);
+  if (rc) return rc;
+  const long n = D * C * 64;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dW, accumulate);
+  if (bf)
+    hipLaunchKernelGGL(pos_grad_kernel<bf16>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const bf16*)dtok, B,
+                       Ntok, D, dpos, dcls, accumulate);
+  else
+    hipLaunchKernelGGL(pos_grad_kernel<float>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const float*)dtok,
+                       B, Ntok, D, dpos, dcls, accumulate);
+  IVIT_LAUNCH_CHECK();
+  char* cw = (char*)work + (long)splits * n * 4;
+  return ivit_colsum(dtok, dtype, D, Np, Ntok, 1, B * Np, D, dbias, accumulate, cw, ivit_colsum_workspace(B * Np, D),
+                     stream);
+}
+
+// ----------------------------------------------------------------------------- NHWC convolution
+template <typename S, typename O>
+static int conv_fwd_t(const void* X, long B, long H, long W, long Cin, const void* Wp, const float* bias, long Cout,
+                      long ks, void* Y, long ldy, hipStream_t st) {
+  const bool bf = sizeof(S) == 2;
+  const int M = (int)(B * H * W), Kc = (int)(ks * ks * Cin);
+  LdConv<S> la{(const S*)X, (int)H, (int)W, (int)Cin, (int)ks, M, Kc, Cin};
+  LdDense<S> lb{(const S*)Wp, Kc, (int)Cout, Kc, 0, 0, 0, {}};
+  EpiStore<O> e{(O*)Y, ldy, {}, bias, IVIT_ACT_NONE, nullptr, 1.f};
+  return launch_gemm<true, true>(bf, la, lb, e, M, (int)Cout, Kc, 1, 1, st);
+}
+
+extern "C" int ivit_conv_fwd(int dtype, const void* X, long B, long H, long W, long Cin, const void* Wp,
+                             const float* bias, long Cout, long ks, void* Y, long ldy, int y_dtype, void* stream) {
+  IVIT_CHECK_ARG(Cin % 8 == 0 && (ks == 1 || ks == 3), "ivit_conv_fwd: Cin %% 8 and ks in {1,3}");
+  hipStream_t st = ivit_stream(stream);
+  int rc;
+  if (dtype == IVIT_BF16)
+    rc = y_dtype == IVIT_BF16 ? conv_fwd_t<bf16, bf16>(X, B, H, W, Cin, Wp, bias, Cout, ks, Y, ldy, st)
+                              : conv_fwd_t<bf16, float>(X, B, H, W, Cin, Wp, bias, Cout, ks, Y, ldy, st);
+  else
+    rc = conv_fwd_t<float, float>(X, B, H, W, Cin, Wp, bias, Cout, ks, Y, ldy, st);
+  if (rc) return rc;
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename S, typename O>
+static int conv_dgrad_t(const void* dY, long lddy, long B, long H, long W, long Cout, const void* Wp, long Cin,
+                        long ks, void* dX, hipStream_t st) {
+  const bool bf = sizeof(S) == 2;
+  const int M = (int)(B * H * W), Kc = (int)(ks * ks * Cout);
+  LdConv<S> la{(const S*)dY, (int)H, (int)W, (int)Cout, (int)ks, M, Kc, lddy};
+  LdConvWFlip<S> lb{(const S*)Wp, (int)Cout, (int)Cin, (int)ks, Kc, (int)Cin};
+  EpiStore<O> e{(O*)dX, Cin, {}, nullptr, IVIT_ACT_NONE, nullptr, 1.f};
+  return launch_gemm<true, false>(bf, la, lb, e, M, (int)Cin, Kc, 1, 1, st);
+}
+
+extern "C" int ivit_conv_dgrad(int dtype, const void* dY, long lddy, long B, long H, long W, long Cout, const void* Wp,
+                               long Cin, long ks, void* dX, int dx_dtype, void* stream) {
+  IVIT_CHECK_ARG(Cout % 8 == 0 && Cin % 8 == 0 && lddy % 8 == 0, "ivit_conv_dgrad: channel counts %% 8");
+  hipStream_t st = ivit_stream(stream);
+  int rc;
+  if (dtype == IVIT_BF16)
+    rc = dx_dtype == IVIT_BF16 ? conv_dgrad_t<bf16, bf16>(dY, lddy, B, H, W, Cout, Wp, Cin, ks, dX, st)
+                               : conv_dgrad_t<bf16, float>(dY, lddy, B, H, W, Cout, Wp, Cin, ks, dX, st);
+  else
+    rc = conv_dgrad_t<float, float>(dY, lddy, B, H, W, Cout, Wp, Cin, ks, dX, st);
+  if (rc) return rc;
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" long ivit_conv_wgrad_workspace(long B, long H, long W, long Cin, long Cout, long ks) {
+  const long M = B * H * W, Kc = ks * ks * Cin;
+  long s = wgrad_splits(Cout, Kc, M, false);
+  const long s2 = wgrad_splits(Cout, Kc, M, true);
+  if (s2 > s) s = s2;
+  return s * Cout * Kc * 4 + ivit_colsum_workspace(M, Cout);
+}
+
+template <typename S>
+static int conv_wgrad_t(const void* dY, long lddy, const void* X, long B, long H, long W, long Cin, long Cout,
+                        long ks, float* slab, int splits, hipStream_t st) {
+  const bool bf = sizeof(S) == 2;
+  const int M = (int)(B * H * W), Kc = (int)(ks * ks * Cin);
+  LdDense<S> la{(const S*)dY, lddy, M, (int)Cout, 0, 0, 0, {}};                 // A[co][m]
+  LdConv<S> lb{(const S*)X, (int)H, (int)W, (int)Cin, (int)ks, M, Kc, Cin};    // B[m][kk]
+  EpiSlab e{slab, Cout, Kc};
+  return launch_gemm<false, false>(bf, la, lb, e, (int)Cout, Kc, M, 1, splits, st);
+}
+
+extern "C" int ivit_conv_wgrad(int dtype, const void* dY, long lddy, const void* X, long B, long H, long W, long Cin,
+                               long Cout, long ks, float* dWp, float* dbias, int accumulate, void* work,
+                               long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(Cout % 8 == 0 && Cin % 8 == 0 && lddy % 8 == 0, "ivit_conv_wgrad: channel counts %% 8");
+  IVIT_CHECK_ARG(work_bytes >= ivit_conv_wgrad_workspace(B, H, W, Cin, Cout, ks), "conv wgrad: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  const bool bf = dtype == IVIT_BF16;
+  const long M = B * H * W, Kc = ks * ks * Cin;
+  const int splits = (int)wgrad_splits(Cout, Kc, M, bf);
+  float* slab = (float*)work;
+  int rc = bf ? conv_wgrad_t<bf16>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, splits, st)
+              : conv_wgrad_t<float>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, splits, st);
+  if (rc) return rc;
+  const long n = Cout * Kc;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dWp, accumulate);
+  IVIT_LAUNCH_CHECK();
+  if (dbias) {
+    char* cw = (char*)work + (long)splits * n * 4;
+    return ivit_colsum(dY, dtype, lddy, 0, 0, 0, M, Cout, dbias, accumulate, cw, ivit_colsum_workspace(M, Cout),
+                       stream);
+  }
+  return 0;
+}
+
+template <typename O>
+__global__ void pack_conv_kernel(const float* __restrict__ w, long Cout, long Cin, long ks, long Cpad, O* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = Cpad * ks * ks * Cin;
+  if (i >= n) return;
+  const long ci = i % Cin, t = i / Cin, kx = t % ks, t2 = t / ks, ky = t2 % ks, co = t2 / ks;
+  const float v = co < Cout ? w[((co * Cin + ci) * ks + ky) * ks + kx] : 0.f;
+  out[i] = from_f32<O>(v);
+}
+
+extern "C" int ivit_pack_conv_weight(int dtype, const float* w, long Cout, long Cin, long ks, long Cout_pad, void* out,
+                                     void* stream) {
+  hipStream_t st = ivit_stream(stream);
+  const long n = Cout_pad * ks * ks * Cin;
+  if (dtype == IVIT_BF16)
+    hipLaunchKernelGGL(pack_conv_kernel<bf16>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, w, Cout, Cin, ks, Cout_pad,
+                       (bf16*)out);
+  else
+    hipLaunchKernelGGL(pack_conv_kernel<float>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, w, Cout, Cin, ks, Cout_pad,
+                       (float*)out);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+__global__ void unpack_conv_grad_kernel(const float* __restrict__ gp, long Cout, long Cin, long ks, float* out,
+                                        int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = Cout * Cin * ks * ks;
+  if (i >= n) return;
+  const long kx = i % ks, t = i / ks, ky = t % ks, t2 = t / ks, ci = t2 % Cin, co = t2 / Cin;
+  const float v = gp[((co * ks + ky) * ks + kx) * Cin + ci];
+  out[i] = accumulate ? out[i] + v : v;
+}
+
+extern "C" int ivit_unpack_conv_grad(const float* gp, long Cout, long Cin, long ks, float* out, int accumulate,
+                                     void* stream) {
+  hipStream_t st = ivit_stream(stream);
+  const long n = Cout * Cin * ks * ks;
+  hipLaunchKernelGGL(unpack_conv_grad_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, gp, Cout, Cin, ks, out,
+                     accumulate);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}

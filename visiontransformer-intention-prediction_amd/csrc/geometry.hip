@@ -1,0 +1,237 @@
+// Eval-path geometry (utils.py): anchors, axis/rotated IoU matrices, delta decode and
+// torchvision-CPU-exact non-maximum suppression.
+#include "geom.h"
+
+#pragma clang fp contract(off)
+
+using namespace ivit;
+
+namespace {
+
+// utils.py:519-562: centres x=(off_y - (s*gy + s/2))*voxel, y=((s*gx + s/2) - off_x)*voxel;
+// rows location-major, anchor-minor.
+__global__ void anchors_kernel(int fh, int fw, int stride, const float* cfgs, int A, float voxel, float off_x,
+                               float off_y, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)fh * fw * A) return;
+  const int a = (int)(i % A);
+  const long loc = i / A;
+  const int gy = (int)(loc / fw), gx = (int)(loc % fw);
+  const float px = (float)(gx * stride) + (float)stride / 2.0f;
+  const float py = (float)(gy * stride) + (float)stride / 2.0f;
+  out[i * 5 + 0] = (off_y - py) * voxel;
+  out[i * 5 + 1] = (px - off_x) * voxel;
+  out[i * 5 + 2] = cfgs[a * 3 + 0];
+  out[i * 5 + 3] = cfgs[a * 3 + 1];
+  out[i * 5 + 4] = cfgs[a * 3 + 2];
+}
+
+__global__ void iou_matrix_kernel(const float* b1, long n1, const float* b2, long n2, float* out, int rotated) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n1 * n2) return;
+  const long r = i / n2, c = i - r * n2;
+  out[i] = rotated ? rotated_iou(b1 + r * 5, b2 + c * 5) : axis_iou(b1 + r * 5, b2 + c * 5);
+}
+
+// utils.py:227-257
+__global__ void decode_kernel(const float* rel, const float* anchors, const long* idx, long n, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* d = rel + i * 6;
+  const float* a = anchors + (idx ? idx[i] : i) * 5;
+  float* o = out + i * 5;
+  o[0] = d[0] * a[2] + a[0];
+  o[1] = d[1] * a[3] + a[1];
+  o[2] = expf(d[2]) * a[2];
+  o[3] = expf(d[3]) * a[3];
+  const float yaw = a[4] + atan2f(d[4], d[5]);
+  o[4] = atan2f(sinf(yaw), cosf(yaw));
+}
+
+// ---- NMS (torchvision CPU nms_kernel_impl): stable descending sort; f32 corners/areas/IoU;
+//      suppress j if (double)IoU > thr.
+// rank by counting: rank(i) = #{j : s_j > s_i  or  (s_j == s_i and j < i)}
+__global__ void nms_rank_kernel(const float* __restrict__ s, long n, int* __restrict__ order) {
+  __shared__ float tile[256];
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const float si = i < n ? s[i] : 0.f;
+  long rank = 0;
+  for (long j0 = 0; j0 < n; j0 += 256) {
+    __syncthreads();
+    if (j0 + threadIdx.x < n) tile[threadIdx.x] = s[j0 + threadIdx.x];
+    __syncthreads();
+    const int lim = (int)min((long)256, n - j0);
+    for (int k = 0; k < lim; ++k) {
+      const float sj = tile[k];
+      const long j = j0 + k;
+      rank += (sj > si) || (sj == si && j < i);
+    }
+  }
+  if (i < n) order[rank] = (int)i;
+}
+
+__global__ void nms_sorted_boxes_kernel(const float* __restrict__ b, const int* __restrict__ order, long n,
+                                        float* __restrict__ sb) {
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const float* q = b + (long)order[p] * 5;
+  const float x1 = q[0] - q[2] / 2.f, y1 = q[1] - q[3] / 2.f, x2 = q[0] + q[2] / 2.f, y2 = q[1] + q[3] / 2.f;
+  sb[p * 5 + 0] = x1;
+  sb[p * 5 + 1] = y1;
+  sb[p * 5 + 2] = x2;
+  sb[p * 5 + 3] = y2;
+  sb[p * 5 + 4] = (x2 - x1) * (y2 - y1);
+}
+
+// mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr.
+__global__ void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, double thr,
+                                unsigned long long* __restrict__ mask) {
+  const int cb = blockIdx.x, rb = blockIdx.y;
+  if (cb < rb) return;
+  __shared__ float cbx[64][5];
+  const int t = threadIdx.x;
+  const long cj = (long)cb * 64 + t;
+  if (cj < n)
+    for (int k = 0; k < 5; ++k) cbx[t][k] = sb[cj * 5 + k];
+  __syncthreads();
+  const long i = (long)rb * 64 + t;
+  if (i >= n) return;
+  const float ix1 = sb[i * 5 + 0], iy1 = sb[i * 5 + 1], ix2 = sb[i * 5 + 2], iy2 = sb[i * 5 + 3],
+              ia = sb[i * 5 + 4];
+  unsigned long long bits = 0;
+  const int lim = (int)min((long)64, n - (long)cb * 64);
+  for (int k = 0; k < lim; ++k) {
+    const long j = (long)cb * 64 + k;
+    if (j <= i) continue;
+    const float xx1 = fmaxf(ix1, cbx[k][0]), yy1 = fmaxf(iy1, cbx[k][1]);
+    const float xx2 = fminf(ix2, cbx[k][2]), yy2 = fminf(iy2, cbx[k][3]);
+    const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+    const float inter = w * h;
+    const float ovr = inter / ((ia + cbx[k][4]) - inter);
+    if ((double)ovr > thr) bits |= 1ull << k;
+  }
+  mask[i * nw + cb] = bits;
+}
+
+constexpr int NMS_MAXW = 1024;  // n <= 65536
+
+__global__ __launch_bounds__(256) void nms_scan_kernel(const unsigned long long* __restrict__ mask, long n, int nw,
+                                                       const int* __restrict__ order, long* __restrict__ keep,
+                                                       long* __restrict__ count) {
+  __shared__ unsigned long long removed[NMS_MAXW];
+  __shared__ unsigned long long kept_s;
+  __shared__ long cnt_s;
+  for (int w = threadIdx.x; w < nw; w += 256) removed[w] = 0ull;
+  if (threadIdx.x == 0) cnt_s = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (int c = 0; c < nw; ++c) {
+    if (threadIdx.x < 64) {
+      const long row = (long)c * 64 + lane;
+      const unsigned long long diag = row < n ? mask[row * nw + c] : 0ull;
+      unsigned long long w = removed[c];
+      unsigned long long kept = 0ull;
+      const int lim = (int)min((long)64, n - (long)c * 64);
+      for (int i = 0; i < lim; ++i) {
+        const unsigned long long d = __shfl(diag, i, 64);
+        if (!((w >> i) & 1ull)) {
+          kept |= 1ull << i;
+          w |= d;
+        }
+      }
+      const long base = cnt_s;
+      if ((kept >> lane) & 1ull) {
+        const unsigned long long below = lane ? (kept & ((1ull << lane) - 1ull)) : 0ull;
+        keep[base + __popcll(below)] = order[row];
+      }
+      if (lane == 0) {
+        kept_s = kept;
+        cnt_s = base + __popcll(kept);
+      }
+    }
+    __syncthreads();
+    const unsigned long long kept = kept_s;
+    if (kept) {
+      for (int wc = c + 1 + threadIdx.x; wc < nw; wc += 256) {
+        unsigned long long acc = removed[wc];
+        unsigned long long kb = kept;
+        while (kb) {
+          const int i = __ffsll((long long)kb) - 1;
+          kb &= kb - 1;
+          acc |= mask[((long)c * 64 + i) * nw + wc];
+        }
+        removed[wc] = acc;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *count = cnt_s;
+}
+
+}  // namespace
+
+extern "C" int ivit_generate_anchors(long bev_h, long bev_w, long stride, const float* cfgs, long A, float voxel,
+                                     float off_x, float off_y, float* out, void* stream) {
+  const int fh = (int)(bev_h / stride), fw = (int)(bev_w / stride);
+  const long n = (long)fh * fw * A;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(anchors_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), fh, fw, (int)stride,
+                     cfgs, (int)A, voxel, off_x, off_y, out);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_axis_iou(const float* b1, long n1, const float* b2, long n2, float* out, void* stream) {
+  if (n1 * n2 <= 0) return 0;
+  hipLaunchKernelGGL(iou_matrix_kernel, dim3(ivit_cdiv(n1 * n2, 256)), dim3(256), 0, ivit_stream(stream), b1, n1, b2,
+                     n2, out, 0);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_rotated_iou(const float* b1, long n1, const float* b2, long n2, float* out, void* stream) {
+  if (n1 * n2 <= 0) return 0;
+  hipLaunchKernelGGL(iou_matrix_kernel, dim3(ivit_cdiv(n1 * n2, 128)), dim3(128), 0, ivit_stream(stream), b1, n1, b2,
+                     n2, out, 1);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_decode_boxes(const float* rel, const float* anchors, const long* idx, long n, float* out,
+                                 void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(decode_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), rel, anchors, idx, n,
+                     out);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" long ivit_nms_workspace(long n) {
+  const long nw = (n + 63) / 64;
+  return n * 4 + n * 5 * 4 + n * nw * 8 + 64;
+}
+
+extern "C" int ivit_nms(const float* boxes_xywha, const float* scores, long n, double iou_thr, long* keep, long* count,
+                        void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(n <= 64L * NMS_MAXW, "ivit_nms: n=%ld exceeds %d", n, 64 * NMS_MAXW);
+  IVIT_CHECK_ARG(work_bytes >= ivit_nms_workspace(n), "ivit_nms: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  if (n <= 0) {
+    (void)hipMemsetAsync(count, 0, sizeof(long), st);
+    IVIT_LAUNCH_CHECK();
+    return 0;
+  }
+  const int nw = (int)((n + 63) / 64);
+  char* w = (char*)work;
+  int* order = (int*)w;
+  w += (n * 4 + 15) / 16 * 16;
+  float* sb = (float*)w;
+  w += (n * 20 + 15) / 16 * 16;
+  unsigned long long* mask = (unsigned long long*)w;
+  hipLaunchKernelGGL(nms_rank_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, scores, n, order);
+  hipLaunchKernelGGL(nms_sorted_boxes_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, boxes_xywha, order, n, sb);
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(nw, nw), dim3(64), 0, st, sb, n, nw, iou_thr, mask);
+  hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(256), 0, st, mask, n, nw, order, keep, count);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,183 @@
+"""Parameter-container modules with torch.nn-compatible names/shapes (so reference
+checkpoints load) whose forwards run the ivit HIP kernels. The fused model path
+(``model_vit.IntentNetViT.forward``) bypasses these per-module forwards and calls the fused
+Functions in ``ops.py`` directly; these forwards serve standalone sub-module calls."""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+import ops
+from _lib import ACT_NONE, BF16, F32
+
+
+def _cdt(dtype):
+    return BF16 if dtype == torch.bfloat16 else F32
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, cdt):
+        shp = x.shape
+        cd = torch.bfloat16 if cdt == BF16 else torch.float32
+        x2 = ops.cast(x.reshape(-1, shp[-1]).contiguous(), cd)
+        wc = ops.cast(w, cd)
+        y, _ = ops.linear_fwd(x2, wc, b, cdt, out_dtype=torch.float32)
+        ctx.save_for_backward(x2, wc)
+        ctx.cdt, ctx.shp = cdt, shp
+        return y.reshape(*shp[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wc = ctx.saved_tensors
+        cd = torch.bfloat16 if ctx.cdt == BF16 else torch.float32
+        d2 = ops.cast(dy.reshape(-1, dy.shape[-1]).contiguous(), cd)
+        dx = ops.linear_dgrad(d2, wc, ctx.cdt, torch.float32)
+        dw, db = ops.linear_wgrad(d2, x2, ctx.cdt)
+        return dx.reshape(ctx.shp), dw, db, None
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, eps):
+        shp = x.shape
+        x2 = x.reshape(-1, shp[-1]).float().contiguous()
+        y, m, r = ops.layernorm_fwd(x2, g, b, eps, torch.float32)
+        ctx.save_for_backward(x2, g, m, r)
+        ctx.shp = shp
+        return y.reshape(shp)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, g, m, r = ctx.saved_tensors
+        dx, _, dg, db = ops.layernorm_bwd(x2, g, m, r, dy.reshape(x2.shape).float().contiguous())
+        return dx.reshape(ctx.shp), dg, db, None
+
+
+class _Conv2dFn(torch.autograd.Function):
+    """NCHW stride-1 same-padding conv through the NHWC implicit-GEMM kernels."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cdt):
+        B, C, H, W = x.shape
+        cd = torch.bfloat16 if cdt == BF16 else torch.float32
+        xh = ops.cast(x.permute(0, 2, 3, 1).contiguous(), cd).reshape(B * H * W, C)
+        wp = ops.pack_conv(w, cdt)
+        y = ops.conv_fwd(xh, B, H, W, wp, b, cdt, torch.float32)
+        ctx.save_for_backward(xh, wp)
+        ctx.meta = (B, C, H, W, w.shape, cdt, b is not None)
+        return y.reshape(B, H, W, -1).permute(0, 3, 1, 2).contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        xh, wp = ctx.saved_tensors
+        B, C, H, W, wshape, cdt, has_b = ctx.meta
+        cd = torch.bfloat16 if cdt == BF16 else torch.float32
+        Cout, k = wshape[0], wshape[2]
+        dyh = ops.cast(dy.permute(0, 2, 3, 1).contiguous(), cd).reshape(B * H * W, Cout)
+        dx = ops.conv_dgrad(dyh, B, H, W, wp, cdt, torch.float32)
+        gp, db = ops.conv_wgrad(dyh, xh, B, H, W, C, Cout, k, cdt, want_bias=has_b)
+        dw = ops.unpack_conv_grad(gp, Cout, C, k)
+        return dx.reshape(B, H, W, C).permute(0, 3, 1, 2).contiguous(), dw, db, None
+
+
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, rm, rv, nbt, training, momentum, eps, relu, resid):
+        B, C, H, W = x.shape
+        xh = x.permute(0, 2, 3, 1).contiguous().reshape(-1, C).float()
+        st = ops.bn_forward(xh, g, b, rm, rv, training, momentum, eps, nbt=nbt if training else None)
+        rh = None if resid is None else resid.permute(0, 2, 3, 1).contiguous().reshape(-1, C).float()
+        y = ops.bn_apply(xh, st, g, b, torch.float32, resid=rh, relu=relu)
+        ctx.save_for_backward(xh, y, g)
+        ctx.st, ctx.meta = st, (B, C, H, W, relu, resid is not None)
+        return y.reshape(B, H, W, C).permute(0, 3, 1, 2).contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        xh, y, g = ctx.saved_tensors
+        B, C, H, W, relu, has_r = ctx.meta
+        dyh = dy.permute(0, 2, 3, 1).contiguous().reshape(-1, C).float()
+        dx, dr, dg, db = ops.bn_backward(xh, y, dyh, ctx.st, g, relu, torch.float32, want_dr=has_r)
+
+        def back(t):
+            return None if t is None else t.reshape(B, H, W, C).permute(0, 3, 1, 2).contiguous()
+        return back(dx), dg, db, None, None, None, None, None, None, None, back(dr)
+
+
+class Linear(nn.Module):
+    def __init__(self, in_features, out_features, bias=True):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
+        self.bias = nn.Parameter(torch.zeros(out_features)) if bias else None
+        nn.init.trunc_normal_(self.weight, std=0.02)
+
+    def forward(self, x):
+        return _LinearFn.apply(x, self.weight, self.bias, _cdt(getattr(self, "compute_dtype", torch.float32)))
+
+
+class LayerNorm(nn.Module):
+    def __init__(self, dim, eps=1e-5):
+        super().__init__()
+        self.normalized_shape, self.eps = (dim,), eps
+        self.weight = nn.Parameter(torch.ones(dim))
+        self.bias = nn.Parameter(torch.zeros(dim))
+
+    def forward(self, x):
+        return _LayerNormFn.apply(x, self.weight, self.bias, self.eps)
+
+
+class Conv2d(nn.Module):
+    """Conv2d parameter container (k x k, stride s, padding p). Standalone forward supports
+    the stride-1 'same' convolutions of the fusion block and heads."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride, self.padding = (kernel_size, kernel_size), (stride, stride), (padding, padding)
+        self.weight = nn.Parameter(torch.empty(out_channels, in_channels, kernel_size, kernel_size))
+        self.bias = nn.Parameter(torch.empty(out_channels)) if bias else None
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            bound = 1 / math.sqrt(in_channels * kernel_size * kernel_size)
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, x):
+        k = self.kernel_size[0]
+        if self.stride[0] != 1 or self.padding[0] != k // 2:
+            raise NotImplementedError("ivit Conv2d standalone forward: stride 1, same padding only")
+        return _Conv2dFn.apply(x, self.weight, self.bias, _cdt(getattr(self, "compute_dtype", torch.float32)))
+
+
+class BatchNorm2d(nn.Module):
+    def __init__(self, num_features, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.num_features, self.eps, self.momentum = num_features, eps, momentum
+        self.weight = nn.Parameter(torch.ones(num_features))
+        self.bias = nn.Parameter(torch.zeros(num_features))
+        self.register_buffer("running_mean", torch.zeros(num_features))
+        self.register_buffer("running_var", torch.ones(num_features))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def forward(self, x, relu=False, resid=None):
+        return _BatchNormFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                  self.num_batches_tracked, self.training, self.momentum, self.eps, relu, resid)
+
+
+class GELU(nn.Module):
+    """Marker module (exact-erf GELU). In the fused path it is the adapter GEMM epilogue."""
+
+    def forward(self, x):
+        return F.gelu(x)
+
+
+class ReLU(nn.Module):
+    def __init__(self, inplace=False):
+        super().__init__()
+
+    def forward(self, x):
+        return F.relu(x)

@@ -1,0 +1,88 @@
+"""DetectionIntentionLoss (loss.py:10-206 of the reference) on device.
+
+Same constructor arguments, same forward signature and the same returned dict keys. The
+whole assignment + focal/Smooth-L1/CE computation is four HIP kernels with no host
+synchronisation (the reference syncs per GT and per `.item()`); ``num_pos_anchors`` is
+therefore returned as a 0-dim device tensor (callers in train_vit.py already handle both).
+
+Intention down-sampling draws one uniform per anchor on the device (``keep_generator``)
+instead of the reference's per-class CPU-order ``torch.rand`` draws: same Bernoulli(0.15)
+law, different random stream. ``forward(..., intent_keep=mask)`` injects the mask for
+parity tests.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+import ops
+from constants import DOMINANT_CLASSES_FOR_DOWNSAMPLING, INTENTION_DOWNSAMPLE_RATIO
+
+
+def pack_gt(gt_list, device):
+    """gt_list[b] = {'boxes_xywha': (G,5), 'intentions': (G,)} → padded device tensors.
+    A missing/malformed entry or G == 0 means "all anchors negative" (loss.py:69-79)."""
+    B = len(gt_list)
+    ok = [isinstance(g, dict) and "boxes_xywha" in g and "intentions" in g for g in gt_list]
+    counts = [int(g["boxes_xywha"].shape[0]) if o else 0 for g, o in zip(gt_list, ok)]
+    G = max(1, max(counts) if counts else 1)
+    gt = torch.zeros((B, G, 5), dtype=torch.float32)
+    gi = torch.zeros((B, G), dtype=torch.int32)
+    for b, (g, o, n) in enumerate(zip(gt_list, ok, counts)):
+        if o and n:
+            gt[b, :n] = g["boxes_xywha"].detach().float().cpu()
+            gi[b, :n] = g["intentions"].detach().cpu().to(torch.int32)
+    ng = torch.tensor(counts, dtype=torch.int32)
+    return (gt.to(device, non_blocking=True), ng.to(device, non_blocking=True), gi.to(device, non_blocking=True))
+
+
+class DetectionIntentionLoss(nn.Module):
+    def __init__(self, iou_threshold=0.6, neg_iou_threshold=0.45, box_weight=1.0, cls_weight=1.0, intent_weight=0.5,
+                 intention_class_weights=None, use_rotated_iou=False, focal_loss_alpha=0.25, focal_loss_gamma=2.0,
+                 smooth_l1_beta=1.0 / 9.0, apply_intention_downsampling=True,
+                 dominant_intentions=DOMINANT_CLASSES_FOR_DOWNSAMPLING,
+                 intention_downsample_ratio=INTENTION_DOWNSAMPLE_RATIO):
+        super().__init__()
+        self.iou_threshold, self.neg_iou_threshold = iou_threshold, neg_iou_threshold
+        self.box_weight, self.cls_weight, self.intent_weight = box_weight, cls_weight, intent_weight
+        self.use_rotated_iou = use_rotated_iou
+        self.focal_loss_alpha, self.focal_loss_gamma, self.smooth_l1_beta = focal_loss_alpha, focal_loss_gamma, smooth_l1_beta
+        self.apply_intention_downsampling = apply_intention_downsampling
+        self.dominant_intentions = set(dominant_intentions)
+        self.intention_downsample_keep_prob = 1.0 - intention_downsample_ratio
+        w = None
+        if not apply_intention_downsampling and intention_class_weights is not None:
+            w = torch.as_tensor(intention_class_weights, dtype=torch.float32)
+        self.register_buffer("final_intention_class_weights", w)
+        self.keep_generator = None
+
+    def _cfg(self, device):
+        dom = 0
+        for d in self.dominant_intentions:
+            dom |= 1 << int(d)
+        cw = self.final_intention_class_weights
+        return {"dominant_mask": dom, "downsampling": self.apply_intention_downsampling,
+                "class_w": None if cw is None else cw.to(device).float().contiguous(),
+                "pos_thr": self.iou_threshold, "neg_thr": self.neg_iou_threshold, "alpha": self.focal_loss_alpha,
+                "gamma": self.focal_loss_gamma, "beta": self.smooth_l1_beta, "w_cls": self.cls_weight,
+                "w_box": self.box_weight, "w_int": self.intent_weight, "rotated": self.use_rotated_iou}
+
+    def forward(self, cls_logits, box_preds, intention_logits, anchors, gt_list, intent_keep=None):
+        B = cls_logits.shape[0]
+        NA = anchors.shape[0]
+        dev = cls_logits.device
+        anchors = anchors.to(dev).float().contiguous()
+        gt, ng, gi = pack_gt(gt_list, dev)
+        keep = None
+        if self.apply_intention_downsampling:
+            if intent_keep is not None:
+                keep = intent_keep.to(dev).float().reshape(B, NA).contiguous()
+            else:
+                u = torch.rand((B, NA), device=dev, generator=self.keep_generator)
+                keep = (u < self.intention_downsample_keep_prob).float()
+        cls = cls_logits.float().reshape(B, NA)
+        box = box_preds.float().reshape(B, NA, 6)
+        it = intention_logits.float().reshape(B, NA, -1)
+        loss, stats = ops.DetLossFn.apply(cls, box, it, anchors, gt, ng, gi, keep, self._cfg(dev))
+        return {"loss": loss, "cls_loss": stats[6].detach(), "box_loss": stats[7].detach(),
+                "intent_loss": stats[8].detach(), "num_pos_anchors": stats[3].detach().round().long()}

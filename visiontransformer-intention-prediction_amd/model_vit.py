@@ -1,0 +1,205 @@
+"""IntentNetViT / TwoStreamViTBackbone / BasicBlock with the reference's constructor
+signatures, attributes and state_dict keys (model_vit.py:1-184), running on the MI355X
+HIP kernels.
+
+``IntentNetViT.forward`` = 2 x (PatchEmbedFn + 12 ViTBlockFn) + NeckFn (final norms,
+adapters, fusion, both heads). ``set_compute_dtype(torch.bfloat16)`` selects the bf16 MFMA
+path (f32 master weights, f32 residual stream / statistics / loss); the default f32 path is
+the exact-f32 parity path.
+"""
+from __future__ import annotations
+
+import warnings
+
+import torch
+import torch.nn as nn
+
+import ops
+import vit as timm_like
+from _lib import BF16, F32
+from constants import GRID_HEIGHT_PX, GRID_WIDTH_PX, LIDAR_TOTAL_CHANNELS, MAP_CHANNELS, NUM_INTENTION_CLASSES
+from heads import DetectionHead, IntentionHead
+from layers import GELU, BatchNorm2d, Conv2d, LayerNorm, Linear, ReLU
+
+
+def conv3x3_for_basic(in_planes, out_planes, stride=1, kernel_size=3):
+    return Conv2d(in_planes, out_planes, kernel_size=kernel_size, stride=stride, padding=(kernel_size - 1) // 2,
+                  bias=False)
+
+
+def conv1x1_for_basic(in_planes, out_planes, stride=1):
+    return Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=False)
+
+
+class BasicBlock(nn.Module):
+    """model_vit.py:19-34: relu(bn2(conv2(relu(bn1(conv1 x)))) + identity)."""
+    expansion: int = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, kernel_size=3):
+        super().__init__()
+        if stride != 1:
+            raise NotImplementedError("ivit fusion BasicBlock: stride 1 only (the reference default)")
+        self.conv1 = conv3x3_for_basic(inplanes, planes, stride, kernel_size=kernel_size)
+        self.bn1 = BatchNorm2d(planes)
+        self.relu = ReLU(inplace=True)
+        self.conv2 = conv3x3_for_basic(planes, planes, kernel_size=kernel_size)
+        self.bn2 = BatchNorm2d(planes)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample[1](self.downsample[0](x))
+        out = self.bn1(self.conv1(x), relu=True)
+        return self.bn2(self.conv2(out), relu=True, resid=identity)
+
+
+class TwoStreamViTBackbone(nn.Module):
+    def __init__(self, lidar_input_channels=LIDAR_TOTAL_CHANNELS, map_input_channels=MAP_CHANNELS,
+                 vit_model_name_lidar="vit_small_patch8_224", vit_model_name_map="vit_small_patch8_224",
+                 pretrained_lidar=False, pretrained_map=False, img_size=(GRID_HEIGHT_PX, GRID_WIDTH_PX),
+                 drop_path_rate_lidar=0.1, drop_path_rate_map=0.1, lidar_adapter_out_channels=192,
+                 map_adapter_out_channels=192, fusion_block_planes=512, fusion_block_layers=2,
+                 fusion_block_kernel_size=3, fusion_block_stride=1, res_block_type=BasicBlock):
+        super().__init__()
+        self.img_size = tuple(img_size)
+        self.lidar_adapter_out_channels = lidar_adapter_out_channels
+        self.map_adapter_out_channels = map_adapter_out_channels
+        self.vit_lidar = timm_like.create_model(vit_model_name_lidar, pretrained=pretrained_lidar,
+                                                in_chans=lidar_input_channels, img_size=self.img_size,
+                                                drop_path_rate=drop_path_rate_lidar)
+        self.vit_lidar.head = nn.Identity()
+        self.lidar_embed_dim = self.vit_lidar.embed_dim
+        self.lidar_num_prefix_tokens = self.vit_lidar.num_prefix_tokens
+        self.lidar_grid_size = tuple(self.vit_lidar.patch_embed.grid_size)
+        self.vit_map = timm_like.create_model(vit_model_name_map, pretrained=pretrained_map,
+                                              in_chans=map_input_channels, img_size=self.img_size,
+                                              drop_path_rate=drop_path_rate_map)
+        self.vit_map.head = nn.Identity()
+        self.map_embed_dim = self.vit_map.embed_dim
+        self.map_num_prefix_tokens = self.vit_map.num_prefix_tokens
+        self.map_grid_size = tuple(self.vit_map.patch_embed.grid_size)
+        if self.lidar_grid_size != self.map_grid_size:
+            raise NotImplementedError("ivit: LiDAR and map patch grids must match (the reference's bilinear "
+                                      "re-grid path, model_vit.py:139, is not part of the hot path)")
+        self.feature_map_grid_h, self.feature_map_grid_w = self.lidar_grid_size
+        self.adapter_lidar = nn.Sequential(LayerNorm(self.lidar_embed_dim),
+                                           Linear(self.lidar_embed_dim, lidar_adapter_out_channels), GELU())
+        self.adapter_map = nn.Sequential(LayerNorm(self.map_embed_dim),
+                                         Linear(self.map_embed_dim, map_adapter_out_channels), GELU())
+        self.fusion_input_channels = lidar_adapter_out_channels + map_adapter_out_channels
+        self.fusion_block_stride = fusion_block_stride
+        self.fusion_block = self._make_fusion_layer(res_block_type, fusion_block_planes, fusion_block_layers,
+                                                    stride=fusion_block_stride,
+                                                    current_inplanes=self.fusion_input_channels,
+                                                    kernel_size_for_block=fusion_block_kernel_size)
+        self.final_feature_channels = fusion_block_planes * res_block_type.expansion
+        self.fusion_layers = fusion_block_layers
+
+    def _get_patch_info(self, vit_model, stream_name=""):
+        pe = vit_model.patch_embed
+        return tuple(pe.grid_size), pe.num_patches
+
+    def _make_fusion_layer(self, block, planes, num_blocks, stride=1, current_inplanes=0, kernel_size_for_block=3):
+        downsample = None
+        outc = planes * block.expansion
+        if stride != 1 or current_inplanes != outc:
+            downsample = nn.Sequential(conv1x1_for_basic(current_inplanes, outc, stride), BatchNorm2d(outc))
+        layers = [block(current_inplanes, planes, stride, downsample, kernel_size=kernel_size_for_block)]
+        for _ in range(1, num_blocks):
+            layers.append(block(outc, planes, kernel_size=kernel_size_for_block))
+        return nn.Sequential(*layers)
+
+    # neck parameters in NeckFn order (names relative to the backbone / model)
+    def neck_names(self):
+        names = []
+        for s in ("lidar", "map"):
+            names += [f"vit_{s}.norm.weight", f"vit_{s}.norm.bias"]
+        for s in ("lidar", "map"):
+            names += [f"adapter_{s}.0.weight", f"adapter_{s}.0.bias", f"adapter_{s}.1.weight", f"adapter_{s}.1.bias"]
+        for n, _ in self.fusion_block.named_parameters():
+            names.append("fusion_block." + n)
+        for n, _ in self.fusion_block.named_buffers():
+            names.append("fusion_block." + n)
+        return names
+
+    def _cdt(self):
+        return BF16 if getattr(self, "compute_dtype", torch.float32) == torch.bfloat16 else F32
+
+    def stream_tokens(self, lidar_bev, map_bev):
+        return self.vit_lidar.forward_tokens(lidar_bev), self.vit_map.forward_tokens(map_bev)
+
+    def forward(self, lidar_bev, map_bev):
+        """model_vit.py:134-142 → fused feature map (B, C, Hf, Wf) f32."""
+        tl, tm = self.stream_tokens(lidar_bev, map_bev)
+        names = self.neck_names()
+        tens = _lookup(self, names)
+        B = lidar_bev.shape[0]
+        Hf, Wf = self.feature_map_grid_h, self.feature_map_grid_w
+        meta = (B, Hf, Wf, self._cdt(), self.training, 0, 0, self.fusion_layers, tuple(names))
+        feat = ops.NeckFn.apply(tl, tm, meta, *tens)[0]
+        return feat.reshape(B, Hf, Wf, -1).permute(0, 3, 1, 2)
+
+
+def _lookup(root, names):
+    sd = dict(root.named_parameters())
+    sd.update(dict(root.named_buffers()))
+    return [sd[n] for n in names]
+
+
+class IntentNetViT(nn.Module):
+    def __init__(self, backbone_cfg: dict | None = None, head_cfg: dict | None = None):
+        super().__init__()
+        if backbone_cfg is None:
+            backbone_cfg = {}
+        backbone_cfg.setdefault("vit_model_name_lidar", "vit_small_patch8_224")
+        backbone_cfg.setdefault("vit_model_name_map", "vit_small_patch8_224")
+        backbone_cfg.setdefault("pretrained_lidar", False)
+        backbone_cfg.setdefault("pretrained_map", False)
+        backbone_cfg.setdefault("img_size", (GRID_HEIGHT_PX, GRID_WIDTH_PX))
+        backbone_cfg.setdefault("lidar_adapter_out_channels", 192)
+        backbone_cfg.setdefault("map_adapter_out_channels", 192)
+        backbone_cfg.setdefault("fusion_block_planes", 512)
+        backbone_cfg.setdefault("fusion_block_layers", 2)
+        backbone_cfg.setdefault("fusion_block_kernel_size", 3)
+        backbone_cfg.setdefault("fusion_block_stride", 1)
+        self.backbone = TwoStreamViTBackbone(**backbone_cfg)
+        fc = self.backbone.final_feature_channels
+        if head_cfg is None:
+            head_cfg = {}
+        self.det_head = DetectionHead(in_channels=fc, **head_cfg)
+        self.intention_head = IntentionHead(in_channels=fc, num_classes=NUM_INTENTION_CLASSES, **head_cfg)
+        try:
+            stride = int(backbone_cfg.get("vit_model_name_lidar", "vit_small_patch8_224").split("_patch")[-1]
+                         .split("_")[0])
+        except ValueError:
+            stride = 8
+            warnings.warn("Could not parse patch stride from ViT name, defaulting to 8.")
+        self.effective_head_stride = stride * backbone_cfg.get("fusion_block_stride", 1)
+        self.compute_dtype = torch.float32
+
+    def set_compute_dtype(self, dtype):
+        """torch.float32 (exact-f32 parity path) or torch.bfloat16 (bf16 MFMA throughput path)."""
+        assert dtype in (torch.float32, torch.bfloat16)
+        for m in self.modules():
+            m.compute_dtype = dtype
+        return self
+
+    def _neck_meta(self, B):
+        bb = self.backbone
+        names = bb.neck_names() + ["det_head.conv.weight", "det_head.conv.bias", "intention_head.conv.weight",
+                                   "intention_head.conv.bias"]
+        cdt = BF16 if self.compute_dtype == torch.bfloat16 else F32
+        meta = (B, bb.feature_map_grid_h, bb.feature_map_grid_w, cdt, self.training, self.det_head.num_anchors,
+                self.intention_head.num_classes, bb.fusion_layers, tuple(names))
+        return meta, names
+
+    def forward(self, lidar_bev, map_bev):
+        """model_vit.py:179-185 → cls (B, A*Hf*Wf, 1), box (.., 6), intent (.., K), all f32."""
+        B = lidar_bev.shape[0]
+        tl, tm = self.backbone.stream_tokens(lidar_bev, map_bev)
+        meta, names = self._neck_meta(B)
+        bb = dict(self.backbone.named_parameters())
+        bb.update(dict(self.backbone.named_buffers()))
+        hd = dict(self.named_parameters())
+        tens = [hd[n] if n.startswith(("det_head", "intention_head")) else bb[n] for n in names]
+        return ops.NeckFn.apply(tl, tm, meta, *tens)

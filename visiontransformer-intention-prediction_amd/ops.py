@@ -1,0 +1,496 @@
+"""Autograd layer over libivit_hip: every differentiable op of the IntentNetViT hot path
+as a ``torch.autograd.Function`` whose forward and backward launch only the hand-written
+HIP kernels (through the C ABI in ``include/ivit.h``). PyTorch is used for device memory,
+streams and autograd plumbing; there is no eager/ATen fallback for the compute.
+
+Granularity (fused for HBM traffic and launch count, coarse enough for DDP overlap):
+  * ``PatchEmbedFn``  timm PatchEmbed + CLS + pos_embed            (model_vit.py:64,71 → timm)
+  * ``ViTBlockFn``    one pre-norm transformer block                (timm Block, ×12 per stream)
+  * ``NeckFn``        final norms + adapters + fusion BasicBlocks + heads
+                      (model_vit.py:116-142, 179-185; heads.py)
+  * ``DetLossFn``     DetectionIntentionLoss                        (loss.py:58-206)
+plus single-op Functions used by the standalone module forwards.
+"""
+from __future__ import annotations
+
+import torch
+
+from _lib import ACT_GELU, ACT_NONE, BF16, F32, dt, lib, ptr, stream, tdtype, workspace
+
+
+def _code(dtype):
+    return BF16 if dtype == torch.bfloat16 else F32
+
+
+def cast(x, dtype):
+    if x.dtype == dtype:
+        return x
+    y = torch.empty(x.shape, dtype=dtype, device=x.device)
+    lib.ivit_cast(ptr(x), dt(x), ptr(y), dt(y), x.numel(), stream())
+    return y
+
+
+# ------------------------------------------------------------------------------ primitives
+def linear_fwd(x, w, b, cdt, act=ACT_NONE, out_dtype=None, want_pre=False, resid=None, row_scale=None, rps=1,
+               out=None, pre=None):
+    """x [M, K] (cdt), w [N, K] (cdt) → act(x w^T + b); resid → f32 residual form."""
+    M, K = x.shape[0], x.shape[-1]
+    N = w.shape[0]
+    if resid is not None:
+        out = torch.empty((M, N), dtype=torch.float32, device=x.device) if out is None else out
+        lib.ivit_linear_fwd(cdt, ptr(x), x.stride(0), ptr(w), ptr(b), M, N, K, ACT_NONE, ptr(out), out.stride(0), F32,
+                            None, ptr(resid), resid.stride(0), ptr(row_scale), rps, stream())
+        return out, None
+    od = tdtype(cdt) if out_dtype is None else out_dtype
+    out = torch.empty((M, N), dtype=od, device=x.device) if out is None else out
+    if want_pre and pre is None:
+        pre = torch.empty((M, N), dtype=od, device=x.device)
+    assert pre is None or pre.stride(0) == out.stride(0)
+    lib.ivit_linear_fwd(cdt, ptr(x), x.stride(0), ptr(w), ptr(b), M, N, K, act, ptr(out), out.stride(0), dt(out),
+                        ptr(pre), None, 0, None, 0, stream())
+    return out, pre
+
+
+def linear_dgrad(dy, w, cdt, out_dtype, gelu_pre=None, out=None):
+    M, N = dy.shape[0], dy.shape[-1]
+    K = w.shape[1]
+    out = torch.empty((M, K), dtype=out_dtype, device=dy.device) if out is None else out
+    lib.ivit_linear_dgrad(cdt, ptr(dy), dy.stride(0), ptr(w), M, N, K, ptr(out), out.stride(0), dt(out),
+                          ptr(gelu_pre), gelu_pre.stride(0) if gelu_pre is not None else 0, stream())
+    return out
+
+
+def linear_wgrad(dy, x, cdt, want_bias=True):
+    M, N = dy.shape[0], dy.shape[-1]
+    K = x.shape[-1]
+    dw = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+    db = torch.empty((N,), dtype=torch.float32, device=dy.device) if want_bias else None
+    ws = workspace(lib.ivit_linear_wgrad_workspace(M, N, K), dy.device)
+    lib.ivit_linear_wgrad(cdt, ptr(dy), dy.stride(0), ptr(x), x.stride(0), M, N, K, ptr(dw), ptr(db), 0, ptr(ws),
+                          ws.numel(), stream())
+    return dw, db
+
+
+def layernorm_fwd(x, g, b, eps, out_dtype, rowmap=(0, 0, 0), M=None):
+    D = x.shape[-1]
+    M = x.shape[0] if M is None else M
+    y = torch.empty((M, D), dtype=out_dtype, device=x.device)
+    mean = torch.empty((M,), dtype=torch.float32, device=x.device)
+    rstd = torch.empty((M,), dtype=torch.float32, device=x.device)
+    lib.ivit_layernorm_fwd(ptr(x), x.stride(0), rowmap[0], rowmap[1], rowmap[2], M, D, ptr(g), ptr(b), eps, ptr(y),
+                           D, dt(y), ptr(mean), ptr(rstd), stream())
+    return y, mean, rstd
+
+
+def layernorm_bwd(x, g, mean, rstd, dy, dres=None, dx=None, xs_dtype=None, row_scale=None, rps=1, rowmap=(0, 0, 0)):
+    M, D = dy.shape[0], dy.shape[-1]
+    if dx is None:
+        dx = torch.empty_like(x, dtype=torch.float32) if dres is None else dres
+    dxs = torch.empty((M, D), dtype=xs_dtype, device=dy.device) if xs_dtype is not None else None
+    dg = torch.empty((D,), dtype=torch.float32, device=dy.device)
+    db = torch.empty((D,), dtype=torch.float32, device=dy.device)
+    ws = workspace(lib.ivit_layernorm_bwd_workspace(M, D), dy.device)
+    lib.ivit_layernorm_bwd(ptr(x), x.stride(0), rowmap[0], rowmap[1], rowmap[2], M, D, ptr(g), ptr(mean), ptr(rstd),
+                           ptr(dy), dy.stride(0), dt(dy), ptr(dres), ptr(dx), dx.stride(0), ptr(dxs),
+                           dt(dxs) if dxs is not None else F32, ptr(row_scale), rps, ptr(dg), ptr(db), 0, ptr(ws),
+                           ws.numel(), stream())
+    return dx, dxs, dg, db
+
+
+class KernelTimer:
+    """Optional HIP-event bracketing of selected C-ABI launches on the current stream
+    (bench.py uses it to measure the roofline kernel's average duration in the timed loop)."""
+    enabled = set()
+    records = {}
+
+    @classmethod
+    def span(cls, name):
+        if name not in cls.enabled:
+            return None
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        cls.records.setdefault(name, []).append((s, e))
+        return e
+
+    @classmethod
+    def mean_ms(cls, name):
+        r = cls.records.get(name, [])
+        return sum(s.elapsed_time(e) for s, e in r) / len(r) if r else float("nan")
+
+
+def attn_fwd(qkv, B, N, H, cdt):
+    D = H * 64
+    out = torch.empty((B * N, D), dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty((B, H, N), dtype=torch.float32, device=qkv.device)
+    ws = workspace(lib.ivit_attn_workspace(cdt, B, N, H, 64, 0), qkv.device)
+    ev = KernelTimer.span("attn_fwd")
+    lib.ivit_attn_fwd(cdt, ptr(qkv), B, N, H, 64, ptr(out), ptr(lse), ptr(ws), ws.numel(), stream())
+    if ev is not None:
+        ev.record()
+    return out, lse
+
+
+def attn_bwd(qkv, out, dout, lse, B, N, H, cdt):
+    dqkv = torch.empty_like(qkv)
+    ws = workspace(lib.ivit_attn_workspace(cdt, B, N, H, 64, 1), qkv.device)
+    lib.ivit_attn_bwd(cdt, ptr(qkv), ptr(out), ptr(dout), ptr(lse), B, N, H, 64, ptr(dqkv), ptr(ws), ws.numel(),
+                      stream())
+    return dqkv
+
+
+def add_act_grad(a, b=None, pre=None, row_scale=None, row_elems=1, out_dtype=None):
+    out = torch.empty(a.shape, dtype=out_dtype or a.dtype, device=a.device)
+    lib.ivit_add_act_grad(ptr(a), dt(a), ptr(b), dt(b) if b is not None else F32, ptr(pre),
+                          dt(pre) if pre is not None else F32, ptr(row_scale), row_elems, ptr(out), dt(out),
+                          a.numel(), stream())
+    return out
+
+
+def pack_conv(w, cdt, cout_pad=None):
+    Cout, Cin, k, _ = w.shape
+    cp = Cout if cout_pad is None else cout_pad
+    out = torch.empty((cp, k, k, Cin), dtype=tdtype(cdt), device=w.device)
+    lib.ivit_pack_conv_weight(cdt, ptr(w), Cout, Cin, k, cp, ptr(out), stream())
+    return out
+
+
+def unpack_conv_grad(gp, Cout, Cin, k):
+    out = torch.empty((Cout, Cin, k, k), dtype=torch.float32, device=gp.device)
+    lib.ivit_unpack_conv_grad(ptr(gp), Cout, Cin, k, ptr(out), 0, stream())
+    return out
+
+
+def conv_fwd(x, B, H, W, wp, bias, cdt, out_dtype):
+    Cout, k, _, Cin = wp.shape
+    y = torch.empty((B * H * W, Cout), dtype=out_dtype, device=x.device)
+    lib.ivit_conv_fwd(cdt, ptr(x), B, H, W, Cin, ptr(wp), ptr(bias), Cout, k, ptr(y), Cout, dt(y), stream())
+    return y
+
+
+def conv_dgrad(dy, B, H, W, wp, cdt, out_dtype):
+    Cout, k, _, Cin = wp.shape
+    dx = torch.empty((B * H * W, Cin), dtype=out_dtype, device=dy.device)
+    lib.ivit_conv_dgrad(cdt, ptr(dy), dy.stride(0), B, H, W, Cout, ptr(wp), Cin, k, ptr(dx), dt(dx), stream())
+    return dx
+
+
+def conv_wgrad(dy, x, B, H, W, Cin, Cout, k, cdt, want_bias=False):
+    gp = torch.empty((Cout, k, k, Cin), dtype=torch.float32, device=dy.device)
+    db = torch.empty((Cout,), dtype=torch.float32, device=dy.device) if want_bias else None
+    ws = workspace(lib.ivit_conv_wgrad_workspace(B, H, W, Cin, Cout, k), dy.device)
+    lib.ivit_conv_wgrad(cdt, ptr(dy), dy.stride(0), ptr(x), B, H, W, Cin, Cout, k, ptr(gp), ptr(db), 0, ptr(ws),
+                        ws.numel(), stream())
+    return gp, db
+
+
+class _BNState:
+    """Per-forward BatchNorm statistics (batch stats in train, running stats in eval)."""
+
+    def __init__(self, mean, invstd):
+        self.mean, self.invstd = mean, invstd
+
+
+def bn_forward(x, g, b, rmean, rvar, training, momentum=0.1, eps=1e-5, nbt=None):
+    M, C = x.shape
+    if training:
+        mean = torch.empty((C,), dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        ws = workspace(lib.ivit_bn_workspace(M, C), x.device)
+        lib.ivit_bn_stats(ptr(x), dt(x), M, C, ptr(mean), ptr(invstd), ptr(rmean), ptr(rvar), momentum, eps, ptr(ws),
+                          ws.numel(), stream())
+        if nbt is not None:
+            nbt.add_(1)
+    else:
+        mean = rmean.clone()
+        invstd = torch.rsqrt(rvar + eps)
+    return _BNState(mean, invstd)
+
+
+def bn_apply(x, st, g, b, out_dtype, resid=None, relu=False):
+    M, C = x.shape
+    y = torch.empty((M, C), dtype=out_dtype, device=x.device)
+    if resid is not None:
+        assert resid.dtype == out_dtype
+    lib.ivit_bn_apply(ptr(x), dt(x), M, C, ptr(st.mean), ptr(st.invstd), ptr(g), ptr(b), ptr(resid), int(relu), ptr(y),
+                      dt(y), stream())
+    return y
+
+
+def bn_backward(x, y, dy, st, g, relu, out_dtype, want_dr=False):
+    M, C = x.shape
+    dx = torch.empty((M, C), dtype=out_dtype, device=x.device)
+    dr = torch.empty((M, C), dtype=out_dtype, device=x.device) if want_dr else None
+    dg = torch.empty((C,), dtype=torch.float32, device=x.device)
+    db = torch.empty_like(dg)
+    ws = workspace(lib.ivit_bn_workspace(M, C), x.device)
+    lib.ivit_bn_bwd(ptr(x), dt(x), ptr(y), dt(y), ptr(dy), dt(dy), M, C, ptr(st.mean), ptr(st.invstd), ptr(g),
+                    int(relu), ptr(dx), dt(dx), ptr(dr), ptr(dg), ptr(db), 0, ptr(ws), ws.numel(), stream())
+    return dx, dr, dg, db
+
+
+# ------------------------------------------------------------------------------ fused Functions
+class PatchEmbedFn(torch.autograd.Function):
+    """timm PatchEmbed(Conv2d k=s=8, bias) → flatten/transpose → cat(CLS) → +pos_embed.
+    img (B, C, H, W) f32 → tokens (B*(Np+1), D) f32. No input gradient (the BEV raster)."""
+
+    @staticmethod
+    def forward(ctx, img, w, b, pos, cls, cdt):
+        B, C, H, W = img.shape
+        D = w.shape[0]
+        Ntok = (H // 8) * (W // 8) + 1
+        wc = cast(w.reshape(D, C * 64), tdtype(cdt))
+        out = torch.empty((B * Ntok, D), dtype=torch.float32, device=img.device)
+        lib.ivit_patch_embed_fwd(cdt, ptr(img), B, C, H, W, ptr(wc), ptr(b), ptr(pos), ptr(cls), D, ptr(out), stream())
+        ctx.save_for_backward(img)
+        ctx.meta = (B, C, H, W, D, cdt, w.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dtok):
+        (img,) = ctx.saved_tensors
+        B, C, H, W, D, cdt, wshape = ctx.meta
+        dtok = cast(dtok.contiguous(), tdtype(cdt))
+        Ntok = (H // 8) * (W // 8) + 1
+        dw = torch.empty(wshape, dtype=torch.float32, device=img.device)
+        db = torch.empty((D,), dtype=torch.float32, device=img.device)
+        dpos = torch.empty((1, Ntok, D), dtype=torch.float32, device=img.device)
+        dcls = torch.empty((1, 1, D), dtype=torch.float32, device=img.device)
+        ws = workspace(lib.ivit_patch_embed_wgrad_workspace(B, C, H, W, D), img.device)
+        lib.ivit_patch_embed_wgrad(cdt, ptr(dtok), ptr(img), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos), ptr(dcls), 0,
+                                   ptr(ws), ws.numel(), stream())
+        return None, dw, db, dpos, dcls, None
+
+
+class ViTBlockFn(torch.autograd.Function):
+    """timm Block: x + dp1(proj(attn(norm1 x))); x + dp2(fc2(gelu(fc1(norm2 x)))).
+    x: (B*N, D) f32 residual stream; GEMM operands in the compute dtype (f32 or bf16)."""
+
+    @staticmethod
+    def forward(ctx, x, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, s1, s2, meta):
+        B, N, H, cdt, eps = meta
+        cd = tdtype(cdt)
+        wq, wp, w1, w2 = cast(qkvw, cd), cast(pw, cd), cast(f1w, cd), cast(f2w, cd)
+        ln1, m1, r1 = layernorm_fwd(x, n1w, n1b, eps, cd)
+        qkv, _ = linear_fwd(ln1, wq, qkvb, cdt)
+        o, lse = attn_fwd(qkv, B, N, H, cdt)
+        x1, _ = linear_fwd(o, wp, pb, cdt, resid=x, row_scale=s1, rps=N)
+        ln2, m2, r2 = layernorm_fwd(x1, n2w, n2b, eps, cd)
+        a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=True)
+        x2, _ = linear_fwd(a, w2, f2b, cdt, resid=x1, row_scale=s2, rps=N)
+        ctx.save_for_backward(x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2)
+        ctx.meta = meta
+        return x2
+
+    @staticmethod
+    def backward(ctx, dx2):
+        (x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2) = ctx.saved_tensors
+        B, N, H, cdt, eps = ctx.meta
+        cd = tdtype(cdt)
+        dx2 = dx2.contiguous()
+        D = x.shape[1]
+        dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
+        dh = linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
+        dW2, db2 = linear_wgrad(dx2s, a, cdt)
+        dln2 = linear_dgrad(dh, w1, cdt, torch.float32)
+        dW1, db1 = linear_wgrad(dh, ln2, cdt)
+        dx1, dx1s, dg2, dbe2 = layernorm_bwd(x1, n2w, m2, r2, dln2, dres=dx2, dx=torch.empty_like(dx2), xs_dtype=cd,
+                                             row_scale=s1, rps=N)
+        do = linear_dgrad(dx1s, wp, cdt, cd)
+        dWp, dbp = linear_wgrad(dx1s, o, cdt)
+        dqkv = attn_bwd(qkv, o, do, lse, B, N, H, cdt)
+        dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
+        dWq, dbq = linear_wgrad(dqkv, ln1, cdt)
+        dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
+        return dx0, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, None, None, None
+
+
+class NeckFn(torch.autograd.Function):
+    """Everything after the ViT blocks (model_vit.py:116-142,179-185; heads.py):
+    final ViT norm (eps 1e-6) → drop CLS → adapter LN(eps 1e-5) → Linear → GELU for each
+    stream, concat to an NHWC (B, Hf, Wf, Cl+Cm) map, fusion BasicBlocks (conv3x3-BN-ReLU-
+    conv3x3-BN + identity/1x1-BN, ReLU), then the det (A*7) + intention (A*K) 3x3 heads as
+    one GEMM, split into (cls, box, intent)."""
+
+    @staticmethod
+    def forward(ctx, tl, tm, meta, *params):
+        (B, Hf, Wf, cdt, training, A, K, layers, names) = meta
+        P = dict(zip(names, params))
+        cd = tdtype(cdt)
+        Np = Hf * Wf
+        Ntok = Np + 1
+        M = B * Np
+        dev = tl.device
+        rm = (Np, Ntok, 1)
+        saved = {}
+        Cl = P["adapter_lidar.1.weight"].shape[0]
+        Cm = P["adapter_map.1.weight"].shape[0]
+        cat = torch.empty((M, Cl + Cm), dtype=cd, device=dev)
+        pre = torch.empty((M, Cl + Cm), dtype=cd, device=dev)
+        for s, t, c0, C in (("lidar", tl, 0, Cl), ("map", tm, Cl, Cm)):
+            y, mf, rf = layernorm_fwd(t, P[f"vit_{s}.norm.weight"], P[f"vit_{s}.norm.bias"], 1e-6, torch.float32,
+                                      rowmap=rm, M=M)
+            z, ma, ra = layernorm_fwd(y, P[f"adapter_{s}.0.weight"], P[f"adapter_{s}.0.bias"], 1e-5, cd)
+            wa = cast(P[f"adapter_{s}.1.weight"], cd)
+            linear_fwd(z, wa, P[f"adapter_{s}.1.bias"], cdt, act=ACT_GELU, out=cat[:, c0:c0 + C],
+                       pre=pre[:, c0:c0 + C])
+            saved[s] = (t, y, mf, rf, z, ma, ra, wa)
+        x = cat
+        bns = {}
+        packs = {}
+        acts = []
+        for li in range(layers):
+            p = f"fusion_block.{li}."
+            w1 = pack_conv(P[p + "conv1.weight"], cdt)
+            w2 = pack_conv(P[p + "conv2.weight"], cdt)
+            c1 = conv_fwd(x, B, Hf, Wf, w1, None, cdt, torch.float32)
+            s1 = bn_forward(c1, P[p + "bn1.weight"], P[p + "bn1.bias"], P[p + "bn1.running_mean"],
+                            P[p + "bn1.running_var"], training, nbt=P.get(p + "bn1.num_batches_tracked"))
+            r1 = bn_apply(c1, s1, P[p + "bn1.weight"], P[p + "bn1.bias"], cd, relu=True)
+            c2 = conv_fwd(r1, B, Hf, Wf, w2, None, cdt, torch.float32)
+            s2 = bn_forward(c2, P[p + "bn2.weight"], P[p + "bn2.bias"], P[p + "bn2.running_mean"],
+                            P[p + "bn2.running_var"], training, nbt=P.get(p + "bn2.num_batches_tracked"))
+            if (p + "downsample.0.weight") in P:
+                wd = pack_conv(P[p + "downsample.0.weight"], cdt)
+                dd = conv_fwd(x, B, Hf, Wf, wd, None, cdt, torch.float32)
+                sd = bn_forward(dd, P[p + "downsample.1.weight"], P[p + "downsample.1.bias"],
+                                P[p + "downsample.1.running_mean"], P[p + "downsample.1.running_var"], training,
+                                nbt=P.get(p + "downsample.1.num_batches_tracked"))
+                idn = bn_apply(dd, sd, P[p + "downsample.1.weight"], P[p + "downsample.1.bias"], cd)
+                bns[p + "ds"] = (dd, sd, idn)
+                packs[p + "ds"] = wd
+            else:
+                idn = x
+            out = bn_apply(c2, s2, P[p + "bn2.weight"], P[p + "bn2.bias"], cd, resid=idn, relu=True)
+            acts.append((x, c1, s1, r1, c2, s2, out))
+            packs[p + "1"], packs[p + "2"] = w1, w2
+            x = out
+        if A == 0:  # backbone-only call (TwoStreamViTBackbone.forward): fused feature map
+            ctx.st = (saved, cat, pre, acts, bns, packs, None, x, 0)
+            ctx.meta, ctx.P = meta, P
+            return (cast(x, torch.float32) if x.dtype != torch.float32 else x.clone(),)
+        Cd, Ci = A * 7, A * K
+        Cp = (Cd + Ci + 7) // 8 * 8
+        wh = torch.cat([P["det_head.conv.weight"], P["intention_head.conv.weight"]], 0)
+        whp = pack_conv(wh, cdt, cout_pad=Cp)
+        bh = torch.zeros((Cp,), dtype=torch.float32, device=dev)
+        bh[:Cd] = P["det_head.conv.bias"]
+        bh[Cd:Cd + Ci] = P["intention_head.conv.bias"]
+        hout = conv_fwd(x, B, Hf, Wf, whp, bh, cdt, torch.float32)
+        cls = torch.empty((B, M // B * A, 1), dtype=torch.float32, device=dev)
+        box = torch.empty((B, M // B * A, 6), dtype=torch.float32, device=dev)
+        intent = torch.empty((B, M // B * A, K), dtype=torch.float32, device=dev)
+        lib.ivit_split_heads(ptr(hout), Cp, M, A, K, ptr(cls), ptr(box), ptr(intent), stream())
+        ctx.st = (saved, cat, pre, acts, bns, packs, whp, x, Cp)
+        ctx.meta = meta
+        ctx.P = P
+        return cls, box, intent
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        (B, Hf, Wf, cdt, training, A, K, layers, names) = ctx.meta
+        saved, cat, pre, acts, bns, packs, whp, x_last, Cp = ctx.st
+        P = ctx.P
+        cd = tdtype(cdt)
+        Np = Hf * Wf
+        M = B * Np
+        dev = cat.device
+        G = {}
+        if A == 0:
+            dx = gouts[0].contiguous().float()
+        else:
+            dcls, dbox, dint = gouts
+            dh = torch.empty((M, Cp), dtype=cd, device=dev)
+            lib.ivit_merge_heads_grad(ptr(dcls.contiguous()), ptr(dbox.contiguous()), ptr(dint.contiguous()), M, A,
+                                      K, ptr(dh), Cp, dt(dh), stream())
+            Cin = x_last.shape[1]
+            gp, dbh = conv_wgrad(dh, x_last, B, Hf, Wf, Cin, Cp, 3, cdt, want_bias=True)
+            Cd, Ci = A * 7, A * K
+            gw = unpack_conv_grad(gp, Cd + Ci, Cin, 3)
+            G["det_head.conv.weight"], G["intention_head.conv.weight"] = gw[:Cd], gw[Cd:]
+            G["det_head.conv.bias"], G["intention_head.conv.bias"] = dbh[:Cd].clone(), dbh[Cd:Cd + Ci].clone()
+            dx = conv_dgrad(dh, B, Hf, Wf, whp, cdt, torch.float32)
+        for li in reversed(range(layers)):
+            p = f"fusion_block.{li}."
+            x, c1, s1, r1, c2, s2, out = acts[li]
+            has_ds = (p + "ds") in bns
+            dc2, dres, G[p + "bn2.weight"], G[p + "bn2.bias"] = bn_backward(c2, out, dx, s2, P[p + "bn2.weight"], True,
+                                                                            cd, want_dr=True)
+            Cm_ = c2.shape[1]
+            gp2, _ = conv_wgrad(dc2, r1, B, Hf, Wf, r1.shape[1], Cm_, 3, cdt)
+            G[p + "conv2.weight"] = unpack_conv_grad(gp2, Cm_, r1.shape[1], 3)
+            dr1 = conv_dgrad(dc2, B, Hf, Wf, packs[p + "2"], cdt, torch.float32)
+            dc1, _, G[p + "bn1.weight"], G[p + "bn1.bias"] = bn_backward(c1, r1, dr1, s1, P[p + "bn1.weight"], True, cd)
+            gp1, _ = conv_wgrad(dc1, x, B, Hf, Wf, x.shape[1], Cm_, 3, cdt)
+            G[p + "conv1.weight"] = unpack_conv_grad(gp1, Cm_, x.shape[1], 3)
+            dxa = conv_dgrad(dc1, B, Hf, Wf, packs[p + "1"], cdt, torch.float32)
+            if has_ds:
+                dd, sd, idn = bns[p + "ds"]
+                ddd, _, G[p + "downsample.1.weight"], G[p + "downsample.1.bias"] = bn_backward(
+                    dd, idn, dres, sd, P[p + "downsample.1.weight"], False, cd)
+                gpd, _ = conv_wgrad(ddd, x, B, Hf, Wf, x.shape[1], Cm_, 1, cdt)
+                G[p + "downsample.0.weight"] = unpack_conv_grad(gpd, Cm_, x.shape[1], 1)
+                dxb = conv_dgrad(ddd, B, Hf, Wf, packs[p + "ds"], cdt, torch.float32)
+            else:
+                dxb = dres
+            if li == 0:
+                # d(adapter pre-activation) = (dxa + dxb) * gelu'(pre)
+                dx = add_act_grad(dxa, dxb, pre=pre, out_dtype=cd)
+            else:
+                dx = add_act_grad(dxa, dxb, out_dtype=torch.float32)
+        dpre = dx
+        Cl = P["adapter_lidar.1.weight"].shape[0]
+        outs = {}
+        for s, c0 in (("lidar", 0), ("map", Cl)):
+            t, y, mf, rf, z, ma, ra, wa = saved[s]
+            C = wa.shape[0]
+            dp = dpre[:, c0:c0 + C]
+            dz = linear_dgrad(dp, wa, cdt, torch.float32)
+            G[f"adapter_{s}.1.weight"], G[f"adapter_{s}.1.bias"] = linear_wgrad(dp, z, cdt)
+            dy, _, G[f"adapter_{s}.0.weight"], G[f"adapter_{s}.0.bias"] = layernorm_bwd(
+                y, P[f"adapter_{s}.0.weight"], ma, ra, dz)
+            dt_ = torch.zeros_like(t)
+            _, _, G[f"vit_{s}.norm.weight"], G[f"vit_{s}.norm.bias"] = layernorm_bwd(
+                t, P[f"vit_{s}.norm.weight"], mf, rf, dy, dx=dt_, rowmap=(Np, Np + 1, 1))
+            outs[s] = dt_
+        grads = [G.get(n) for n in names]
+        del ctx.st, ctx.P
+        return (outs["lidar"], outs["map"], None) + tuple(grads)
+
+
+class DetLossFn(torch.autograd.Function):
+    """DetectionIntentionLoss on device (loss.py:58-206). Returns the 16-float stats vector;
+    element 5 is the loss (0 with no gradient when non-finite, loss.py:190-198)."""
+
+    @staticmethod
+    def forward(ctx, cls, box, intent, anchors, gt, ngt, gint, keep, cfg):
+        B, NA = cls.shape[0], cls.shape[1]
+        K = intent.shape[-1]
+        G = gt.shape[1]
+        dev = cls.device
+        stats = torch.zeros((16,), dtype=torch.float32, device=dev)
+        ws = workspace(lib.ivit_det_loss_workspace(B, NA, G), dev)
+        cls, box, intent = cls.contiguous(), box.contiguous(), intent.contiguous()
+        lib.ivit_det_loss_fwd(ptr(cls), ptr(box), ptr(intent), ptr(anchors), B, NA, K, ptr(gt), ptr(ngt), ptr(gint), G,
+                              ptr(keep), cfg["dominant_mask"], int(cfg["downsampling"]), ptr(cfg.get("class_w")),
+                              cfg["pos_thr"], cfg["neg_thr"], cfg["alpha"], cfg["gamma"], cfg["beta"], cfg["w_cls"],
+                              cfg["w_box"], cfg["w_int"], int(cfg["rotated"]), ptr(stats), ptr(ws), ws.numel(),
+                              stream())
+        ctx.save_for_backward(cls, box, intent, keep, stats, ws)
+        ctx.cfg = cfg
+        ctx.shape = (B, NA, K)
+        ctx.mark_non_differentiable(stats)
+        loss = stats[5:6].clone().reshape(())
+        return loss, stats
+
+    @staticmethod
+    def backward(ctx, gloss, _gstats):
+        cls, box, intent, keep, stats, ws = ctx.saved_tensors
+        B, NA, K = ctx.shape
+        cfg = ctx.cfg
+        g = gloss.reshape(1).float().contiguous()
+        dcls, dbox, dint = torch.empty_like(cls), torch.empty_like(box), torch.empty_like(intent)
+        lib.ivit_det_loss_bwd(ptr(cls), ptr(box), ptr(intent), B, NA, K, ptr(keep), cfg["dominant_mask"],
+                              int(cfg["downsampling"]), ptr(cfg.get("class_w")), cfg["alpha"], cfg["gamma"],
+                              cfg["beta"], cfg["w_cls"], cfg["w_box"], cfg["w_int"], ptr(stats), ptr(g), ptr(dcls),
+                              ptr(dbox), ptr(dint), ptr(ws), ws.numel(), stream())
+        return dcls, dbox, dint, None, None, None, None, None, None

@@ -1,0 +1,70 @@
+"""Fused AdamW (torch.optim.AdamW semantics as used at train_vit.py:130: lr 1e-4, wd 1e-4,
+betas (0.9, 0.999), eps 1e-8, decoupled weight decay) — one HIP launch per parameter group
+over device pointer tables instead of torch's per-tensor foreach kernels."""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from _lib import lib, ptr, stream
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._tables = {}
+
+    def _table(self, tensors, device):
+        key = tuple(t.data_ptr() for t in tensors)
+        tab = self._tables.get(key)
+        if tab is None:
+            tab = torch.tensor(key, dtype=torch.int64).to(device)
+            if len(self._tables) > 64:
+                self._tables.clear()
+            self._tables[key] = tab
+        return tab
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            by_step = {}
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.dtype != torch.float32 or p.grad.dtype != torch.float32 or not p.is_contiguous() \
+                        or not p.grad.is_contiguous():
+                    raise TypeError("FusedAdamW: contiguous f32 params/grads required")
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                st["step"] += 1
+                by_step.setdefault(st["step"], []).append(p)
+            for step, ps in by_step.items():
+                dev = ps[0].device
+                st = [self.state[p] for p in ps]
+                tp = self._table(ps, dev)
+                tg = self._table([p.grad for p in ps], dev)
+                tm = self._table([s["exp_avg"] for s in st], dev)
+                tv = self._table([s["exp_avg_sq"] for s in st], dev)
+                sizes = self._table_sizes(ps, dev)
+                bc1 = 1.0 - b1 ** step
+                bc2s = math.sqrt(1.0 - b2 ** step)
+                lib.ivit_adamw(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(sizes), max(p.numel() for p in ps),
+                               group["lr"], b1, b2, group["eps"], group["weight_decay"], bc1, bc2s, stream())
+        return loss
+
+    def _table_sizes(self, ps, device):
+        key = ("sizes",) + tuple(p.numel() for p in ps)
+        tab = self._tables.get(key)
+        if tab is None:
+            tab = torch.tensor([p.numel() for p in ps], dtype=torch.int64).to(device)
+            self._tables[key] = tab
+        return tab

@@ -1,0 +1,129 @@
+"""timm-compatible VisionTransformer stream (the object ``timm.create_model`` returns at
+model_vit.py:64,71): same attribute surface (``patch_embed.grid_size``, ``num_prefix_tokens``,
+``embed_dim``, ``cls_token``, assignable ``head``, ``forward_features``) and the same
+``state_dict`` keys as timm's ``vit_{small,tiny}_patch8_224``, so reference checkpoints load.
+Compute runs in ``ops.PatchEmbedFn`` + ``ops.ViTBlockFn`` (HIP)."""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+import ops
+from _lib import BF16, F32
+from layers import Conv2d, LayerNorm, Linear, _LayerNormFn
+
+VIT_ARCH = {
+    "vit_small_patch8_224": dict(embed_dim=384, depth=12, num_heads=6, patch=8, mlp_ratio=4),
+    "vit_tiny_patch8_224": dict(embed_dim=192, depth=12, num_heads=3, patch=8, mlp_ratio=4),
+}
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, img_size, patch_size, in_chans, embed_dim):
+        super().__init__()
+        self.img_size = tuple(img_size)
+        self.patch_size = (patch_size, patch_size)
+        self.grid_size = (self.img_size[0] // patch_size, self.img_size[1] // patch_size)
+        self.num_patches = self.grid_size[0] * self.grid_size[1]
+        self.proj = Conv2d(in_chans, embed_dim, patch_size, stride=patch_size)
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.num_heads, self.head_dim = num_heads, dim // num_heads
+        self.scale = self.head_dim ** -0.5
+        self.qkv = Linear(dim, dim * 3)
+        self.proj = Linear(dim, dim)
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = Linear(dim, hidden)
+        self.fc2 = Linear(hidden, dim)
+
+
+class Block(nn.Module):
+    def __init__(self, dim, num_heads, mlp_ratio, drop_path):
+        super().__init__()
+        self.norm1 = LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, num_heads)
+        self.norm2 = LayerNorm(dim, eps=1e-6)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+        self.drop_path_rate = drop_path
+
+    def _scales(self, B, device):
+        """timm DropPath: per-sample Bernoulli(1-p) / (1-p), independent per branch."""
+        p = self.drop_path_rate
+        if not self.training or p <= 0.0:
+            return None, None
+        keep = 1.0 - p
+        s = torch.empty((2, B), device=device).bernoulli_(keep).div_(keep)
+        return s[0].contiguous(), s[1].contiguous()
+
+    def forward_flat(self, x, B, N, cdt):
+        s1, s2 = self._scales(B, x.device)
+        return ops.ViTBlockFn.apply(x, self.norm1.weight, self.norm1.bias, self.attn.qkv.weight, self.attn.qkv.bias,
+                                    self.attn.proj.weight, self.attn.proj.bias, self.norm2.weight, self.norm2.bias,
+                                    self.mlp.fc1.weight, self.mlp.fc1.bias, self.mlp.fc2.weight, self.mlp.fc2.bias,
+                                    s1, s2, (B, N, self.attn.num_heads, cdt, 1e-6))
+
+    def forward(self, x):
+        B, N, D = x.shape
+        cdt = BF16 if getattr(self, "compute_dtype", torch.float32) == torch.bfloat16 else F32
+        return self.forward_flat(x.reshape(B * N, D).contiguous().float(), B, N, cdt).reshape(B, N, D)
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, img_size=(224, 224), patch_size=8, in_chans=3, embed_dim=384, depth=12, num_heads=6,
+                 mlp_ratio=4.0, drop_path_rate=0.0):
+        super().__init__()
+        self.embed_dim = self.num_features = embed_dim
+        self.num_prefix_tokens = 1
+        self.patch_embed = PatchEmbed(img_size, patch_size, in_chans, embed_dim)
+        n_tok = self.patch_embed.num_patches + 1
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
+        self.pos_embed = nn.Parameter(torch.randn(1, n_tok, embed_dim) * 0.02)
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, depth)]
+        self.blocks = nn.ModuleList([Block(embed_dim, num_heads, mlp_ratio, dpr[i]) for i in range(depth)])
+        self.norm = LayerNorm(embed_dim, eps=1e-6)
+        self.head = nn.Identity()
+        nn.init.normal_(self.cls_token, std=1e-6)
+        self.compute_dtype = torch.float32
+
+    def _cdt(self):
+        return BF16 if self.compute_dtype == torch.bfloat16 else F32
+
+    def forward_tokens(self, x):
+        """Patch embed + all blocks, without the final norm: (B*(Np+1), D) f32 residual stream."""
+        B, C, H, W = x.shape
+        if (H, W) != self.patch_embed.img_size:
+            raise ValueError(f"Input size {(H, W)} != model img_size {self.patch_embed.img_size} (timm strict size)")
+        cdt = self._cdt()
+        t = ops.PatchEmbedFn.apply(x.float().contiguous(), self.patch_embed.proj.weight, self.patch_embed.proj.bias,
+                                   self.pos_embed, self.cls_token, cdt)
+        N = self.patch_embed.num_patches + 1
+        for blk in self.blocks:
+            t = blk.forward_flat(t, B, N, cdt)
+        return t
+
+    def forward_features(self, x):
+        B = x.shape[0]
+        t = self.forward_tokens(x)
+        return _LayerNormFn.apply(t, self.norm.weight, self.norm.bias, 1e-6).reshape(B, -1, self.embed_dim)
+
+    def forward(self, x):
+        return self.head(self.forward_features(x)[:, 0])
+
+
+def create_model(model_name, pretrained=False, in_chans=3, img_size=(224, 224), drop_path_rate=0.0, **_):
+    """timm.create_model surface used by the reference (model_vit.py:64,71)."""
+    if pretrained:
+        raise RuntimeError("pretrained weights are not available offline; pass pretrained=False")
+    a = VIT_ARCH[model_name]
+    return VisionTransformer(img_size=img_size, patch_size=a["patch"], in_chans=in_chans, embed_dim=a["embed_dim"],
+                             depth=a["depth"], num_heads=a["num_heads"], mlp_ratio=a["mlp_ratio"],
+                             drop_path_rate=drop_path_rate)
