@@ -310,7 +310,7 @@ def assign_targets(anchors, gt_list, pos_thr=0.6, neg_thr=0.45, iou_fn=axis_alig
     """loss.py:58-126 — per-sample IoU assignment, force-match and delta encoding."""
     B, NA = len(gt_list), anchors.shape[0]
     cls_t = torch.full((B, NA), -1, dtype=torch.long)
-    box_t = torch.zeros((B, NA, 6))
+    box_t = torch.zeros((B, NA, 6), dtype=anchors.dtype)
     int_t = torch.full((B, NA), -1, dtype=torch.long)
     for b in range(B):
         g = gt_list[b]

@@ -53,9 +53,10 @@ def test_linear_fwd_dgrad_wgrad(M, N, K, cd):
     dyd = ops.cast(dy.to(DEV), cd)
     dx = ops.linear_dgrad(dyd, wd, cdt, torch.float32)
     assert _rel(dx, dy.double() @ w.double()) < tol
-    dxg = ops.linear_dgrad(dyd, wd, cdt, torch.float32, gelu_pre=ops.cast(pre, cd) if cd == torch.float32 else pre)
-    hp = pre.float().cpu().double().requires_grad_(True)
-    F.gelu(hp).backward(dy.double() @ w.double())
+    prek = ops.cast(torch.randn(M, K).to(DEV), cd)
+    dxg = ops.linear_dgrad(dyd, wd, cdt, torch.float32, gelu_pre=prek)
+    hp = prek.float().cpu().double().requires_grad_(True)
+    F.gelu(hp).backward(dyd.float().cpu().double() @ wd.float().cpu().double())
     assert _rel(dxg, hp.grad) < tol * 2
     dw, db = ops.linear_wgrad(dyd, xd, cdt)
     assert _rel(dw, dy.double().T @ x.double()) < tol
