@@ -20,8 +20,11 @@ constexpr int GBK16 = 64;  // bf16 K tile
 constexpr int GBK32 = 16;  // f32 K tile
 
 // z -> element offset: (z / zdiv) * s1 + (z % zdiv) * s2
+// (32-bit index math only: a 64-bit division is a ~100-instruction software loop on CDNA.)
 struct BatchOff {
-  long zdiv = 1, s1 = 0, s2 = 0;
+  int zdiv;
+  long s1, s2;
+  __host__ __device__ BatchOff(long zd = 1, long a = 0, long b = 0) : zdiv((int)zd), s1(a), s2(b) {}
   IVIT_DEV long at(int z) const { return (long)(z / zdiv) * s1 + (long)(z % zdiv) * s2; }
 };
 
@@ -32,20 +35,29 @@ struct BatchOff {
 template <typename S>
 struct LdDense {
   static constexpr bool kRowFast = false;
-  const S* p; long ld; int R, C; long rpb, rstride, roff; BatchOff bo;
+  static constexpr bool kGlds = sizeof(S) == 2;
+  const S* p; long ld; int R, C; int rpb; long rstride; int roff; BatchOff bo;
+  IVIT_DEV LdDense bind(int z) const {  // fold the batch offset into the base once per block
+    LdDense t = *this;
+    t.p = p + bo.at(z);
+    return t;
+  }
   IVIT_DEV long row_addr(int r) const { return rpb ? (long)(r / rpb) * rstride + roff + r % rpb : (long)r; }
-  IVIT_DEV uint4 load8(int z, int r, int c) const {
+  IVIT_DEV const void* src8(int, int r, int c) const {
+    return (r >= R || c >= C) ? nullptr : (const void*)(p + row_addr(r) * ld + c);
+  }
+  IVIT_DEV uint4 load8(int, int r, int c) const {
     if (r >= R || c >= C) return make_uint4(0, 0, 0, 0);
-    const S* q = p + bo.at(z) + row_addr(r) * ld + c;
+    const S* q = p + row_addr(r) * ld + c;
     if constexpr (sizeof(S) == 2) {
       return *(const uint4*)q;
     } else {
       return f32x8_to_bf16x8(*(const float4*)q, *(const float4*)(q + 4));
     }
   }
-  IVIT_DEV float4 load4(int z, int r, int c) const {
+  IVIT_DEV float4 load4(int, int r, int c) const {
     if (r >= R || c >= C) return make_float4(0.f, 0.f, 0.f, 0.f);
-    const S* q = p + bo.at(z) + row_addr(r) * ld + c;
+    const S* q = p + row_addr(r) * ld + c;
     if constexpr (sizeof(S) == 4) {
       return *(const float4*)q;
     } else {
@@ -60,6 +72,8 @@ struct LdDense {
 template <typename S>
 struct LdPatch {
   static constexpr bool kRowFast = true;  // consecutive patches are consecutive 32-B runs
+  static constexpr bool kGlds = false;    // f32 image converted to bf16 on the way: register staging
+  IVIT_DEV LdPatch bind(int) const { return *this; }
   const S* img; int Bn, Cin, H, W, Wp, Np; int R, C;
   IVIT_DEV const S* addr(int r, int c) const {
     const int b = r / Np, pi = r - b * Np, gy = pi / Wp, gx = pi - gy * Wp;
@@ -89,7 +103,13 @@ struct LdPatch {
 template <typename S>
 struct LdConv {
   static constexpr bool kRowFast = false;
+  static constexpr bool kGlds = sizeof(S) == 2;
   const S* x; int H, W, Cin, ks; int R, C; long ldc;  // ldc = channel stride of a pixel
+  IVIT_DEV LdConv bind(int) const { return *this; }
+  IVIT_DEV const void* src8(int, int r, int c) const {
+    long off;
+    return at(r, c, off) ? (const void*)(x + off) : nullptr;
+  }
   IVIT_DEV bool at(int r, int c, long& off) const {
     if (r >= R || c >= C) return false;
     const int tap = c / Cin, ci = c - tap * Cin;
@@ -124,7 +144,12 @@ struct LdConv {
 template <typename S>
 struct LdConvWFlip {
   static constexpr bool kRowFast = false;
+  static constexpr bool kGlds = sizeof(S) == 2;
   const S* w; int Cout, Cin, ks; int R, C;
+  IVIT_DEV LdConvWFlip bind(int) const { return *this; }
+  IVIT_DEV const void* src8(int, int r, int c) const {
+    return (r >= R || c >= C) ? nullptr : (const void*)addr(r, c);
+  }
   IVIT_DEV const S* addr(int r, int c) const {
     const int tap = r / Cout, co = r - tap * Cout;
     const int ky = tap / ks, kx = tap - ky * ks;
@@ -148,50 +173,116 @@ struct LdConvWFlip {
 };
 
 // ----------------------------------------------------------------------------- epilogues
-// apply(z, split, m, n, v) is called once per output element with m < M, n < N.
+// apply8(z, split, m, n, v, nv): outputs (m, n .. n+nv-1), nv <= 8, m < M, n < N. The engine
+// hands each lane 8 consecutive columns (accumulators transposed through LDS), so stores are
+// 16-byte vectors whenever the destination is aligned.
 template <typename O>
 struct EpiStore {  // out = act(alpha*acc + bias[n]); optional pre-activation copy
   O* out; long ldo; BatchOff bo; const float* bias; int act; O* pre; float alpha;
-  IVIT_DEV void apply(int z, int, int m, int n, float v) const {
-    v = v * alpha + (bias ? bias[n] : 0.f);
-    const long o = bo.at(z) + (long)m * ldo + n;
-    if (pre) pre[o] = from_f32<O>(v);
-    if (act == IVIT_ACT_GELU) v = gelu_erf(v);
-    else if (act == IVIT_ACT_RELU) v = fmaxf(v, 0.f);
-    out[o] = from_f32<O>(v);
+  IVIT_DEV EpiStore bind(int z) const {
+    EpiStore t = *this;
+    const long o = bo.at(z);
+    t.out = out + o;
+    t.pre = pre ? pre + o : nullptr;
+    return t;
+  }
+  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
+    float x[8];
+    float bb[8];
+    if (bias) load8f(bias + n, bb, nv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = v[k] * alpha + (bias ? bb[k] : 0.f);
+    const long o = (long)m * ldo + n;
+    if (pre) store8(pre + o, x, nv);
+    if (act == IVIT_ACT_GELU) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = gelu_t<O>(x[k]);
+    } else if (act == IVIT_ACT_RELU) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = fmaxf(x[k], 0.f);
+    }
+    store8(out + o, x, nv);
   }
 };
 
 struct EpiResid {  // out(f32) = res + scale[m / rps] * (acc + bias[n])
-  float* out; long ldo; const float* res; long ldr; const float* bias; const float* scale; long rps;
-  IVIT_DEV void apply(int, int, int m, int n, float v) const {
-    v += bias ? bias[n] : 0.f;
-    if (scale) v *= scale[m / rps];
-    out[(long)m * ldo + n] = res[(long)m * ldr + n] + v;
+  float* out; long ldo; const float* res; long ldr; const float* bias; const float* scale; int rps;
+  IVIT_DEV EpiResid bind(int) const { return *this; }
+  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
+    float bb[8], rr[8], x[8];
+    if (bias) load8f(bias + n, bb, nv);
+    load8f(res + (long)m * ldr + n, rr, nv);
+    const float s = scale ? scale[m / rps] : 1.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = rr[k] + s * (v[k] + (bias ? bb[k] : 0.f));
+    store8(out + (long)m * ldo + n, x, nv);
   }
 };
 
 template <typename O, typename P>
 struct EpiGeluGrad {  // out = acc * gelu'(pre)
   O* out; long ldo; const P* pre; long ldp;
-  IVIT_DEV void apply(int, int, int m, int n, float v) const {
-    out[(long)m * ldo + n] = from_f32<O>(v * gelu_erf_grad(to_f32(pre[(long)m * ldp + n])));
+  IVIT_DEV EpiGeluGrad bind(int) const { return *this; }
+  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
+    float pp[8], x[8];
+    load8f(pre + (long)m * ldp + n, pp, nv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = v[k] * gelu_grad_t<O>(pp[k]);
+    store8(out + (long)m * ldo + n, x, nv);
   }
 };
 
 struct EpiSlab {  // split-K partial slab [split][M][N] (f32)
   float* slab; long M, N;
-  IVIT_DEV void apply(int, int split, int m, int n, float v) const { slab[((long)split * M + m) * N + n] = v; }
+  IVIT_DEV EpiSlab bind(int) const { return *this; }
+  IVIT_DEV void apply8(int, int split, int m, int n, const float (&v)[8], int nv) const {
+    store8(slab + ((long)split * M + m) * N + n, v, nv);
+  }
 };
 
 struct EpiPatch {  // token (b, 1 + p) of x(f32) = acc + bias[n] + pos[1 + p][n]
   float* out; int Np, D; const float* bias; const float* pos;
-  IVIT_DEV void apply(int, int, int m, int n, float v) const {
+  IVIT_DEV EpiPatch bind(int) const { return *this; }
+  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
     const int b = m / Np, p = m - b * Np;
     const long row = (long)b * (Np + 1) + 1 + p;
-    out[row * D + n] = v + bias[n] + pos[(long)(1 + p) * D + n];
+    float bb[8], pp[8], x[8];
+    load8f(bias + n, bb, nv);
+    load8f(pos + (long)(1 + p) * D + n, pp, nv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = v[k] + bb[k] + pp[k];
+    store8(out + row * D + n, x, nv);
   }
 };
+
+// Wave-local accumulator transpose through LDS (the staging buffers are free after the
+// main loop): 32-row halves of the wave's 64x64 tile, row stride 68 floats.
+constexpr int EP_LD = 68;
+template <class EPI>
+IVIT_DEV void epilogue_tile(float* ep, f32x16 (&acc)[2][2], const EPI& epi, int z, int split, int mbase, int nbase,
+                            int M, int N, int lane) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        ep[((r & 3) + 8 * (r >> 2) + 4 * h) * EP_LD + 32 * j + (lane & 31)] = acc[i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes are complete
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int row = (lane >> 3) + 8 * t, c0 = (lane & 7) * 8;
+      float v[8];
+      const float4 a = *(const float4*)(ep + row * EP_LD + c0);
+      const float4 b = *(const float4*)(ep + row * EP_LD + c0 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      const int m = mbase + 32 * i + row, n = nbase + c0;
+      if (m < M && n < N) epi.apply8(z, split, m, n, v, min(8, N - n));
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+}
 
 // ----------------------------------------------------------------------------- LDS images
 // K-contiguous bf16 image: rows x 64 k (128-B rows); 16-B chunk c of row r stored at
@@ -226,13 +317,16 @@ IVIT_DEV bf16x8 frag_mn(const char* img, int kbase, int colbase, int lane) {
 
 // ----------------------------------------------------------------------------- bf16 kernel
 template <class LA, class LB, class EPI, bool A_KC, bool B_KC>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(LA la_, LB lb_, EPI epi_, int M, int N, int K,
                                                          int tilesM, int tilesN, int splits, int kchunk) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][16384];  // [stage][A|B][image]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = lin / tilesN, tn = lin - tm * tilesN;
   const int z = blockIdx.y / splits, split = blockIdx.y - z * splits;
+  const LA la = la_.bind(z);
+  const LB lb = lb_.bind(z);
+  const EPI epi = epi_.bind(z);
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int nk = (kend - kbeg + GBK16 - 1) / GBK16;
@@ -323,26 +417,16 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(LA la, LB lb, EPI epi
     }
     __syncthreads();
   }
-  // C layout (32x32 f32): col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + 32 * j + (lane & 31);
-      if (n >= N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < M) epi.apply(z, split, m, n, acc[i][j][r]);
-      }
-    }
+  // C layout (32x32 f32): col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5); transposed via LDS
+  epilogue_tile((float*)&smem[0][0][0] + wv * (32 * EP_LD), acc, epi, z, split, m0 + wm * 64, n0 + wn * 64, M, N,
+                lane);
 }
 
 // ----------------------------------------------------------------------------- f32 kernel
 // K-contiguous f32 image [128][17] (row pad -> conflict-free ds_read_b32 column reads);
 // MN-contiguous f32 image [16][128].
 template <class LA, class LB, class EPI, bool A_KC, bool B_KC>
-__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, EPI epi, int M, int N, int K,
+__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la_, LB lb_, EPI epi_, int M, int N, int K,
                                                         int tilesM, int tilesN, int splits, int kchunk) {
   constexpr int KCS = 17;                       // K-contig row stride (floats)
   constexpr int IMG = 128 * KCS > 16 * 128 ? 128 * KCS : 16 * 128;
@@ -351,6 +435,9 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, EPI epi,
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = lin / tilesN, tn = lin - tm * tilesN;
   const int z = blockIdx.y / splits, split = blockIdx.y - z * splits;
+  const LA la = la_.bind(z);
+  const LB lb = lb_.bind(z);
+  const EPI epi = epi_.bind(z);
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int nk = (kend - kbeg + GBK32 - 1) / GBK32;
@@ -442,18 +529,100 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(LA la, LB lb, EPI epi,
     }
     __syncthreads();
   }
+  epilogue_tile(&smem[0][0][0] + wv * (32 * EP_LD), acc, epi, z, split, m0 + wm * 64, n0 + wn * 64, M, N, lane);
+}
+
+// ----------------------------------------------------------------------------- bf16 LDS-DMA kernel
+// Same tiling/fragments/epilogue as gemm_bf16_kernel, but operands stream HBM -> LDS with
+// global_load_lds_dwordx4 (no VGPR staging): the next K tile is in flight during the
+// current tile's MFMAs, retired by a counted vmcnt and a raw s_barrier (no __syncthreads:
+// its fence would drain the DMA). The swizzle moves to the per-lane SOURCE address: each
+// 1-KiB wave piece is lane-linear in LDS (cdna_hip_programming.md §5 rule 21). Out-of-range
+// rows/taps read a zero page.
+static __device__ __attribute__((aligned(16))) uint4 g_zero16[4];
+
+template <class L>
+IVIT_DEV void glds_piece(const L& ld, int z, bool kc, char* img, int piece, int lane, int o0, int k0, int kend) {
+  const void* src;
+  if (kc) {  // image rows = m/n (128-B rows); a piece = 8 rows
+    const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128(row);
+    const int kk = k0 + c * 8;
+    src = kk < kend ? ld.src8(z, o0 + row, kk) : nullptr;
+  } else {   // image rows = k (256-B rows); a piece = 4 rows
+    const int row = piece * 4 + (lane >> 4), c = (lane & 15) ^ ((row & 3) << 2);
+    const int kk = k0 + row;
+    src = kk < kend ? ld.src8(z, kk, o0 + c * 8) : nullptr;
+  }
+  __builtin_amdgcn_global_load_lds(src ? src : (const void*)g_zero16,
+                                   (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
+}
+
+template <class LA, class LB, class EPI, bool A_KC, bool B_KC>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, EPI epi_, int M, int N, int K,
+                                                              int tilesM, int tilesN, int splits, int kchunk) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][16384];  // [stage][A|B][image]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = lin / tilesN, tn = lin - tm * tilesN;
+  const int z = blockIdx.y / splits, split = blockIdx.y - z * splits;
+  const LA la = la_.bind(z);
+  const LB lb = lb_.bind(z);
+  const EPI epi = epi_.bind(z);
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
+  const int nk = (kend - kbeg + GBK16 - 1) / GBK16;
+
+  auto issue = [&](int stage, int k0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds_piece(la, z, A_KC, smem[stage][0], wv * 4 + i, lane, m0, k0, kend);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds_piece(lb, z, B_KC, smem[stage][1], wv * 4 + i, lane, n0, k0, kend);
+  };
+
+  f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + 32 * j + (lane & 31);
-      if (n >= N) continue;
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < M) epi.apply(z, split, m, n, acc[i][j][r]);
-      }
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) issue(0, kbeg);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      issue(cur ^ 1, kbeg + (kt + 1) * GBK16);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this tile's 8 pieces have landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    __builtin_amdgcn_s_barrier();                         // ... for every wave's pieces
+    const char* ia = smem[cur][0];
+    const char* ib = smem[cur][1];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int rb0 = wm * 64 + 32 * i;
+        fa[i] = A_KC ? frag_kc(ia, rb0 + (lane & 31), 2 * t + (lane >> 5)) : frag_mn(ia, 16 * t, rb0, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cb0 = wn * 64 + 32 * j;
+        fb[j] = B_KC ? frag_kc(ib, cb0 + (lane & 31), 2 * t + (lane >> 5)) : frag_mn(ib, 16 * t, cb0, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of this stage are done
+    __builtin_amdgcn_s_barrier();                         // ... everyone's, before it is refilled
+  }
+  epilogue_tile((float*)&smem[0][0][0] + wv * (32 * EP_LD), acc, epi, z, split, m0 + wm * 64, n0 + wn * 64, M, N,
+                lane);
 }
 
 // ----------------------------------------------------------------------------- launcher
@@ -469,10 +638,14 @@ int launch_gemm(bool bf16_path, const LA& la, const LB& lb, const EPI& epi, int 
   int kchunk = ivit_cdiv(ivit_cdiv(K, splits), bk) * bk;
   if (kchunk <= 0) kchunk = bk;
   dim3 grid(tilesM * tilesN, batch * splits);
-  if (bf16_path)
-    hipLaunchKernelGGL((gemm_bf16_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N, K,
-                       tilesM, tilesN, splits, kchunk);
-  else
+  if (bf16_path) {
+    if constexpr (LA::kGlds && LB::kGlds)
+      hipLaunchKernelGGL((gemm_bf16_glds_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N,
+                         K, tilesM, tilesN, splits, kchunk);
+    else
+      hipLaunchKernelGGL((gemm_bf16_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N, K,
+                         tilesM, tilesN, splits, kchunk);
+  } else
     hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N, K,
                        tilesM, tilesN, splits, kchunk);
   return 0;

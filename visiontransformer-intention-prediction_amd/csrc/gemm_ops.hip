@@ -48,14 +48,6 @@ __global__ void colsum_partial_kernel(const S* __restrict__ X, long ld, long rpb
   if (ph == 0 && col < N)
     part[(long)blockIdx.y * N + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
-__global__ void colsum_final_kernel(const float* __restrict__ part, long chunks, long N, float* __restrict__ out,
-                                    int accumulate) {
-  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (long k = 0; k < chunks; ++k) s += part[k * N + c];
-  out[c] = accumulate ? out[c] + s : s;
-}
 
 extern "C" long ivit_colsum_workspace(long M, long N) { return (long)ivit_cdiv(M, CS_ROWS) * N * 4; }
 
@@ -72,8 +64,7 @@ extern "C" int ivit_colsum(const void* X, int x_dtype, long ld, long rpb, long r
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, g, dim3(256), 0, st, (const float*)X, ld, rpb, rstride, roff, M,
                        N, (float*)work);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(ivit_cdiv(N, 256)), dim3(256), 0, st, (const float*)work, chunks, N,
-                     out, accumulate);
+  launch_colreduce(st, (const float*)work, chunks, N, (int)N, out, (int)N, nullptr, accumulate);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -94,7 +85,7 @@ static int linear_fwd_t(const void* X, long ldx, const void* W, const float* bia
   LdDense<S> la{(const S*)X, ldx, (int)M, (int)K, 0, 0, 0, {}};
   LdDense<S> lb{(const S*)W, K, (int)N, (int)K, 0, 0, 0, {}};
   if (resid) {
-    EpiResid e{(float*)Y, ldy, resid, ldr, bias, rs, rps > 0 ? rps : 1};
+    EpiResid e{(float*)Y, ldy, resid, ldr, bias, rs, (int)(rps > 0 ? rps : 1)};
     return launch_gemm<true, true>(bf, la, lb, e, M, N, K, 1, 1, st);
   }
   EpiStore<O> e{(O*)Y, ldy, {}, bias, act, (O*)Ypre, 1.f};

@@ -51,17 +51,6 @@ IVIT_DEV float gelu_erf_grad(float x) {
   return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
 
-IVIT_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-IVIT_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
 // 8 bf16 <-> uint4 reinterpretation
 union Pack8 {
   uint4 u;
@@ -74,12 +63,111 @@ union Pack4 {
   bf16 h[4];
 };
 
+// Fast GELU / GELU' for bf16 outputs: erf by Abramowitz-Stegun 7.1.26 (|err| <= 1.5e-7, far below
+// bf16 resolution); erf(x/sqrt2) and the Gaussian density share one exp(-x^2/2).
+IVIT_DEV float erf_as(float x, float e /* = exp(-x*x) */) {
+  const float a = fabsf(x);
+  const float t = __frcp_rn(1.0f + 0.3275911f * a);
+  const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float r = 1.0f - p * e;
+  return x < 0.f ? -r : r;
+}
+IVIT_DEV float gelu_fast(float x) {
+  const float e = __expf(-0.5f * x * x);
+  return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f, e));
+}
+IVIT_DEV float gelu_grad_fast(float x) {
+  const float e = __expf(-0.5f * x * x);
+  return 0.5f * (1.0f + erf_as(x * 0.70710678118654752f, e)) + x * 0.39894228040143268f * e;
+}
+template <typename O> IVIT_DEV float gelu_t(float x) { return sizeof(O) == 2 ? gelu_fast(x) : gelu_erf(x); }
+template <typename O> IVIT_DEV float gelu_grad_t(float x) {
+  return sizeof(O) == 2 ? gelu_grad_fast(x) : gelu_erf_grad(x);
+}
+
+IVIT_DEV bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// store 8 consecutive values (vectorised when aligned and complete)
+template <typename O>
+IVIT_DEV void store8(O* p, const float (&x)[8], int nv) {
+  if (nv >= 8 && al16(p)) {
+    if constexpr (sizeof(O) == 2) {
+      Pack8 q;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) q.h[k] = (bf16)x[k];
+      *(uint4*)p = q.u;
+    } else {
+      *(float4*)p = make_float4(x[0], x[1], x[2], x[3]);
+      *(float4*)(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
+    }
+  } else {
+    for (int k = 0; k < nv && k < 8; ++k) p[k] = from_f32<O>(x[k]);
+  }
+}
+template <typename T>
+IVIT_DEV void load8f(const T* p, float (&x)[8], int nv) {
+  if (nv >= 8 && al16(p)) {
+    if constexpr (sizeof(T) == 2) {
+      Pack8 q;
+      q.u = *(const uint4*)p;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = (float)q.h[k];
+    } else {
+      const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = k < nv ? to_f32(p[k]) : 0.f;
+  }
+}
+
+IVIT_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+IVIT_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+
 IVIT_DEV uint4 f32x8_to_bf16x8(float4 a, float4 b) {
   Pack8 p;
   p.h[0] = f2bf(a.x); p.h[1] = f2bf(a.y); p.h[2] = f2bf(a.z); p.h[3] = f2bf(a.w);
   p.h[4] = f2bf(b.x); p.h[5] = f2bf(b.y); p.h[6] = f2bf(b.z); p.h[7] = f2bf(b.w);
   return p.u;
 }
+
+// Column reduction of per-block partial sums: out[c] (+)= sum_b part[b * pstride + c].
+// 1024 threads = 64 columns x 16 partial phases, so long partial lists reduce in parallel.
+// Columns >= C0 go to out1[c - C0] (two outputs packed in one partial row, e.g. dgamma|dbeta).
+namespace {
+__global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict__ part, int nb, long pstride, int C,
+                                                         float* out0, int C0, float* out1, int acc) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < C)
+    for (int b = ph; b < nb; b += 16) s += part[(long)b * pstride + c];
+  __shared__ float red[16][64];
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
+    float* o = c < C0 ? (out0 ? out0 + c : nullptr) : (out1 ? out1 + (c - C0) : nullptr);
+    if (o) *o = acc ? *o + t : t;
+  }
+}
+inline void launch_colreduce(hipStream_t st, const float* part, int nb, long pstride, int C, float* out0, int C0,
+                             float* out1, int acc) {
+  hipLaunchKernelGGL(colreduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, nb, pstride, C, out0, C0, out1,
+                     acc);
+}
+}  // namespace
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): blocks b and b+8 share an XCD under round-robin dispatch, so give each

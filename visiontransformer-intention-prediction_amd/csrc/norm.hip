@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ X
   if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
 }
 
-constexpr int LNB_BLOCKS = 512;
+constexpr int LNB_ROWS = 8;  // rows per wave; a block (4 waves) covers 32 rows
 
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ X, long ldx, long rpb, long rstride,
                                                      long roff, long M, int D, const float* __restrict__ g,
@@ -63,7 +63,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ X
   float pg[LN_MAXV], pb[LN_MAXV];
 #pragma unroll
   for (int i = 0; i < LN_MAXV; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
-  for (long row = (long)blockIdx.x * 4 + wv; row < M; row += (long)gridDim.x * 4) {
+  const long r0 = ((long)blockIdx.x * 4 + wv) * LNB_ROWS;
+  for (long row = r0; row < min(M, r0 + LNB_ROWS); ++row) {
     const float* x = X + rowmap(row, rpb, rstride, roff) * ldx;
     const float mu = mean[row], rs = rstd[row];
     float xh[LN_MAXV], gy[LN_MAXV];
@@ -105,14 +106,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ X
   }
 }
 
-__global__ void ln_bwd_final_kernel(const float* __restrict__ part, int nb, int D, float* dg, float* db, int acc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  float sg = 0.f, sb = 0.f;
-  for (int k = 0; k < nb; ++k) { sg += part[(k * 2 + 0) * D + c]; sb += part[(k * 2 + 1) * D + c]; }
-  if (dg) dg[c] = acc ? dg[c] + sg : sg;
-  if (db) db[c] = acc ? db[c] + sb : sb;
-}
 
 // ---------------------------------------------------------------- BatchNorm (NHWC [M, C])
 constexpr int BN_ROWS = 128;
@@ -227,7 +220,9 @@ extern "C" int ivit_layernorm_fwd(const float* X, long ldx, long rpb, long rstri
   return 0;
 }
 
-extern "C" long ivit_layernorm_bwd_workspace(long M, long D) { return (long)LNB_BLOCKS * 2 * D * 4; }
+extern "C" long ivit_layernorm_bwd_workspace(long M, long D) {
+  return (long)ivit_cdiv(M, 4 * LNB_ROWS) * 2 * D * 4 + 16;
+}
 
 extern "C" int ivit_layernorm_bwd(const float* X, long ldx, long rpb, long rstride, long roff, long M, long D,
                                   const float* gamma, const float* mean, const float* rstd, const void* dY, long lddy,
@@ -238,13 +233,11 @@ extern "C" int ivit_layernorm_bwd(const float* X, long ldx, long rpb, long rstri
   IVIT_CHECK_ARG(work_bytes >= ivit_layernorm_bwd_workspace(M, D), "ivit_layernorm_bwd: workspace too small");
   if (M <= 0) return 0;
   hipStream_t st = ivit_stream(stream);
-  int nb = ivit_cdiv(M, 4);
-  if (nb > LNB_BLOCKS) nb = LNB_BLOCKS;
+  const int nb = ivit_cdiv(M, 4 * LNB_ROWS);
   hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rpb, rstride, roff, M, (int)D, gamma, mean,
                      rstd, dY, lddy, dy_dtype, dres, dX, lddx, dXs, dxs_dtype, row_scale,
                      rows_per_scale > 0 ? rows_per_scale : 1, (float*)work);
-  hipLaunchKernelGGL(ln_bwd_final_kernel, dim3(ivit_cdiv(D, 256)), dim3(256), 0, st, (const float*)work, nb, (int)D,
-                     dgamma, dbeta, accumulate);
+  launch_colreduce(st, (const float*)work, nb, 2 * D, (int)(2 * D), dgamma, (int)D, dbeta, accumulate);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
