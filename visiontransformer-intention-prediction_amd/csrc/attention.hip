@@ -10,6 +10,8 @@
 //             queries); both recompute P from the saved LSE. No atomics.
 // f32 path (parity): exact-f32 MFMA GEMMs through the generic engine with the score
 //             matrix materialised in the workspace, plus row-softmax kernels.
+#include <stdlib.h>
+
 #include "gemm_engine.h"
 
 using namespace ivit;
@@ -31,6 +33,18 @@ IVIT_DEV void tile_gload(const bf16* base, long ld, int r0, int nrows, int tid, 
   for (int i = 0; i < 2; ++i) {
     const int idx = tid + 256 * i, row = idx >> 3, ch = idx & 7;
     r[i] = (r0 + row < nrows) ? *(const uint4*)(base + (long)(r0 + row) * ld + ch * 8) : make_uint4(0, 0, 0, 0);
+  }
+}
+// The same 64 x 64 tile by LDS-DMA: 8 lane-linear 1-KiB pieces (2 per wave), the chunk
+// swizzle applied to the per-lane source address; rows >= nrows read the zero page.
+IVIT_DEV void tile_glds(const bf16* base, long ld, int r0, int nrows, char* img, int wv, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int piece = wv * 2 + i;
+    const int row = piece * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz128(row);
+    const void* src = (r0 + row < nrows) ? (const void*)(base + (long)(r0 + row) * ld + c * 8) : (const void*)g_zero16;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
   }
 }
 IVIT_DEV void tile_sstore(char* img, int tid, const uint4 (&r)[2]) {
@@ -136,19 +150,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16* __res
         s[t][r] = v;
         mx = fmaxf(mx, v);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = half_swap_max(mx);
     const float mn = fmaxf(m, mx);
-    const float alpha = exp2f(m - mn);
+    const float alpha = fast_exp2(m - mn);
     float rs = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[t][r] - mn);
+        const float p = fast_exp2(s[t][r] - mn);
         s[t][r] = p;
         rs += p;
       }
-    rs += __shfl_xor(rs, 32, 64);
+    rs = half_swap_sum(rs);
     l = l * alpha + rs;
     m = mn;
 #pragma unroll
@@ -183,6 +197,268 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16* __res
         c.h[j] = (bf16)(o1[4 * g + j] * inv);
       }
       const int d = 8 * g + 4 * hl;  // rows (r&3) + 8(r>>2) + 4h of O^T
+      *(uint2*)(orow + d) = a.u;
+      *(uint2*)(orow + 32 + d) = c.u;
+    }
+    if (hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
+  }
+}
+
+// ------------------------------------------------------------------------- forward v2 (bf16)
+// 64 queries per wave (two 32-query groups share every K/V fragment read: half the LDS bytes
+// per MFMA of v1), 256 queries per workgroup. Softmax per score: one FMA (scale folded in)
+// + one exp2; key masking only on the last (partial) tile; the O rescale is skipped when no
+// lane's running max moved (exact, wave-uniform test).
+constexpr int AQ2 = 256;
+
+template <bool MASK>
+IVIT_DEV void fwd_tile2(const char* kimg, const char* vimg, const bf16x8 (&qf)[2][4], f32x16 (&o)[2][2],
+                        float (&m)[2], float (&l)[2], int kbase, int N, float c2, int lane) {
+  const int hl = lane >> 5;
+  // one 32-key sub-tile at a time: scores for both query groups = 32 live f32 registers
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x16 s[2] = {zero16(), zero16()};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[0][ks], s[0], 0, 0, 0);
+      s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[1][ks], s[1], 0, 0, 0);
+    }
+    bool moved = false;
+    float alpha[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      float mx = NEG_BIG;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (MASK) {
+          const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= N) s[g][r] = NEG_BIG;
+        }
+        mx = fmaxf(mx, s[g][r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[g], mx * c2);
+      alpha[g] = exp2f(m[g] - mn);
+      moved |= mn != m[g];
+      m[g] = mn;
+      float rs = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(fmaf(s[g][r], c2, -mn));
+        s[g][r] = p;
+        rs += p;
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l[g] = l[g] * alpha[g] + rs;
+    }
+    if (__any(moved)) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o[g][0][r] *= alpha[g]; o[g][1][r] *= alpha[g]; }
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const int rb = 32 * t + 16 * ss;
+      const bf16x8 va0 = tr_acc_order(vimg, rb, 0, lane);
+      const bf16x8 va1 = tr_acc_order(vimg, rb, 32, lane);
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const bf16x8 pb = pack_acc(s[g], ss);
+        o[g][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, pb, o[g][0], 0, 0, 0);
+        o[g][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, pb, o[g][1], 0, 0, 0);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16_v2_kernel(const bf16* __restrict__ qkv, int N, int H,
+                                                                  bf16* __restrict__ out, float* __restrict__ lse,
+                                                                  float c2) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int qw = blockIdx.x * AQ2 + wv * 64;
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int q = qw + 32 * g + (lane & 31);
+    load_row_frags(Qb + (long)q * ld, q < N, lane, qf[g]);
+  }
+  f32x16 o[2][2];
+  float m[2] = {NEG_BIG, NEG_BIG}, l[2] = {0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < 2; ++g) { o[g][0] = zero16(); o[g][1] = zero16(); }
+  const int nt = (N + AK - 1) / AK;
+  // K/V tiles stream HBM -> LDS by LDS-DMA, one tile ahead; raw barriers + explicit vmcnt
+  tile_glds(Kb, ld, 0, N, smem[0][0], wv, lane);
+  tile_glds(Vb, ld, 0, N, smem[0][1], wv, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) {
+      tile_glds(Kb, ld, (kt + 1) * AK, N, smem[cur ^ 1][0], wv, lane);
+      tile_glds(Vb, ld, (kt + 1) * AK, N, smem[cur ^ 1][1], wv, lane);
+    }
+    if ((kt + 1) * AK <= N)
+      fwd_tile2<false>(smem[cur][0], smem[cur][1], qf, o, m, l, kt * AK, N, c2, lane);
+    else
+      fwd_tile2<true>(smem[cur][0], smem[cur][1], qf, o, m, l, kt * AK, N, c2, lane);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // next tile landed; my reads done
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int q = qw + 32 * g + (lane & 31);
+    if (q >= N) continue;
+    const float inv = 1.f / l[g];
+    bf16* orow = out + ((long)b * N + q) * D + h * 64;
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      Pack4 a, c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a.h[j] = (bf16)(o[g][0][4 * gg + j] * inv);
+        c.h[j] = (bf16)(o[g][1][4 * gg + j] * inv);
+      }
+      const int d = 8 * gg + 4 * hl;
+      *(uint2*)(orow + d) = a.u;
+      *(uint2*)(orow + 32 + d) = c.u;
+    }
+    if (hl == 0) lse[(long)z * N + q] = (m[g] + log2f(l[g])) * 0.69314718055994531f;
+  }
+}
+
+// ------------------------------------------------------------------------- forward v3 (bf16)
+// v1's shape (32 queries per wave) with: K/V by LDS-DMA one tile ahead (no staging VGPRs),
+// key masking only on the last tile, the scale folded into one FMA before exp2, and the O
+// rescale skipped when no lane's max moved. WAVES = 4 or 8 waves per workgroup share a tile.
+template <bool MASK>
+IVIT_DEV void fwd_tile3(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], f32x16& o0, f32x16& o1,
+                        float& m, float& l, int kbase, int N, float c2, int lane) {
+  const int hl = lane >> 5;
+  f32x16 s[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    s[t] = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s[t], 0, 0, 0);
+    }
+  }
+  float mx = NEG_BIG;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (MASK) {
+        const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (key >= N) s[t][r] = NEG_BIG;
+      }
+      mx = fmaxf(mx, s[t][r]);
+    }
+  mx = half_swap_max(mx);
+  const float mn = fmaxf(m, mx * c2);
+  const float alpha = fast_exp2(m - mn);
+  const bool moved = mn != m;
+  m = mn;
+  float rs = 0.f;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = fast_exp2(fmaf(s[t][r], c2, -mn));
+      s[t][r] = p;
+      rs += p;
+    }
+  rs = half_swap_sum(rs);
+  l = l * alpha + rs;
+  if (__any(moved)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 pb = pack_acc(s[t], ss);
+      const int rb = 32 * t + 16 * ss;
+      const bf16x8 va0 = tr_acc_order(vimg, rb, 0, lane);
+      const bf16x8 va1 = tr_acc_order(vimg, rb, 32, lane);
+      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, pb, o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, pb, o1, 0, 0, 0);
+    }
+}
+
+// LDS-DMA of a 64x64 tile spread over W waves (8 pieces)
+template <int W>
+IVIT_DEV void tile_glds_w(const bf16* base, long ld, int r0, int nrows, char* img, int wv, int lane) {
+#pragma unroll
+  for (int i = 0; i < 8 / W; ++i) {
+    const int piece = wv * (8 / W) + i;
+    const int row = piece * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ swz128(row);
+    const void* src = (r0 + row < nrows) ? (const void*)(base + (long)(r0 + row) * ld + c * 8) : (const void*)g_zero16;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v3_kernel(const bf16* __restrict__ qkv, int N, int H,
+                                                                        bf16* __restrict__ out,
+                                                                        float* __restrict__ lse, float c2) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int q = blockIdx.x * (32 * W) + wv * 32 + (lane & 31);
+  bf16x8 qf[4];
+  load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
+  f32x16 o0 = zero16(), o1 = zero16();
+  float m = NEG_BIG, l = 0.f;
+  const int nt = (N + AK - 1) / AK;
+  tile_glds_w<W>(Kb, ld, 0, N, smem[0][0], wv, lane);
+  tile_glds_w<W>(Vb, ld, 0, N, smem[0][1], wv, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nt) {
+      tile_glds_w<W>(Kb, ld, (kt + 1) * AK, N, smem[cur ^ 1][0], wv, lane);
+      tile_glds_w<W>(Vb, ld, (kt + 1) * AK, N, smem[cur ^ 1][1], wv, lane);
+    }
+    if ((kt + 1) * AK <= N)
+      fwd_tile3<false>(smem[cur][0], smem[cur][1], qf, o0, o1, m, l, kt * AK, N, c2, lane);
+    else
+      fwd_tile3<true>(smem[cur][0], smem[cur][1], qf, o0, o1, m, l, kt * AK, N, c2, lane);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  if (q < N) {
+    const float inv = 1.f / l;
+    bf16* orow = out + ((long)b * N + q) * D + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      Pack4 a, c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a.h[j] = (bf16)(o0[4 * g + j] * inv);
+        c.h[j] = (bf16)(o1[4 * g + j] * inv);
+      }
+      const int d = 8 * g + 4 * hl;
       *(uint2*)(orow + d) = a.u;
       *(uint2*)(orow + 32 + d) = c.u;
     }
@@ -260,7 +536,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16_kernel(const bf16* __
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const float p = key < N ? exp2f(s[r] * c2 - lse2) : 0.f;
+        const float p = key < N ? fast_exp2(fmaf(s[r], c2, -lse2)) : 0.f;
         s[r] = p * (dp[r] - dlt);  // dS^T[key][q]
       }
       // dQ[q][d] += dS[q][key] K[key][d]  (X = dS^T as the A operand)
@@ -362,7 +638,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* _
         const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float p = exp2f(s[4 * g + j] * c2 - lv[j]);
+          const float p = fast_exp2(fmaf(s[4 * g + j], c2, -lv[j]));
           s[4 * g + j] = p;                               // P[q][key]
           dp[4 * g + j] = p * (dp[4 * g + j] - dv[j]);    // dS[q][key]
         }
@@ -473,9 +749,25 @@ extern "C" int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H,
   const float scale = 1.0f / sqrtf((float)Dh);
   if (B * N * H == 0) return 0;
   if (dtype == IVIT_BF16) {
-    dim3 g(ivit_cdiv(N, AQ), B * H);
-    hipLaunchKernelGGL(attn_fwd_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H, (bf16*)out, lse,
-                       scale * LOG2E);
+    const char* ev = getenv("IVIT_ATTN_FWD_VARIANT");
+    const int variant = ev ? atoi(ev) : 3;
+    if (variant == 1) {
+      dim3 g(ivit_cdiv(N, AQ), B * H);
+      hipLaunchKernelGGL(attn_fwd_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H, (bf16*)out,
+                         lse, scale * LOG2E);
+    } else if (variant == 2) {
+      dim3 g(ivit_cdiv(N, AQ2), B * H);
+      hipLaunchKernelGGL(attn_fwd_bf16_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H, (bf16*)out,
+                         lse, scale * LOG2E);
+    } else if (variant == 3) {
+      dim3 g(ivit_cdiv(N, 128), B * H);
+      hipLaunchKernelGGL(attn_fwd_bf16_v3_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
+    } else {
+      dim3 g(ivit_cdiv(N, 256), B * H);
+      hipLaunchKernelGGL(attn_fwd_bf16_v3_kernel<8>, g, dim3(512), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
+    }
     IVIT_LAUNCH_CHECK();
     return 0;
   }

@@ -122,6 +122,21 @@ IVIT_DEV void load8f(const T* p, float (&x)[8], int nv) {
   }
 }
 
+// Raw v_exp_f32 (2^x; results below 2^-126 flush to 0 — harmless for softmax weights).
+// exp2f() adds a denormal range reduction: 4-5 VALU ops per call.
+IVIT_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Combine a value with its lane^32 partner without LDS: v_permlane32_swap exchanges the
+// wave halves, so max/sum of the pair is symmetric (cdna_hip_programming.md T12).
+IVIT_DEV float half_swap_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+IVIT_DEV float half_swap_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 IVIT_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
