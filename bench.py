@@ -12,7 +12,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -90,22 +89,24 @@ def main():
     ap.add_argument("--grid", type=str, default="400x720")
     ap.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--bucket-mb", type=int, default=64)
+    ap.add_argument("--bucket-mb", type=float, default=64)
+    ap.add_argument("--ddp", choices=["buckets", "torch"], default="buckets",
+                    help="gradient exchange: ddp.GradBuckets (default) or torch DistributedDataParallel")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    sys.path.insert(0, PKG)
+    from ddp import init_distributed
+    rank, local, world, dev = init_distributed()
+    if dev.type != "cuda":
+        raise RuntimeError("bench.py needs a ROCm GPU (the HIP kernels have no CPU path)")
 
     import loss as L
     import model_vit
     import ops
     import utils
     from optim import FusedAdamW
+    from synthetic import synthetic_batch
+    from trainer import Trainer
 
     H, W = (int(v) for v in args.grid.split("x"))
     B = args.batch
@@ -113,30 +114,21 @@ def main():
     torch.manual_seed(0)
     model = model_vit.IntentNetViT(backbone_cfg={"img_size": (H, W)}).to(dev).set_compute_dtype(cd).train()
     net = model
-    if world > 1:
+    if world > 1 and args.ddp == "torch":
         net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
                                                         gradient_as_bucket_view=True, broadcast_buffers=False)
     opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
     lf = L.DetectionIntentionLoss(use_rotated_iou=False, apply_intention_downsampling=True)
     anchors = utils.generate_anchors(H, W, 8, device=dev)
-    g = torch.Generator().manual_seed(1234 + rank)
-    lidar = torch.rand((B, 290, H, W), generator=g).to(dev)
-    mp = (torch.rand((B, 9, H, W), generator=g) < 0.1).float().to(dev)
-    sc = H / 400.0
-    gts = []
-    for _ in range(B):
-        u = torch.rand((20, 5), generator=g)
-        boxes = torch.stack([-20 * sc + 80 * sc * u[:, 0], -72 * sc + 144 * sc * u[:, 1], 1.5 + 1.5 * u[:, 2],
-                             3.5 + 3.0 * u[:, 3], -math.pi + 2 * math.pi * u[:, 4]], 1)
-        gts.append({"boxes_xywha": boxes, "intentions": torch.randint(0, 8, (20,), generator=g)})
+    # inputs resident in HBM before the timed region (SURVEY.md §8d primary placement)
+    batch = synthetic_batch(B, (H, W), torch.Generator().manual_seed(1234 + rank), device=dev)
+    trainer = Trainer(net, lf, opt, anchors, world=world if args.ddp == "buckets" else 1,
+                      bucket_mb=args.bucket_mb, check_nan=False)
+    if trainer.buckets is None and world > 1 and args.ddp == "buckets":
+        raise RuntimeError("gradient buckets missing for world > 1")
 
     def step():
-        opt.zero_grad(set_to_none=True)
-        c, b, i = net(lidar, mp)
-        d = lf(c, b, i, anchors, gts)
-        d["loss"].backward()
-        opt.step()
-        return d
+        return trainer.step(batch)
 
     for _ in range(args.warmup):
         step()

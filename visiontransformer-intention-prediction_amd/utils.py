@@ -89,6 +89,31 @@ def apply_nms(boxes_xywha: torch.Tensor, scores: torch.Tensor, iou_threshold: fl
     return keep[: int(count.item())]
 
 
+def postprocess_batch(cls_logits: torch.Tensor, box_preds_rel: torch.Tensor, intent_logits: torch.Tensor,
+                      anchors: torch.Tensor, conf_threshold: float = 0.1, nms_threshold: float = 0.2):
+    """eval_vit.py:157-180 for a whole batch: sigmoid → score >= conf → decode → NMS → argmax
+    intention, per sample; returns [{'pred_scores', 'pred_boxes_xywha', 'pred_intentions'}]
+    as device tensors (the caller moves them to the host when it needs them)."""
+    B = cls_logits.shape[0]
+    scores = torch.sigmoid(cls_logits.reshape(B, -1).float())
+    box = box_preds_rel.reshape(B, scores.shape[1], -1)
+    it = intent_logits.reshape(B, scores.shape[1], -1)
+    out = []
+    for b in range(B):
+        idx = torch.nonzero(scores[b] >= conf_threshold).squeeze(1)
+        res = {"pred_scores": scores.new_empty((0,)), "pred_boxes_xywha": scores.new_empty((0, 5)),
+               "pred_intentions": torch.empty((0,), dtype=torch.long, device=scores.device)}
+        if idx.numel() > 0:
+            sf = scores[b].index_select(0, idx)
+            dec = decode_box_predictions(box[b].index_select(0, idx), anchors.index_select(0, idx))
+            keep = apply_nms(dec, sf, nms_threshold)
+            if keep.numel() > 0:
+                res = {"pred_scores": sf[keep], "pred_boxes_xywha": dec[keep],
+                       "pred_intentions": torch.argmax(it[b].index_select(0, idx)[keep], dim=-1)}
+        out.append(res)
+    return out
+
+
 def calculate_ap(recall: np.ndarray, precision: np.ndarray) -> float:
     """utils.py:564-575 (VOC-style AP; host-side metric)."""
     mrec = np.concatenate(([0.0], recall, [1.0]))
