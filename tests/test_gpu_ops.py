@@ -29,7 +29,7 @@ def _lin_case(M, N, K, dtype):
     return x, w, b
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 200, 136), (1000, 1152, 384), (77, 64, 1536)])
+@pytest.mark.parametrize("M,N,K", [(300, 200, 136), (1000, 1152, 384), (77, 64, 1536), (9002, 384, 1152)])
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
 def test_linear_fwd_dgrad_wgrad(M, N, K, cd):
     import ops
@@ -61,6 +61,9 @@ def test_linear_fwd_dgrad_wgrad(M, N, K, cd):
     dw, db = ops.linear_wgrad(dyd, xd, cdt)
     assert _rel(dw, dy.double().T @ x.double()) < tol
     assert _rel(db, dy.double().sum(0)) < tol
+    # the bias gradient is an f32 sum of the exact operand values (fused into the bf16 GEMM)
+    assert _rel(db, dyd.float().cpu().double().sum(0)) < 1e-5
+    assert _rel(dw, dyd.float().cpu().double().T @ xd.float().cpu().double()) < 1e-5
 
 
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
@@ -141,7 +144,7 @@ def test_conv_nhwc(k, cd):
     assert _rel(dx.reshape(B, H, W, Cin).permute(0, 3, 1, 2), xr.grad) < tol
     gp, db = ops.conv_wgrad(dyh, xh, B, H, W, Cin, Cout, k, cdt, want_bias=True)
     assert _rel(ops.unpack_conv_grad(gp, Cout, Cin, k), wr.grad) < tol
-    assert _rel(db, dyh.float().cpu().double().sum(0)) < tol
+    assert _rel(db, dyh.float().cpu().double().sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])

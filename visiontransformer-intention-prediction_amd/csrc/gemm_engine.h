@@ -11,6 +11,8 @@
 // bf16 path: 128x128x64 tile, 4 waves (2x2) x 64x64, v_mfma_f32_32x32x16_bf16.
 // f32  path: 128x128x16 tile, 4 waves (2x2) x 64x64, v_mfma_f32_32x32x2_f32 (exact f32).
 #pragma once
+#include <type_traits>
+
 #include "ivit_common.h"
 
 namespace ivit {
@@ -43,6 +45,23 @@ struct LdDense {
     return t;
   }
   IVIT_DEV long row_addr(int r) const { return rpb ? (long)(r / rpb) * rstride + roff + r % rpb : (long)r; }
+  // LDS-DMA fast path (see gemm_bf16_glds_kernel): the per-lane source of an image piece is
+  // a k-invariant 32-bit element offset plus a uniform per-K-tile advance. Rows / columns
+  // past the matrix edge are clamped to the last valid one — they only feed output rows or
+  // columns that the epilogue never stores; the K edge goes through the generic path.
+  static constexpr bool kLinear = true;
+  IVIT_DEV bool lin_ok(bool kc) const {
+    return R > 0 && C >= 8 && (kc || rpb == 0) && (row_addr(R - 1) + 65) * ld + C < 0x7fffffffL;
+  }
+  IVIT_DEV int lin_off(bool kc, int piece, int lane, int o0) const {
+    if (kc) {  // image rows = m/n (8 per piece), chunks along k
+      const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128_(row);
+      return (int)(row_addr(min(o0 + row, R - 1)) * ld) + c * 8;
+    }
+    const int row = piece * 4 + (lane >> 4), c = (lane & 15) ^ ((row & 3) << 2);  // rows = k
+    return (int)(row * ld) + min(o0 + c * 8, C - 8);
+  }
+  IVIT_DEV static int swz128_(int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 1) | ((r >> 2) & 1); }
   IVIT_DEV const void* src8(int, int r, int c) const {
     return (r >= R || c >= C) ? nullptr : (const void*)(p + row_addr(r) * ld + c);
   }
@@ -71,6 +90,7 @@ struct LdDense {
 // r = m = b*Np + gy*Wp + gx ; c = kk = (ch*P + ky)*P + kx  (chunk of 8 = one kx row).
 template <typename S>
 struct LdPatch {
+  static constexpr bool kLinear = false;
   static constexpr bool kRowFast = true;  // consecutive patches are consecutive 32-B runs
   static constexpr bool kGlds = false;    // f32 image converted to bf16 on the way: register staging
   IVIT_DEV LdPatch bind(int) const { return *this; }
@@ -102,6 +122,7 @@ struct LdPatch {
 // flip = true reads the spatially flipped tap (dgrad of the transposed conv).
 template <typename S>
 struct LdConv {
+  static constexpr bool kLinear = false;
   static constexpr bool kRowFast = false;
   static constexpr bool kGlds = sizeof(S) == 2;
   const S* x; int H, W, Cin, ks; int R, C; long ldc;  // ldc = channel stride of a pixel
@@ -143,6 +164,7 @@ struct LdConv {
 // (the flipped tap), col c = ci  ->  W[co][ks-1-ky'][ks-1-kx'][ci].
 template <typename S>
 struct LdConvWFlip {
+  static constexpr bool kLinear = false;
   static constexpr bool kRowFast = false;
   static constexpr bool kGlds = sizeof(S) == 2;
   const S* w; int Cout, Cin, ks; int R, C;
@@ -233,7 +255,11 @@ struct EpiGeluGrad {  // out = acc * gelu'(pre)
 };
 
 struct EpiSlab {  // split-K partial slab [split][M][N] (f32)
-  float* slab; long M, N;
+  // bslab != null (bf16 LDS-DMA path, MN-contiguous A only): the blocks of the first column
+  // tile also write per-split row sums of A, bslab[split][m] = sum_k A[m][k] — the bias
+  // gradient of a wgrad (colsum of dY) — computed on the MFMA pipe against a ones operand.
+  static constexpr bool kBiasOnes = true;
+  float* slab; long M, N; float* bslab = nullptr;
   IVIT_DEV EpiSlab bind(int) const { return *this; }
   IVIT_DEV void apply8(int, int split, int m, int n, const float (&v)[8], int nv) const {
     store8(slab + ((long)split * M + m) * N + n, v, nv);
@@ -557,11 +583,17 @@ IVIT_DEV void glds_piece(const L& ld, int z, bool kc, char* img, int piece, int 
                                    (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
 }
 
+template <class E, class = void>
+struct BiasOnes { static constexpr bool v = false; };
+template <class E>
+struct BiasOnes<E, std::void_t<decltype(E::kBiasOnes)>> { static constexpr bool v = E::kBiasOnes; };
+
 template <class LA, class LB, class EPI, bool A_KC, bool B_KC>
 __global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, EPI epi_, int M, int N, int K,
                                                               int tilesM, int tilesN, int splits, int kchunk) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][16384];  // [stage][A|B][image]
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 1, wn = wv & 1;  // wave-uniform (SGPR)
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = lin / tilesN, tn = lin - tm * tilesN;
   const int z = blockIdx.y / splits, split = blockIdx.y - z * splits;
@@ -572,11 +604,57 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, 
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int nk = (kend - kbeg + GBK16 - 1) / GBK16;
 
+  // Fast path for dense operands: k-invariant per-lane offsets, uniform per-tile advance
+  // (K-contiguous: +k0 elements; MN-contiguous: +k0 rows). Generic gather otherwise and
+  // for a partial last K tile.
+  int offA[4] = {0, 0, 0, 0}, offB[4] = {0, 0, 0, 0};
+  bool fastA = false, fastB = false;
+  if constexpr (LA::kLinear) {
+    fastA = la.lin_ok(A_KC);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) offA[i] = la.lin_off(A_KC, wv * 4 + i, lane, m0);
+  }
+  if constexpr (LB::kLinear) {
+    fastB = lb.lin_ok(B_KC);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) offB[i] = lb.lin_off(B_KC, wv * 4 + i, lane, n0);
+  }
   auto issue = [&](int stage, int k0) {
+    const bool full = k0 + GBK16 <= kend;
+    char* ia = smem[stage][0];
+    char* ib = smem[stage][1];
+    if constexpr (LA::kLinear) {
+      if (fastA && full) {
+        const auto* base = la.p + (A_KC ? (long)k0 : (long)k0 * la.ld);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds_piece(la, z, A_KC, smem[stage][0], wv * 4 + i, lane, m0, k0, kend);
+        for (int i = 0; i < 4; ++i)
+          __builtin_amdgcn_global_load_lds((const void*)(base + offA[i]),
+                                           (__attribute__((address_space(3))) void*)(ia + (wv * 4 + i) * 1024), 16,
+                                           0, 0);
+      } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds_piece(lb, z, B_KC, smem[stage][1], wv * 4 + i, lane, n0, k0, kend);
+        for (int i = 0; i < 4; ++i) glds_piece(la, z, A_KC, ia, wv * 4 + i, lane, m0, k0, kend);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds_piece(la, z, A_KC, ia, wv * 4 + i, lane, m0, k0, kend);
+    }
+    if constexpr (LB::kLinear) {
+      if (fastB && full) {
+        const auto* base = lb.p + (B_KC ? (long)k0 : (long)k0 * lb.ld);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          __builtin_amdgcn_global_load_lds((const void*)(base + offB[i]),
+                                           (__attribute__((address_space(3))) void*)(ib + (wv * 4 + i) * 1024), 16,
+                                           0, 0);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) glds_piece(lb, z, B_KC, ib, wv * 4 + i, lane, n0, k0, kend);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds_piece(lb, z, B_KC, ib, wv * 4 + i, lane, n0, k0, kend);
+    }
   };
 
   f32x16 acc[2][2];
@@ -586,6 +664,17 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, 
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  f32x16 accb;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) accb[r] = 0.f;
+  bool dob = false;
+  bf16x8 ones;
+  if constexpr (BiasOnes<EPI>::v) {
+    static_assert(!A_KC, "row sums of A need the MN-contiguous A image");
+    dob = epi.bslab != nullptr && tn == 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  }
 
   if (nk > 0) issue(0, kbeg);
   for (int kt = 0; kt < nk; ++kt) {
@@ -617,9 +706,24 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, 
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if constexpr (BiasOnes<EPI>::v) {
+        if (dob) {  // wave (wm, wn) sums A rows wm*64 + 32*wn .. +31 (one extra MFMA per 4)
+          if (wn == 0) accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], ones, accb, 0, 0, 0);
+          else accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], ones, accb, 0, 0, 0);
+        }
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of this stage are done
     __builtin_amdgcn_s_barrier();                         // ... everyone's, before it is refilled
+  }
+  if constexpr (BiasOnes<EPI>::v) {
+    if (dob && (lane & 31) == 0) {  // every column of accb holds the row sum; lanes 0 / 32 keep rows
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * wn + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < M) epi.bslab[(long)split * M + m] = accb[r];
+      }
+    }
   }
   epilogue_tile((float*)&smem[0][0][0] + wv * (32 * EP_LD), acc, epi, z, split, m0 + wm * 64, n0 + wn * 64, M, N,
                 lane);
@@ -638,6 +742,9 @@ int launch_gemm(bool bf16_path, const LA& la, const LB& lb, const EPI& epi, int 
   int kchunk = ivit_cdiv(ivit_cdiv(K, splits), bk) * bk;
   if (kchunk <= 0) kchunk = bk;
   dim3 grid(tilesM * tilesN, batch * splits);
+  if constexpr (BiasOnes<EPI>::v) {  // fused row sums exist only in the LDS-DMA kernel
+    if (epi.bslab && !(bf16_path && LA::kGlds && LB::kGlds)) return IVIT_ERR_UNSUPPORTED;
+  }
   if (bf16_path) {
     if constexpr (LA::kGlds && LB::kGlds)
       hipLaunchKernelGGL((gemm_bf16_glds_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N,

@@ -27,6 +27,35 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, long n, int
   out[i] = accumulate ? out[i] + s : s;
 }
 
+// Two slab sets in one launch: i < n0 -> out0[i] (+)= sum_s slab0[s][i]; else out1[i - n0]
+// (+)= sum_s slab1[s][i - n0] (weight gradient and its fused bias gradient).
+__global__ void splitk_reduce2_kernel(const float* __restrict__ slab0, long n0, float* __restrict__ out0,
+                                      const float* __restrict__ slab1, long n1, float* __restrict__ out1, int splits,
+                                      int accumulate) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const float* sl = slab0;
+  float* out = out0;
+  long n = n0;
+  if (i >= n0) {
+    i -= n0;
+    sl = slab1;
+    out = out1;
+    n = n1;
+    if (i >= n1) return;
+  }
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += sl[(long)k * n + i];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+static int reduce_wgrad(hipStream_t st, const float* slab, long n, float* dW, const float* bslab, long nb, float* db,
+                        int splits, int accumulate) {
+  hipLaunchKernelGGL(splitk_reduce2_kernel, dim3(ivit_cdiv(n + (bslab ? nb : 0), 256)), dim3(256), 0, st, slab, n, dW,
+                     bslab, bslab ? nb : 0, db, splits, accumulate);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
 // Column sums in two passes (deterministic): partial[chunk][col] then out[col].
 constexpr int CS_ROWS = 256;
 template <typename S>
@@ -147,16 +176,17 @@ static long wgrad_splits(long Mo, long No, long Kr, bool bf) {
 extern "C" long ivit_linear_wgrad_workspace(long M, long N, long K) {
   const long s = wgrad_splits(N, K, M, true) > wgrad_splits(N, K, M, false) ? wgrad_splits(N, K, M, true)
                                                                              : wgrad_splits(N, K, M, false);
-  return s * N * K * 4 + ivit_colsum_workspace(M, N);
+  const long cw = ivit_colsum_workspace(M, N);
+  return s * N * K * 4 + (s * N * 4 > cw ? s * N * 4 : cw);
 }
 
 template <typename S>
 static int linear_wgrad_t(const void* dY, long lddy, const void* X, long ldx, long M, long N, long K, float* slab,
-                          int splits, hipStream_t st) {
+                          float* bslab, int splits, hipStream_t st) {
   const bool bf = sizeof(S) == 2;
   LdDense<S> la{(const S*)dY, lddy, (int)M, (int)N, 0, 0, 0, {}};  // A[n][m] (MN-contig), rows = m
   LdDense<S> lb{(const S*)X, ldx, (int)M, (int)K, 0, 0, 0, {}};    // B[m][k] (MN-contig)
-  EpiSlab e{slab, N, K};
+  EpiSlab e{slab, N, K, bslab};
   return launch_gemm<false, false>(bf, la, lb, e, N, K, M, 1, splits, st);
 }
 
@@ -170,13 +200,13 @@ extern "C" int ivit_linear_wgrad(int dtype, const void* dY, long lddy, const voi
   const bool bf = dtype == IVIT_BF16;
   const int splits = (int)wgrad_splits(N, K, M, bf);
   float* slab = (float*)work;
-  int rc = bf ? linear_wgrad_t<bf16>(dY, lddy, X, ldx, M, N, K, slab, splits, st)
-              : linear_wgrad_t<float>(dY, lddy, X, ldx, M, N, K, slab, splits, st);
+  float* bslab = (bf && dbias) ? slab + (long)splits * N * K : nullptr;  // bias fused into the bf16 GEMM
+  int rc = bf ? linear_wgrad_t<bf16>(dY, lddy, X, ldx, M, N, K, slab, bslab, splits, st)
+              : linear_wgrad_t<float>(dY, lddy, X, ldx, M, N, K, slab, nullptr, splits, st);
   if (rc) return rc;
-  const long n = N * K;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dW, accumulate);
-  IVIT_LAUNCH_CHECK();
-  if (dbias) {
+  rc = reduce_wgrad(st, slab, N * K, dW, bslab, N, dbias, splits, accumulate);
+  if (rc) return rc;
+  if (dbias && !bslab) {
     char* cw = (char*)work + (long)splits * N * K * 4;
     rc = ivit_colsum(dY, dtype, lddy, 0, 0, 0, M, N, dbias, accumulate, cw, ivit_colsum_workspace(M, N), stream);
     if (rc) return rc;
@@ -333,17 +363,18 @@ extern "C" long ivit_conv_wgrad_workspace(long B, long H, long W, long Cin, long
   long s = wgrad_splits(Cout, Kc, M, false);
   const long s2 = wgrad_splits(Cout, Kc, M, true);
   if (s2 > s) s = s2;
-  return s * Cout * Kc * 4 + ivit_colsum_workspace(M, Cout);
+  const long cw = ivit_colsum_workspace(M, Cout);
+  return s * Cout * Kc * 4 + (s * Cout * 4 > cw ? s * Cout * 4 : cw);
 }
 
 template <typename S>
 static int conv_wgrad_t(const void* dY, long lddy, const void* X, long B, long H, long W, long Cin, long Cout,
-                        long ks, float* slab, int splits, hipStream_t st) {
+                        long ks, float* slab, float* bslab, int splits, hipStream_t st) {
   const bool bf = sizeof(S) == 2;
   const int M = (int)(B * H * W), Kc = (int)(ks * ks * Cin);
   LdDense<S> la{(const S*)dY, lddy, M, (int)Cout, 0, 0, 0, {}};                 // A[co][m]
   LdConv<S> lb{(const S*)X, (int)H, (int)W, (int)Cin, (int)ks, M, Kc, Cin};    // B[m][kk]
-  EpiSlab e{slab, Cout, Kc};
+  EpiSlab e{slab, Cout, Kc, bslab};
   return launch_gemm<false, false>(bf, la, lb, e, (int)Cout, Kc, M, 1, splits, st);
 }
 
@@ -357,13 +388,14 @@ extern "C" int ivit_conv_wgrad(int dtype, const void* dY, long lddy, const void*
   const long M = B * H * W, Kc = ks * ks * Cin;
   const int splits = (int)wgrad_splits(Cout, Kc, M, bf);
   float* slab = (float*)work;
-  int rc = bf ? conv_wgrad_t<bf16>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, splits, st)
-              : conv_wgrad_t<float>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, splits, st);
-  if (rc) return rc;
   const long n = Cout * Kc;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dWp, accumulate);
-  IVIT_LAUNCH_CHECK();
-  if (dbias) {
+  float* bslab = (bf && dbias) ? slab + (long)splits * n : nullptr;
+  int rc = bf ? conv_wgrad_t<bf16>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, bslab, splits, st)
+              : conv_wgrad_t<float>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, nullptr, splits, st);
+  if (rc) return rc;
+  rc = reduce_wgrad(st, slab, n, dWp, bslab, Cout, dbias, splits, accumulate);
+  if (rc) return rc;
+  if (dbias && !bslab) {
     char* cw = (char*)work + (long)splits * n * 4;
     return ivit_colsum(dY, dtype, lddy, 0, 0, 0, M, Cout, dbias, accumulate, cw, ivit_colsum_workspace(M, Cout),
                        stream);
