@@ -169,7 +169,7 @@ def main():
         "config": {"workload": f"IntentNetViT train step (fwd+loss+bwd+AdamW), {args.dtype}, {H}x{W}, "
                                f"batch {B}/GPU", "global_batch": gb, "per_gpu_batch": B, "grid": [H, W],
                    "tokens_per_stream": N, "parallelism": f"dp{world}"},
-        "roofline": {"kernel": "attn_fwd_bf16_kernel (ivit_attn_fwd)", "bound": "mfma",
+        "roofline": {"kernel": "attn_fwd_bf16_v4_kernel<4> (ivit_attn_fwd)", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": None,
                      "per_launch": f"4*B*H*N^2*64 = {afl:.4g} flop (B={B}, H=6, N={N}); {attn_ms:.4f} ms avg over "

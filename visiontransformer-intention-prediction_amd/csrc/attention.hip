@@ -466,6 +466,94 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v3_kernel(const b
   }
 }
 
+// ------------------------------------------------------------------------- forward v4 (bf16)
+// v3 with (a) k-invariant per-lane DMA source offsets (a full tile is base + r0*ld + off,
+// the row guard only on the ragged last tile) and (b) the tile loop unrolled by two so the
+// LDS stage is a compile-time constant: every fragment read is a per-lane base plus an
+// immediate offset instead of fresh address arithmetic per tile.
+template <int W>
+IVIT_DEV int dma_off(int i, int wv, int lane, long ld) {
+  const int piece = wv * (8 / W) + i;
+  const int row = piece * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ swz128(row);
+  return (int)(row * ld) + c * 8;
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v4_kernel(const bf16* __restrict__ qkv, int N, int H,
+                                                                        bf16* __restrict__ out,
+                                                                        float* __restrict__ lse, float c2) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int q = blockIdx.x * (32 * W) + wv * 32 + (lane & 31);
+  bf16x8 qf[4];
+  load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
+  f32x16 o0 = zero16(), o1 = zero16();
+  float m = NEG_BIG, l = 0.f;
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  int off[8 / W];
+#pragma unroll
+  for (int i = 0; i < 8 / W; ++i) off[i] = dma_off<W>(i, wv, lane, ld);
+  auto issue = [&](int kt, char* kimg, char* vimg) {
+    if (kt < nfull) {
+      const bf16* kb = Kb + (long)kt * AK * ld;
+      const bf16* vb = Vb + (long)kt * AK * ld;
+#pragma unroll
+      for (int i = 0; i < 8 / W; ++i) {
+        const int piece = wv * (8 / W) + i;
+        __builtin_amdgcn_global_load_lds((const void*)(kb + off[i]),
+                                         (__attribute__((address_space(3))) void*)(kimg + piece * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(vb + off[i]),
+                                         (__attribute__((address_space(3))) void*)(vimg + piece * 1024), 16, 0, 0);
+      }
+    } else {
+      tile_glds_w<W>(Kb, ld, kt * AK, N, kimg, wv, lane);
+      tile_glds_w<W>(Vb, ld, kt * AK, N, vimg, wv, lane);
+    }
+  };
+  auto step = [&](auto stage, int kt) {
+    constexpr int S = decltype(stage)::value;
+    if (kt + 1 < nt) issue(kt + 1, smem[S ^ 1][0], smem[S ^ 1][1]);
+    if (kt < nfull)
+      fwd_tile3<false>(smem[S][0], smem[S][1], qf, o0, o1, m, l, kt * AK, N, c2, lane);
+    else
+      fwd_tile3<true>(smem[S][0], smem[S][1], qf, o0, o1, m, l, kt * AK, N, c2, lane);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  issue(0, smem[0][0], smem[0][1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nt; kt += 2) {
+    step(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < nt) step(std::integral_constant<int, 1>{}, kt + 1);
+  }
+  if (q < N) {
+    const float inv = 1.f / l;
+    bf16* orow = out + ((long)b * N + q) * D + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      Pack4 a, c;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a.h[j] = (bf16)(o0[4 * g + j] * inv);
+        c.h[j] = (bf16)(o1[4 * g + j] * inv);
+      }
+      const int d = 8 * g + 4 * hl;
+      *(uint2*)(orow + d) = a.u;
+      *(uint2*)(orow + 32 + d) = c.u;
+    }
+    if (hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
+  }
+}
+
 // delta[z][q] = sum_d dO[q][d] O[q][d]   (one thread per (b, n, h) row of 64)
 template <typename T>
 __global__ void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__ dout, long B, int N, int H,
@@ -680,6 +768,284 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* _
   }
 }
 
+// ------------------------------------------------------------------------- backward v2 (bf16)
+// Row constants for the backward in a padded layout [z][Npad] (Npad = N rounded up to 64):
+// lse2 = lse * log2(e) (+1e30 on padding rows, so their probabilities are exactly 0) and
+// delta = rowsum(dO * O) (0 on padding). One thread per (z, padded row), 16-B loads.
+__global__ void attn_rows_v2_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                                    const float* __restrict__ lse, int B, int N, int Npad, int H,
+                                    float* __restrict__ lse2p, float* __restrict__ deltap) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * H * Npad) return;
+  const int z = (int)(i / Npad), n = (int)(i - (long)z * Npad);
+  if (n >= N) {
+    lse2p[i] = 1e30f;
+    deltap[i] = 0.f;
+    return;
+  }
+  const int b = z / H, h = z - b * H, D = H * 64;
+  const uint4* a = (const uint4*)(o + ((long)b * N + n) * D + h * 64);
+  const uint4* g = (const uint4*)(dout + ((long)b * N + n) * D + h * 64);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    Pack8 x, y;
+    x.u = a[k];
+    y.u = g[k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s = fmaf(bf2f(x.h[j]), bf2f(y.h[j]), s);
+  }
+  deltap[i] = s;
+  lse2p[i] = lse[(long)z * N + n] * LOG2E;
+}
+
+// One dQ tile step: keys kbase.. of the K/V images against this wave's 32 queries.
+template <bool MASK>
+IVIT_DEV void dq_tile(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], const bf16x8 (&gf)[4], f32x16& a0,
+                      f32x16& a1, float lse2, float dlt, int kbase, int N, float c2, int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x16 s = zero16(), dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] = -dlt;  // row constant as the initial accumulator
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      const bf16x8 va = *(const bf16x8*)(vimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, gf[ks], dp, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = fast_exp2(fmaf(s[r], c2, -lse2));
+      if (MASK) {
+        const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (key >= N) p = 0.f;
+      }
+      s[r] = p * dp[r];  // dS^T[key][q]
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const bf16x8 xa = pack_acc(s, ss);
+      const int rb = 32 * t + 16 * ss;
+      const bf16x8 kb0 = tr_acc_order(kimg, rb, 0, lane);
+      const bf16x8 kb1 = tr_acc_order(kimg, rb, 32, lane);
+      a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, kb0, a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, kb1, a1, 0, 0, 0);
+    }
+  }
+}
+
+// dQ: 4 waves x 32 queries; K/V tiles by LDS-DMA (k-invariant offsets, ragged tail guarded),
+// tile loop unrolled by two so the LDS stage is a compile-time constant.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __restrict__ qkv,
+                                                                const bf16* __restrict__ dout,
+                                                                const float* __restrict__ lse2p,
+                                                                const float* __restrict__ deltap, int N, int Npad,
+                                                                int H, bf16* __restrict__ dqkv, float c2,
+                                                                float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int q = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  const bool qv = q < N;
+  bf16x8 qf[4], gf[4];
+  load_row_frags(Qb + (long)q * ld, qv, lane, qf);
+  load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
+  const float lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
+  const float dlt = qv ? deltap[(long)z * Npad + q] : 0.f;
+  f32x16 a0 = zero16(), a1 = zero16();
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  int off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) off[i] = dma_off<4>(i, wv, lane, ld);
+  auto issue = [&](int kt, char* kimg, char* vimg) {
+    if (kt < nfull) {
+      const bf16* kb = Kb + (long)kt * AK * ld;
+      const bf16* vb = Vb + (long)kt * AK * ld;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int piece = wv * 2 + i;
+        __builtin_amdgcn_global_load_lds((const void*)(kb + off[i]),
+                                         (__attribute__((address_space(3))) void*)(kimg + piece * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(vb + off[i]),
+                                         (__attribute__((address_space(3))) void*)(vimg + piece * 1024), 16, 0, 0);
+      }
+    } else {
+      tile_glds_w<4>(Kb, ld, kt * AK, N, kimg, wv, lane);
+      tile_glds_w<4>(Vb, ld, kt * AK, N, vimg, wv, lane);
+    }
+  };
+  auto step = [&](auto stage, int kt) {
+    constexpr int S = decltype(stage)::value;
+    if (kt + 1 < nt) issue(kt + 1, smem[S ^ 1][0], smem[S ^ 1][1]);
+    if (kt < nfull)
+      dq_tile<false>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane);
+    else
+      dq_tile<true>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  issue(0, smem[0][0], smem[0][1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nt; kt += 2) {
+    step(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < nt) step(std::integral_constant<int, 1>{}, kt + 1);
+  }
+  const int qw = blockIdx.x * AQ + wv * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qq = qw + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    if (qq < N) {
+      bf16* row = dqkv + ((long)b * N + qq) * ld + h * 64;
+      row[lane & 31] = (bf16)(a0[r] * scale);
+      row[32 + (lane & 31)] = (bf16)(a1[r] * scale);
+    }
+  }
+}
+
+// One dK/dV tile step: queries of the Q/dO images (rows past N are zero with lse2 = 1e30,
+// so P = 0 there and no mask is needed) against this wave's 32 keys.
+IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, const float* drow,
+                       const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], f32x16& dk0, f32x16& dk1, f32x16& dv0,
+                       f32x16& dv1, float c2, int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x16 s = zero16(), dp;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j: -delta as the initial accumulator
+      const float4 d4 = *(const float4*)(drow + 32 * t + 8 * g + 4 * hl);
+      dp[4 * g + 0] = -d4.x; dp[4 * g + 1] = -d4.y; dp[4 * g + 2] = -d4.z; dp[4 * g + 3] = -d4.w;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 qa = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      const bf16x8 ga = *(const bf16x8*)(gimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[ks], dp, 0, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 l4 = *(const float4*)(lrow + 32 * t + 8 * g + 4 * hl);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = fast_exp2(fmaf(s[4 * g + j], c2, -lv[j]));
+        s[4 * g + j] = p;                  // P[q][key]
+        dp[4 * g + j] = p * dp[4 * g + j];  // dS[q][key]
+      }
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const int rb = 32 * t + 16 * ss;
+      const bf16x8 pa = pack_acc(s, ss);
+      const bf16x8 g0 = tr_acc_order(gimg, rb, 0, lane);
+      const bf16x8 g1 = tr_acc_order(gimg, rb, 32, lane);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, g0, dv0, 0, 0, 0);
+      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, g1, dv1, 0, 0, 0);
+      const bf16x8 da = pack_acc(dp, ss);
+      const bf16x8 q0 = tr_acc_order(qimg, rb, 0, lane);
+      const bf16x8 q1 = tr_acc_order(qimg, rb, 32, lane);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, q0, dk0, 0, 0, 0);
+      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, q1, dk1, 0, 0, 0);
+    }
+  }
+}
+
+// dK/dV: 4 waves x 32 keys; Q, dO tiles and their lse2 / delta rows by LDS-DMA.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __restrict__ qkv,
+                                                                 const bf16* __restrict__ dout,
+                                                                 const float* __restrict__ lse2p,
+                                                                 const float* __restrict__ deltap, int N, int Npad,
+                                                                 int H, bf16* __restrict__ dqkv, float c2,
+                                                                 float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][Q|dO]
+  __shared__ __attribute__((aligned(16))) float srow[2][2][AK];    // [stage][lse2|delta]
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const bf16* Gb = dout + (long)b * N * D + h * 64;
+  const float* L = lse2p + (long)z * Npad;
+  const float* Dl = deltap + (long)z * Npad;
+  const int key = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  bf16x8 kf[4], vf[4];
+  load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
+  load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
+  f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  int offq[2], offg[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    offq[i] = dma_off<4>(i, wv, lane, ld);
+    offg[i] = dma_off<4>(i, wv, lane, D);
+  }
+  auto issue = [&](int qt, int S) {
+    char* qimg = smem[S][0];
+    char* gimg = smem[S][1];
+    if (qt < nfull) {
+      const bf16* qb = Qb + (long)qt * AK * ld;
+      const bf16* gb = Gb + (long)qt * AK * D;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int piece = wv * 2 + i;
+        __builtin_amdgcn_global_load_lds((const void*)(qb + offq[i]),
+                                         (__attribute__((address_space(3))) void*)(qimg + piece * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(gb + offg[i]),
+                                         (__attribute__((address_space(3))) void*)(gimg + piece * 1024), 16, 0, 0);
+      }
+    } else {
+      tile_glds_w<4>(Qb, ld, qt * AK, N, qimg, wv, lane);
+      tile_glds_w<4>(Gb, D, qt * AK, N, gimg, wv, lane);
+    }
+    if (wv == 0) {  // 64 lse2 + 64 delta floats (the padded arrays cover every tile row)
+      __builtin_amdgcn_global_load_lds((const void*)(L + qt * AK + lane),
+                                       (__attribute__((address_space(3))) void*)(&srow[S][0][0]), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Dl + qt * AK + lane),
+                                       (__attribute__((address_space(3))) void*)(&srow[S][1][0]), 4, 0, 0);
+    }
+  };
+  auto step = [&](auto stage, int qt) {
+    constexpr int S = decltype(stage)::value;
+    if (qt + 1 < nt) issue(qt + 1, S ^ 1);
+    dkv_tile(smem[S][0], smem[S][1], srow[S][0], srow[S][1], kf, vf, dk0, dk1, dv0, dv1, c2, lane);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int qt = 0; qt < nt; qt += 2) {
+    step(std::integral_constant<int, 0>{}, qt);
+    if (qt + 1 < nt) step(std::integral_constant<int, 1>{}, qt + 1);
+  }
+  const int kw = blockIdx.x * AQ + wv * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    if (kk < N) {
+      bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
+      row[D + (lane & 31)] = (bf16)(dk0[r] * scale);
+      row[D + 32 + (lane & 31)] = (bf16)(dk1[r] * scale);
+      row[2 * D + (lane & 31)] = (bf16)dv0[r];
+      row[2 * D + 32 + (lane & 31)] = (bf16)dv1[r];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- f32 row kernels
 // S rows (already scaled) -> P = softmax, zero padding columns; lse = max + log(sum).
 __global__ void softmax_rows_kernel(float* __restrict__ S, long ldS, int N, float* __restrict__ lse) {
@@ -736,7 +1102,7 @@ long ld_scores(long N) { return (N + 7) / 8 * 8; }
 }  // namespace
 
 extern "C" long ivit_attn_workspace(int dtype, long B, long N, long H, long Dh, int backward) {
-  if (dtype == IVIT_BF16) return backward ? B * H * N * 4 : 0;
+  if (dtype == IVIT_BF16) return backward ? 2 * B * H * ((N + AK - 1) / AK * AK) * 4 : 0;
   const long one = B * H * N * ld_scores(N) * 4;
   return backward ? 2 * one : one;
 }
@@ -750,7 +1116,7 @@ extern "C" int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H,
   if (B * N * H == 0) return 0;
   if (dtype == IVIT_BF16) {
     const char* ev = getenv("IVIT_ATTN_FWD_VARIANT");
-    const int variant = ev ? atoi(ev) : 3;
+    const int variant = ev ? atoi(ev) : 5;
     if (variant == 1) {
       dim3 g(ivit_cdiv(N, AQ), B * H);
       hipLaunchKernelGGL(attn_fwd_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H, (bf16*)out,
@@ -762,6 +1128,14 @@ extern "C" int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H,
     } else if (variant == 3) {
       dim3 g(ivit_cdiv(N, 128), B * H);
       hipLaunchKernelGGL(attn_fwd_bf16_v3_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
+    } else if (variant == 5) {
+      dim3 g(ivit_cdiv(N, 128), B * H);
+      hipLaunchKernelGGL(attn_fwd_bf16_v4_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
+    } else if (variant == 6) {
+      dim3 g(ivit_cdiv(N, 256), B * H);
+      hipLaunchKernelGGL(attn_fwd_bf16_v4_kernel<8>, g, dim3(512), 0, st, (const bf16*)qkv, (int)N, (int)H,
                          (bf16*)out, lse, scale * LOG2E);
     } else {
       dim3 g(ivit_cdiv(N, 256), B * H);
@@ -798,10 +1172,25 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
   if (B * N * H == 0) return 0;
   const long D = H * Dh, ldq = 3 * D;
   if (dtype == IVIT_BF16) {
+    const char* ev = getenv("IVIT_ATTN_BWD_VARIANT");
+    const int variant = ev ? atoi(ev) : 2;
+    dim3 g(ivit_cdiv(N, AQ), B * H);
+    if (variant != 1) {
+      const long Npad = (N + AK - 1) / AK * AK;
+      float* lse2p = (float*)work;
+      float* deltap = lse2p + B * H * Npad;
+      hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad, 256)), dim3(256), 0, st, (const bf16*)out,
+                         (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
+      hipLaunchKernelGGL(attn_bwd_dq_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
+                         deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+      hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
+                         deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+      IVIT_LAUNCH_CHECK();
+      return 0;
+    }
     float* delta = (float*)work;
     hipLaunchKernelGGL(attn_delta_kernel<bf16>, dim3(ivit_cdiv(B * N * H, 256)), dim3(256), 0, st,
                        (const bf16*)out, (const bf16*)dout, B, (int)N, (int)H, delta);
-    dim3 g(ivit_cdiv(N, AQ), B * H);
     hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse, delta,
                        (int)N, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
     hipLaunchKernelGGL(attn_bwd_dkv_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse,

@@ -1,6 +1,8 @@
 // LayerNorm (timm Block norm1/norm2/norm, eps 1e-6; adapter LN eps 1e-5, model_vit.py:82-83)
 // and BatchNorm2d in training mode (BasicBlock bn1/bn2/downsample, model_vit.py:24-31) on
 // NHWC maps. All statistics in f32; column reductions are two-pass and deterministic.
+#include <stdlib.h>
+
 #include "ivit_common.h"
 
 namespace {
@@ -17,6 +19,167 @@ IVIT_DEV long rowmap(long r, long rpb, long rstride, long roff) {
 }
 
 constexpr int LN_MAXV = 8;  // D <= 512
+
+// ---- vectorised LayerNorm: one half-wave (32 lanes) per row, 16 B per lane per access,
+// 4 rows per half-wave in flight (a 256-thread block covers 32 rows). D % 128 == 0, D <= 512;
+// all row strides multiples of 4 and base pointers 16-B aligned (checked on the host).
+static inline bool al16h(const void* p) { return ((uintptr_t)p & 15) == 0; }
+// IVIT_LN_SCALAR=1 selects the one-wave-per-row kernels (A/B and numerics comparisons)
+static inline bool ln_scalar() {
+  const char* v = getenv("IVIT_LN_SCALAR");
+  return v && v[0] == '1';
+}
+IVIT_DEV long rowmap32(int r, int rpb, int rstride, int roff) {
+  return rpb ? (long)(r / rpb) * rstride + roff + r % rpb : (long)r;
+}
+IVIT_DEV float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 32);
+  return v;
+}
+template <typename T> IVIT_DEV float4 ld4(const T* p);
+template <> IVIT_DEV float4 ld4<float>(const float* p) { return *(const float4*)p; }
+template <> IVIT_DEV float4 ld4<bf16>(const bf16* p) {
+  Pack4 t;
+  t.u = *(const uint2*)p;
+  return make_float4(bf2f(t.h[0]), bf2f(t.h[1]), bf2f(t.h[2]), bf2f(t.h[3]));
+}
+template <typename T> IVIT_DEV void st4(T* p, float4 v);
+template <> IVIT_DEV void st4<float>(float* p, float4 v) { *(float4*)p = v; }
+template <> IVIT_DEV void st4<bf16>(bf16* p, float4 v) {
+  Pack4 t;
+  t.h[0] = f2bf(v.x); t.h[1] = f2bf(v.y); t.h[2] = f2bf(v.z); t.h[3] = f2bf(v.w);
+  *(uint2*)p = t.u;
+}
+constexpr int LNV_ROWS = 4;  // rows per half-wave
+
+template <typename TO, int NC>
+__global__ __launch_bounds__(256) void ln_fwd_vec_kernel(const float* __restrict__ X, long ldx, int rpb, int rstride,
+                                                         int roff, int M, const float* __restrict__ g,
+                                                         const float* __restrict__ bta, float eps, TO* __restrict__ Y,
+                                                         long ldy, float* __restrict__ mean,
+                                                         float* __restrict__ rstd) {
+  constexpr int D = NC * 128;
+  const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31;
+  float4 gg[NC], bb[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    gg[i] = *(const float4*)(g + 4 * (hl + 32 * i));
+    bb[i] = *(const float4*)(bta + 4 * (hl + 32 * i));
+  }
+  const int r0 = (blockIdx.x * 8 + hw) * LNV_ROWS;
+#pragma unroll
+  for (int k = 0; k < LNV_ROWS; ++k) {
+    const int row = r0 + k;
+    if (row < M) {
+      const float* x = X + rowmap32(row, rpb, rstride, roff) * ldx;
+      float4 v[NC];
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        v[i] = *(const float4*)(x + 4 * (hl + 32 * i));
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+      }
+      const float mu = half_sum(s) * (1.0f / D);
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const float a = v[i].x - mu, b = v[i].y - mu, c = v[i].z - mu, d = v[i].w - mu;
+        q += (a * a + b * b) + (c * c + d * d);
+      }
+      const float rs = 1.0f / sqrtf(half_sum(q) * (1.0f / D) + eps);
+      TO* y = Y + (long)row * ldy;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        float4 o;
+        o.x = (v[i].x - mu) * rs * gg[i].x + bb[i].x;
+        o.y = (v[i].y - mu) * rs * gg[i].y + bb[i].y;
+        o.z = (v[i].z - mu) * rs * gg[i].z + bb[i].z;
+        o.w = (v[i].w - mu) * rs * gg[i].w + bb[i].w;
+        st4<TO>(y + 4 * (hl + 32 * i), o);
+      }
+      if (hl == 0) { mean[row] = mu; rstd[row] = rs; }
+    }
+  }
+}
+
+// dX(f32) = dres + rs*(g*dy - mean(g*dy) - xhat*mean(g*dy*xhat)); dXs = TS(dX * scale);
+// per-block partial column sums of dy*xhat and dy -> part[blk][2][D]
+template <typename TY, typename TS, int NC>
+__global__ __launch_bounds__(256) void ln_bwd_vec_kernel(const float* __restrict__ X, long ldx, int rpb, int rstride,
+                                                         int roff, int M, const float* __restrict__ g,
+                                                         const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, const TY* __restrict__ dY,
+                                                         long lddy, const float* dres, float* dX, long lddx,
+                                                         TS* __restrict__ dXs, const float* __restrict__ rscale,
+                                                         int rps, float* __restrict__ part) {
+  constexpr int D = NC * 128;
+  const int hw = threadIdx.x >> 5, hl = threadIdx.x & 31;
+  float4 gg[NC], pg[NC], pb[NC];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    gg[i] = *(const float4*)(g + 4 * (hl + 32 * i));
+    pg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    pb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int r0 = (blockIdx.x * 8 + hw) * LNV_ROWS;
+#pragma unroll
+  for (int k = 0; k < LNV_ROWS; ++k) {
+    const int row = r0 + k;
+    if (row < M) {
+      const long xr = rowmap32(row, rpb, rstride, roff);
+      const float* x = X + xr * ldx;
+      const TY* dy = dY + (long)row * lddy;
+      const float mu = mean[row], rs = rstd[row];
+      float4 xh[NC], gy[NC];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const int c = 4 * (hl + 32 * i);
+        const float4 xv = *(const float4*)(x + c);
+        const float4 d = ld4<TY>(dy + c);
+        xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+        gy[i] = make_float4(d.x * gg[i].x, d.y * gg[i].y, d.z * gg[i].z, d.w * gg[i].w);
+        s1 += (gy[i].x + gy[i].y) + (gy[i].z + gy[i].w);
+        s2 += (gy[i].x * xh[i].x + gy[i].y * xh[i].y) + (gy[i].z * xh[i].z + gy[i].w * xh[i].w);
+        pg[i].x += d.x * xh[i].x; pg[i].y += d.y * xh[i].y; pg[i].z += d.z * xh[i].z; pg[i].w += d.w * xh[i].w;
+        pb[i].x += d.x; pb[i].y += d.y; pb[i].z += d.z; pb[i].w += d.w;
+      }
+      s1 = half_sum(s1) * (1.0f / D);
+      s2 = half_sum(s2) * (1.0f / D);
+      const float sc = rscale ? rscale[row / rps] : 1.f;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const int c = 4 * (hl + 32 * i);
+        float4 o;
+        o.x = rs * (gy[i].x - s1 - xh[i].x * s2);
+        o.y = rs * (gy[i].y - s1 - xh[i].y * s2);
+        o.z = rs * (gy[i].z - s1 - xh[i].z * s2);
+        o.w = rs * (gy[i].w - s1 - xh[i].w * s2);
+        if (dres) {
+          const float4 r = *(const float4*)(dres + xr * lddx + c);
+          o.x += r.x; o.y += r.y; o.z += r.z; o.w += r.w;
+        }
+        *(float4*)(dX + xr * lddx + c) = o;
+        if (dXs) st4<TS>(dXs + (long)row * D + c, make_float4(o.x * sc, o.y * sc, o.z * sc, o.w * sc));
+      }
+    }
+  }
+  __shared__ float4 red[2][8][NC * 32];
+#pragma unroll
+  for (int i = 0; i < NC; ++i) { red[0][hw][hl + 32 * i] = pg[i]; red[1][hw][hl + 32 * i] = pb[i]; }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * NC * 32; t += 256) {
+    const int w = t / (NC * 32), c4 = t - w * (NC * 32);
+    float4 a = red[w][0][c4];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      const float4 b = red[w][j][c4];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    *(float4*)(part + ((long)blockIdx.x * 2 + w) * D + 4 * c4) = a;
+  }
+}
 
 // one wave per row, D % 64 == 0
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ X, long ldx, long rpb, long rstride,
@@ -214,8 +377,26 @@ extern "C" int ivit_layernorm_fwd(const float* X, long ldx, long rpb, long rstri
                                   float* mean, float* rstd, void* stream) {
   IVIT_CHECK_ARG(D % 64 == 0 && D <= 64 * LN_MAXV, "ivit_layernorm_fwd: D must be a multiple of 64, <= 512");
   if (M <= 0) return 0;
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3(ivit_cdiv(M, 4)), dim3(256), 0, ivit_stream(stream), X, ldx, rpb, rstride,
-                     roff, M, (int)D, gamma, beta, eps, Y, ldy, y_dtype, mean, rstd);
+  hipStream_t st = ivit_stream(stream);
+  const bool vec = !ln_scalar() && D % 128 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16h(X) && al16h(Y) && al16h(gamma) &&
+                   al16h(beta) && M < (1L << 30) && rstride < (1L << 30) && roff < (1L << 30) && rpb < (1L << 30);
+  if (vec) {
+    const dim3 grid(ivit_cdiv(M, 8 * LNV_ROWS));
+#define LNF(NC)                                                                                                   \
+  if (D == NC * 128) {                                                                                            \
+    if (y_dtype == IVIT_BF16)                                                                                     \
+      hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, NC>), grid, dim3(256), 0, st, X, ldx, (int)rpb, (int)rstride,    \
+                         (int)roff, (int)M, gamma, beta, eps, (bf16*)Y, ldy, mean, rstd);                         \
+    else                                                                                                          \
+      hipLaunchKernelGGL((ln_fwd_vec_kernel<float, NC>), grid, dim3(256), 0, st, X, ldx, (int)rpb, (int)rstride,   \
+                         (int)roff, (int)M, gamma, beta, eps, (float*)Y, ldy, mean, rstd);                        \
+  }
+    LNF(1) LNF(2) LNF(3) LNF(4)
+#undef LNF
+  } else {
+    hipLaunchKernelGGL(ln_fwd_kernel, dim3(ivit_cdiv(M, 4)), dim3(256), 0, st, X, ldx, rpb, rstride, roff, M, (int)D,
+                       gamma, beta, eps, Y, ldy, y_dtype, mean, rstd);
+  }
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -233,10 +414,31 @@ extern "C" int ivit_layernorm_bwd(const float* X, long ldx, long rpb, long rstri
   IVIT_CHECK_ARG(work_bytes >= ivit_layernorm_bwd_workspace(M, D), "ivit_layernorm_bwd: workspace too small");
   if (M <= 0) return 0;
   hipStream_t st = ivit_stream(stream);
-  const int nb = ivit_cdiv(M, 4 * LNB_ROWS);
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rpb, rstride, roff, M, (int)D, gamma, mean,
-                     rstd, dY, lddy, dy_dtype, dres, dX, lddx, dXs, dxs_dtype, row_scale,
-                     rows_per_scale > 0 ? rows_per_scale : 1, (float*)work);
+  const int nb = ivit_cdiv(M, 4 * LNB_ROWS);  // = cdiv(M, 8 * LNV_ROWS): both kernels cover 32 rows per block
+  const int rps = (int)(rows_per_scale > 0 ? rows_per_scale : 1);
+  const bool vec = !ln_scalar() && D % 128 == 0 && ldx % 4 == 0 && lddy % 4 == 0 && lddx % 4 == 0 && al16h(X) && al16h(dY) &&
+                   al16h(dX) && al16h(gamma) && (!dres || al16h(dres)) && (!dXs || al16h(dXs)) && M < (1L << 30) &&
+                   rstride < (1L << 30) && roff < (1L << 30) && rpb < (1L << 30);
+  if (vec) {
+#define LNB(NC, TY, TS)                                                                                              \
+  hipLaunchKernelGGL((ln_bwd_vec_kernel<TY, TS, NC>), dim3(nb), dim3(256), 0, st, X, ldx, (int)rpb, (int)rstride,     \
+                     (int)roff, (int)M, gamma, mean, rstd, (const TY*)dY, lddy, dres, dX, lddx, (TS*)dXs, row_scale, \
+                     rps, (float*)work)
+#define LNB_D(NC)                                                                                                    \
+  if (D == NC * 128) {                                                                                               \
+    if (dy_dtype == IVIT_BF16) {                                                                                     \
+      if (dxs_dtype == IVIT_BF16) LNB(NC, bf16, bf16); else LNB(NC, bf16, float);                                    \
+    } else {                                                                                                         \
+      if (dxs_dtype == IVIT_BF16) LNB(NC, float, bf16); else LNB(NC, float, float);                                  \
+    }                                                                                                                \
+  }
+    LNB_D(1) LNB_D(2) LNB_D(3) LNB_D(4)
+#undef LNB_D
+#undef LNB
+  } else {
+    hipLaunchKernelGGL(ln_bwd_kernel, dim3(nb), dim3(256), 0, st, X, ldx, rpb, rstride, roff, M, (int)D, gamma, mean,
+                       rstd, dY, lddy, dy_dtype, dres, dX, lddx, dXs, dxs_dtype, row_scale, (long)rps, (float*)work);
+  }
   launch_colreduce(st, (const float*)work, nb, 2 * D, (int)(2 * D), dgamma, (int)D, dbeta, accumulate);
   IVIT_LAUNCH_CHECK();
   return 0;
