@@ -37,7 +37,7 @@ o, lse = ops.attn_fwd(qkv, B, N, H, BF16)
 dref = None
 for rnd in range(2):
     for bv in ["1", "2"]:
-        os.environ["IVIT_ATTN_BWD_VARIANT"] = bv
+        os.environ["IVIT_ATTN_DKV_VARIANT"] = bv
         d = ops.attn_bwd(qkv, o, dout, lse, B, N, H, BF16)
         if dref is None:
             dref = d.float()

@@ -341,9 +341,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_v2_kernel(const bf16* __
 // v1's shape (32 queries per wave) with: K/V by LDS-DMA one tile ahead (no staging VGPRs),
 // key masking only on the last tile, the scale folded into one FMA before exp2, and the O
 // rescale skipped when no lane's max moved. WAVES = 4 or 8 waves per workgroup share a tile.
-template <bool MASK>
+// MSUM: the row sums l come from the MFMA pipe (a ones operand beside P·V, kept in lacc) instead
+// of 32 VALU adds per tile — the loop is VALU-issue-bound at head dim 64.
+template <bool MASK, bool MSUM = false>
 IVIT_DEV void fwd_tile3(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], f32x16& o0, f32x16& o1,
-                        float& m, float& l, int kbase, int N, float c2, int lane) {
+                        float& m, float& l, int kbase, int N, float c2, int lane, f32x16* lacc = nullptr) {
   const int hl = lane >> 5;
   f32x16 s[2];
 #pragma unroll
@@ -378,13 +380,21 @@ IVIT_DEV void fwd_tile3(const char* kimg, const char* vimg, const bf16x8 (&qf)[4
     for (int r = 0; r < 16; ++r) {
       const float p = fast_exp2(fmaf(s[t][r], c2, -mn));
       s[t][r] = p;
-      rs += p;
+      if (!MSUM) rs += p;
     }
-  rs = half_swap_sum(rs);
-  l = l * alpha + rs;
+  if (!MSUM) {
+    rs = half_swap_sum(rs);
+    l = l * alpha + rs;
+  }
   if (__any(moved)) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+    if (MSUM) (*lacc)[0] *= alpha;  // only element 0 is read back
+  }
+  bf16x8 ones;
+  if (MSUM) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -396,6 +406,7 @@ IVIT_DEV void fwd_tile3(const char* kimg, const char* vimg, const bf16x8 (&qf)[4
       const bf16x8 va1 = tr_acc_order(vimg, rb, 32, lane);
       o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, pb, o0, 0, 0, 0);
       o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, pb, o1, 0, 0, 0);
+      if (MSUM) *lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, *lacc, 0, 0, 0);
     }
 }
 
@@ -479,8 +490,8 @@ IVIT_DEV int dma_off(int i, int wv, int lane, long ld) {
   return (int)(row * ld) + c * 8;
 }
 
-template <int W>
-__global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v4_kernel(const bf16* __restrict__ qkv, int N, int H,
+template <int W, int MINB = 8 / W, bool MSUM = false>
+__global__ __launch_bounds__(64 * W, MINB) void attn_fwd_bf16_v4_kernel(const bf16* __restrict__ qkv, int N, int H,
                                                                         bf16* __restrict__ out,
                                                                         float* __restrict__ lse, float c2) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
@@ -495,7 +506,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v4_kernel(const b
   const int q = blockIdx.x * (32 * W) + wv * 32 + (lane & 31);
   bf16x8 qf[4];
   load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
-  f32x16 o0 = zero16(), o1 = zero16();
+  f32x16 o0 = zero16(), o1 = zero16(), lacc = zero16();
   float m = NEG_BIG, l = 0.f;
   const int nt = (N + AK - 1) / AK, nfull = N / AK;
   int off[8 / W];
@@ -522,9 +533,9 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v4_kernel(const b
     constexpr int S = decltype(stage)::value;
     if (kt + 1 < nt) issue(kt + 1, smem[S ^ 1][0], smem[S ^ 1][1]);
     if (kt < nfull)
-      fwd_tile3<false>(smem[S][0], smem[S][1], qf, o0, o1, m, l, kt * AK, N, c2, lane);
+      fwd_tile3<false, MSUM>(smem[S][0], smem[S][1], qf, o0, o1, m, l, kt * AK, N, c2, lane, &lacc);
     else
-      fwd_tile3<true>(smem[S][0], smem[S][1], qf, o0, o1, m, l, kt * AK, N, c2, lane);
+      fwd_tile3<true, MSUM>(smem[S][0], smem[S][1], qf, o0, o1, m, l, kt * AK, N, c2, lane, &lacc);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
@@ -535,6 +546,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v4_kernel(const b
     step(std::integral_constant<int, 0>{}, kt);
     if (kt + 1 < nt) step(std::integral_constant<int, 1>{}, kt + 1);
   }
+  if (MSUM) l = lacc[0];
   if (q < N) {
     const float inv = 1.f / l;
     bf16* orow = out + ((long)b * N + q) * D + h * 64;
@@ -554,115 +566,14 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v4_kernel(const b
   }
 }
 
-// delta[z][q] = sum_d dO[q][d] O[q][d]   (one thread per (b, n, h) row of 64)
-template <typename T>
-__global__ void attn_delta_kernel(const T* __restrict__ o, const T* __restrict__ dout, long B, int N, int H,
-                                  float* __restrict__ delta) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * N * H) return;
-  const int D = H * 64;
-  const long bn = i / H;
-  const int h = (int)(i - bn * H);
-  const T* a = o + bn * D + h * 64;
-  const T* g = dout + bn * D + h * 64;
-  float s = 0.f;
-#pragma unroll 8
-  for (int d = 0; d < 64; ++d) s += to_f32(a[d]) * to_f32(g[d]);
-  const long b = bn / N, n = bn - b * N;
-  delta[(b * H + h) * N + n] = s;
-}
-
-// ------------------------------------------------------------------------- dQ (bf16)
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16_kernel(const bf16* __restrict__ qkv,
-                                                                  const bf16* __restrict__ dout,
-                                                                  const float* __restrict__ lse,
-                                                                  const float* __restrict__ delta, int N, int H,
-                                                                  bf16* __restrict__ dqkv, float c2, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
-  const int q = blockIdx.x * AQ + wv * 32 + (lane & 31);
-  const bool qv = q < N;
-  bf16x8 qf[4], gf[4];
-  load_row_frags(Qb + (long)q * ld, qv, lane, qf);
-  load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
-  const float lse2 = qv ? lse[(long)z * N + q] * LOG2E : 1e30f;
-  const float dlt = qv ? delta[(long)z * N + q] : 0.f;
-
-  f32x16 a0 = zero16(), a1 = zero16();  // dQ[q][d]: col d, rows q
-  const int nt = (N + AK - 1) / AK;
-  uint4 rk[2], rv[2];
-  tile_gload(Kb, ld, 0, N, tid, rk);
-  tile_gload(Vb, ld, 0, N, tid, rv);
-  tile_sstore(smem[0][0], tid, rk);
-  tile_sstore(smem[0][1], tid, rv);
-  __syncthreads();
-  for (int kt = 0; kt < nt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nt) {
-      tile_gload(Kb, ld, (kt + 1) * AK, N, tid, rk);
-      tile_gload(Vb, ld, (kt + 1) * AK, N, tid, rv);
-    }
-    const char* kimg = smem[cur][0];
-    const char* vimg = smem[cur][1];
-    const int kbase = kt * AK;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-        const bf16x8 va = *(const bf16x8*)(vimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, gf[ks], dp, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const float p = key < N ? fast_exp2(fmaf(s[r], c2, -lse2)) : 0.f;
-        s[r] = p * (dp[r] - dlt);  // dS^T[key][q]
-      }
-      // dQ[q][d] += dS[q][key] K[key][d]  (X = dS^T as the A operand)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 xa = pack_acc(s, ss);
-        const int rb = 32 * t + 16 * ss;
-        const bf16x8 kb0 = tr_acc_order(kimg, rb, 0, lane);
-        const bf16x8 kb1 = tr_acc_order(kimg, rb, 32, lane);
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, kb0, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, kb1, a1, 0, 0, 0);
-      }
-    }
-    if (kt + 1 < nt) {
-      tile_sstore(smem[cur ^ 1][0], tid, rk);
-      tile_sstore(smem[cur ^ 1][1], tid, rv);
-    }
-    __syncthreads();
-  }
-  // a0/a1: rows = q within this wave's 32, col = d
-  const int qw = blockIdx.x * AQ + wv * 32;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int qq = qw + (r & 3) + 8 * (r >> 2) + 4 * hl;
-    if (qq < N) {
-      bf16* row = dqkv + ((long)b * N + qq) * ld + h * 64;
-      row[lane & 31] = (bf16)(a0[r] * scale);
-      row[32 + (lane & 31)] = (bf16)(a1[r] * scale);
-    }
-  }
-}
-
 // ------------------------------------------------------------------------- dK, dV (bf16)
+// (register-staged variant, IVIT_ATTN_DKV_VARIANT=1; rows from the padded lse2 / delta arrays)
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* __restrict__ qkv,
                                                                    const bf16* __restrict__ dout,
-                                                                   const float* __restrict__ lse,
-                                                                   const float* __restrict__ delta, int N, int H,
-                                                                   bf16* __restrict__ dqkv, float c2, float scale) {
+                                                                   const float* __restrict__ lse2p,
+                                                                   const float* __restrict__ deltap, int N, int Npad,
+                                                                   int H, bf16* __restrict__ dqkv, float c2,
+                                                                   float scale) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][Q|dO]
   __shared__ float srow[2][2][AK];                                  // [stage][lse2|delta]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
@@ -673,8 +584,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* _
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
   const bf16* Gb = dout + (long)b * N * D + h * 64;
-  const float* L = lse + (long)z * N;
-  const float* Dl = delta + (long)z * N;
+  const float* L = lse2p + (long)z * Npad;
+  const float* Dl = deltap + (long)z * Npad;
   const int key = blockIdx.x * AQ + wv * 32 + (lane & 31);
   bf16x8 kf[4], vf[4];
   load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
@@ -685,10 +596,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* _
   uint4 rq[2], rg[2];
   float rl = 0.f, rd = 0.f;
   auto rows_load = [&](int q0) {
-    if (tid < AK) {
-      const int qq = q0 + tid;
-      rl = qq < N ? L[qq] * LOG2E : 1e30f;
-      rd = qq < N ? Dl[qq] : 0.f;
+    if (tid < AK) {  // padded rows: lse2 = 1e30, delta = 0
+      rl = L[q0 + tid];
+      rd = Dl[q0 + tid];
     }
   };
   tile_gload(Qb, ld, 0, N, tid, rq);
@@ -771,32 +681,34 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* _
 // ------------------------------------------------------------------------- backward v2 (bf16)
 // Row constants for the backward in a padded layout [z][Npad] (Npad = N rounded up to 64):
 // lse2 = lse * log2(e) (+1e30 on padding rows, so their probabilities are exactly 0) and
-// delta = rowsum(dO * O) (0 on padding). One thread per (z, padded row), 16-B loads.
+// delta = rowsum(dO * O) (0 on padding). 8 lanes per (z, padded row), one 16-B load of O
+// and of dO each (a wave reads 8 whole 128-B row segments), reduced across the 8 lanes.
 __global__ void attn_rows_v2_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
                                     const float* __restrict__ lse, int B, int N, int Npad, int H,
                                     float* __restrict__ lse2p, float* __restrict__ deltap) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long i = t >> 3;  // (z, padded row)
+  const int part = (int)(t & 7);
   if (i >= (long)B * H * Npad) return;
+  // rows ordered n-major within (b, h): consecutive i share (b, h) -> contiguous stores
   const int z = (int)(i / Npad), n = (int)(i - (long)z * Npad);
-  if (n >= N) {
-    lse2p[i] = 1e30f;
-    deltap[i] = 0.f;
-    return;
-  }
-  const int b = z / H, h = z - b * H, D = H * 64;
-  const uint4* a = (const uint4*)(o + ((long)b * N + n) * D + h * 64);
-  const uint4* g = (const uint4*)(dout + ((long)b * N + n) * D + h * 64);
   float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  if (n < N) {
+    const int b = z / H, h = z - b * H, D = H * 64;
+    const long off = ((long)b * N + n) * D + h * 64 + part * 8;
     Pack8 x, y;
-    x.u = a[k];
-    y.u = g[k];
+    x.u = *(const uint4*)(o + off);
+    y.u = *(const uint4*)(dout + off);
 #pragma unroll
     for (int j = 0; j < 8; ++j) s = fmaf(bf2f(x.h[j]), bf2f(y.h[j]), s);
   }
-  deltap[i] = s;
-  lse2p[i] = lse[(long)z * N + n] * LOG2E;
+  s += __shfl_xor(s, 1, 8);
+  s += __shfl_xor(s, 2, 8);
+  s += __shfl_xor(s, 4, 8);
+  if (part == 0) {
+    deltap[i] = s;
+    lse2p[i] = n < N ? lse[(long)z * N + n] * LOG2E : 1e30f;
+  }
 }
 
 // One dQ tile step: keys kbase.. of the K/V images against this wave's 32 queries.
@@ -920,12 +832,7 @@ IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, co
   const int hl = lane >> 5;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    f32x16 s = zero16(), dp;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j: -delta as the initial accumulator
-      const float4 d4 = *(const float4*)(drow + 32 * t + 8 * g + 4 * hl);
-      dp[4 * g + 0] = -d4.x; dp[4 * g + 1] = -d4.y; dp[4 * g + 2] = -d4.z; dp[4 * g + 3] = -d4.w;
-    }
+    f32x16 s = zero16(), dp = zero16();
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const bf16x8 qa = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
@@ -933,15 +840,18 @@ IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, co
       s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
       dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[ks], dp, 0, 0, 0);
     }
+    // row constants read after the MFMA chains are issued (off the chains' critical path)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j
       const float4 l4 = *(const float4*)(lrow + 32 * t + 8 * g + 4 * hl);
+      const float4 d4 = *(const float4*)(drow + 32 * t + 8 * g + 4 * hl);
       const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+      const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float p = fast_exp2(fmaf(s[4 * g + j], c2, -lv[j]));
-        s[4 * g + j] = p;                  // P[q][key]
-        dp[4 * g + j] = p * dp[4 * g + j];  // dS[q][key]
+        s[4 * g + j] = p;                             // P[q][key]
+        dp[4 * g + j] = p * (dp[4 * g + j] - dv[j]);  // dS[q][key]
       }
     }
 #pragma unroll
@@ -1133,6 +1043,14 @@ extern "C" int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H,
       dim3 g(ivit_cdiv(N, 128), B * H);
       hipLaunchKernelGGL(attn_fwd_bf16_v4_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
                          (bf16*)out, lse, scale * LOG2E);
+    } else if (variant == 8) {  // v4 with the row sums on the MFMA pipe
+      dim3 g(ivit_cdiv(N, 128), B * H);
+      hipLaunchKernelGGL((attn_fwd_bf16_v4_kernel<4, 2, true>), g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
+    } else if (variant == 7) {  // v4 held to 3 workgroups (12 waves) per CU
+      dim3 g(ivit_cdiv(N, 128), B * H);
+      hipLaunchKernelGGL((attn_fwd_bf16_v4_kernel<4, 3>), g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
     } else if (variant == 6) {
       dim3 g(ivit_cdiv(N, 256), B * H);
       hipLaunchKernelGGL(attn_fwd_bf16_v4_kernel<8>, g, dim3(512), 0, st, (const bf16*)qkv, (int)N, (int)H,
@@ -1172,29 +1090,22 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
   if (B * N * H == 0) return 0;
   const long D = H * Dh, ldq = 3 * D;
   if (dtype == IVIT_BF16) {
-    const char* ev = getenv("IVIT_ATTN_BWD_VARIANT");
-    const int variant = ev ? atoi(ev) : 2;
+    const char* ev = getenv("IVIT_ATTN_DKV_VARIANT");
+    const int dkv_variant = ev ? atoi(ev) : 2;
     dim3 g(ivit_cdiv(N, AQ), B * H);
-    if (variant != 1) {
-      const long Npad = (N + AK - 1) / AK * AK;
-      float* lse2p = (float*)work;
-      float* deltap = lse2p + B * H * Npad;
-      hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad, 256)), dim3(256), 0, st, (const bf16*)out,
-                         (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
-      hipLaunchKernelGGL(attn_bwd_dq_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
+    const long Npad = (N + AK - 1) / AK * AK;
+    float* lse2p = (float*)work;
+    float* deltap = lse2p + B * H * Npad;
+    hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad * 8, 256)), dim3(256), 0, st,
+                       (const bf16*)out, (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
+    hipLaunchKernelGGL(attn_bwd_dq_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p, deltap,
+                       (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    if (dkv_variant == 1)
+      hipLaunchKernelGGL(attn_bwd_dkv_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
                          deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    else
       hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
                          deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
-      IVIT_LAUNCH_CHECK();
-      return 0;
-    }
-    float* delta = (float*)work;
-    hipLaunchKernelGGL(attn_delta_kernel<bf16>, dim3(ivit_cdiv(B * N * H, 256)), dim3(256), 0, st,
-                       (const bf16*)out, (const bf16*)dout, B, (int)N, (int)H, delta);
-    hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse, delta,
-                       (int)N, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
-    hipLaunchKernelGGL(attn_bwd_dkv_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse,
-                       delta, (int)N, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
     IVIT_LAUNCH_CHECK();
     return 0;
   }

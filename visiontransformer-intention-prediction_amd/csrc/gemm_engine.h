@@ -11,6 +11,8 @@
 // bf16 path: 128x128x64 tile, 4 waves (2x2) x 64x64, v_mfma_f32_32x32x16_bf16.
 // f32  path: 128x128x16 tile, 4 waves (2x2) x 64x64, v_mfma_f32_32x32x2_f32 (exact f32).
 #pragma once
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "ivit_common.h"
@@ -49,17 +51,21 @@ struct LdDense {
   // a k-invariant 32-bit element offset plus a uniform per-K-tile advance. Rows / columns
   // past the matrix edge are clamped to the last valid one — they only feed output rows or
   // columns that the epilogue never stores; the K edge goes through the generic path.
-  static constexpr bool kLinear = true;
-  IVIT_DEV bool lin_ok(bool kc) const {
+  static constexpr bool kFast = true, kMayZero = false;
+  using Pre = int;
+  IVIT_DEV bool fast_ok(bool kc) const {
     return R > 0 && C >= 8 && (kc || rpb == 0) && (row_addr(R - 1) + 65) * ld + C < 0x7fffffffL;
   }
-  IVIT_DEV int lin_off(bool kc, int piece, int lane, int o0) const {
+  IVIT_DEV Pre pre(bool kc, int piece, int lane, int o0) const {
     if (kc) {  // image rows = m/n (8 per piece), chunks along k
       const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128_(row);
       return (int)(row_addr(min(o0 + row, R - 1)) * ld) + c * 8;
     }
     const int row = piece * 4 + (lane >> 4), c = (lane & 15) ^ ((row & 3) << 2);  // rows = k
     return (int)(row * ld) + min(o0 + c * 8, C - 8);
+  }
+  IVIT_DEV const void* fast_src(const Pre& o, bool kc, int k0) const {
+    return p + (kc ? (long)k0 : (long)k0 * ld) + o;
   }
   IVIT_DEV static int swz128_(int r) { return (((r >> 1) & 1) << 2) | (((r >> 3) & 1) << 1) | ((r >> 2) & 1); }
   IVIT_DEV const void* src8(int, int r, int c) const {
@@ -90,7 +96,7 @@ struct LdDense {
 // r = m = b*Np + gy*Wp + gx ; c = kk = (ch*P + ky)*P + kx  (chunk of 8 = one kx row).
 template <typename S>
 struct LdPatch {
-  static constexpr bool kLinear = false;
+  static constexpr bool kFast = false;
   static constexpr bool kRowFast = true;  // consecutive patches are consecutive 32-B runs
   static constexpr bool kGlds = false;    // f32 image converted to bf16 on the way: register staging
   IVIT_DEV LdPatch bind(int) const { return *this; }
@@ -122,11 +128,32 @@ struct LdPatch {
 // flip = true reads the spatially flipped tap (dgrad of the transposed conv).
 template <typename S>
 struct LdConv {
-  static constexpr bool kLinear = false;
   static constexpr bool kRowFast = false;
   static constexpr bool kGlds = sizeof(S) == 2;
   const S* x; int H, W, Cin, ks; int R, C; long ldc;  // ldc = channel stride of a pixel
   IVIT_DEV LdConv bind(int) const { return *this; }
+  // LDS-DMA fast path (K-contiguous image, Cin % 64 == 0, so a 64-wide K tile sits in one
+  // tap): the pixel of each lane's row is decomposed once; per tile only the tap's (dy, dx)
+  // bounds test and one add remain.
+  static constexpr bool kFast = true, kMayZero = true;  // padding taps read the zero page
+  struct Pre { int base; int yx; };
+  IVIT_DEV bool fast_ok(bool kc) const {
+    return kc && Cin % 64 == 0 && R > 0 && (long)R * ldc + C < 0x7fffffffL;
+  }
+  IVIT_DEV Pre pre(bool kc, int piece, int lane, int o0) const {
+    const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ LdDense<S>::swz128_(row);
+    const int r = min(o0 + row, R - 1);
+    const int xw = r % W, y = (r / W) % H;
+    return {(int)(r * ldc) + c * 8, (y << 16) | xw};
+  }
+  IVIT_DEV const void* fast_src(const Pre& o, bool, int k0) const {
+    const int tap = k0 / Cin, ci0 = k0 - tap * Cin;
+    const int ky = tap / ks, kx = tap - ky * ks, pad = ks >> 1;
+    const int dy = ky - pad, dx = kx - pad;
+    const int yy = (o.yx >> 16) + dy, xx = (o.yx & 0xffff) + dx;
+    if (yy < 0 || yy >= H || xx < 0 || xx >= W) return nullptr;
+    return x + o.base + (dy * W + dx) * ldc + ci0;
+  }
   IVIT_DEV const void* src8(int, int r, int c) const {
     long off;
     return at(r, c, off) ? (const void*)(x + off) : nullptr;
@@ -164,11 +191,26 @@ struct LdConv {
 // (the flipped tap), col c = ci  ->  W[co][ks-1-ky'][ks-1-kx'][ci].
 template <typename S>
 struct LdConvWFlip {
-  static constexpr bool kLinear = false;
   static constexpr bool kRowFast = false;
   static constexpr bool kGlds = sizeof(S) == 2;
   const S* w; int Cout, Cin, ks; int R, C;
   IVIT_DEV LdConvWFlip bind(int) const { return *this; }
+  // LDS-DMA fast path (MN-contiguous image, Cout % 64 == 0: a 64-row K tile is one tap):
+  // per lane a fixed (row, column) offset, per tile a uniform (co0, flipped tap) base.
+  static constexpr bool kFast = true, kMayZero = false;
+  using Pre = int;
+  IVIT_DEV bool fast_ok(bool kc) const {
+    return !kc && Cout % 64 == 0 && C >= 8 && (long)Cout * ks * ks * Cin < 0x7fffffffL;
+  }
+  IVIT_DEV Pre pre(bool, int piece, int lane, int o0) const {
+    const int row = piece * 4 + (lane >> 4), c = (lane & 15) ^ ((row & 3) << 2);
+    return row * ks * ks * Cin + min(o0 + c * 8, C - 8);
+  }
+  IVIT_DEV const void* fast_src(const Pre& o, bool, int k0) const {
+    const int tap = k0 / Cout, co0 = k0 - tap * Cout;
+    const int ky = tap / ks, kx = tap - ky * ks;
+    return w + ((co0 * ks + (ks - 1 - ky)) * ks + (ks - 1 - kx)) * Cin + o;
+  }
   IVIT_DEV const void* src8(int, int r, int c) const {
     return (r >= R || c >= C) ? nullptr : (const void*)addr(r, c);
   }
@@ -583,15 +625,44 @@ IVIT_DEV void glds_piece(const L& ld, int z, bool kc, char* img, int piece, int 
                                    (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
 }
 
+// One operand's P pieces of a K tile for this wave: fast (precomputed per-lane state) or the
+// generic gather (bounds-checked per element chunk).
+template <int P, class L>
+IVIT_DEV void glds_operand(const L& ld, int z, bool kc, char* img, int wv, int lane, int o0, int k0, int kend,
+                           bool fast, const typename L::Pre (&pre)[P]) {
+  if (fast) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const void* src = ld.fast_src(pre[i], kc, k0);
+      if constexpr (L::kMayZero) src = src ? src : (const void*)g_zero16;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + (wv * P + i) * 1024), 16,
+                                       0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < P; ++i) glds_piece(ld, z, kc, img, wv * P + i, lane, o0, k0, kend);
+  }
+}
+
 template <class E, class = void>
 struct BiasOnes { static constexpr bool v = false; };
 template <class E>
 struct BiasOnes<E, std::void_t<decltype(E::kBiasOnes)>> { static constexpr bool v = E::kBiasOnes; };
 
-template <class LA, class LB, class EPI, bool A_KC, bool B_KC>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, EPI epi_, int M, int N, int K,
-                                                              int tilesM, int tilesN, int splits, int kchunk) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2][16384];  // [stage][A|B][image]
+// WM waves along M (tile BM = 64*WM rows) x 2 waves along N (BN = 128), each wave 64x64.
+// WM = 2: 128x128 tile, 4 waves, two workgroups per CU. WM = 4: 256x128 tile, 8 waves, one
+// workgroup per CU — half the B-tile traffic per flop and twice the work per K step for the
+// skinny M = 36 008 token GEMMs (K-contiguous A only: the A image keeps 128-B rows).
+template <class LA, class LB, class EPI, bool A_KC, bool B_KC, int WM>
+__global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void gemm_bf16_glds_kernel(LA la_, LB lb_, EPI epi_, int M,
+                                                                                   int N, int K, int tilesM,
+                                                                                   int tilesN, int splits,
+                                                                                   int kchunk) {
+  constexpr int BM = 64 * WM, NW = 2 * WM;
+  constexpr int PA = BM / 8 / NW, PB = 16 / NW;  // 1-KiB pieces per wave per K tile
+  constexpr int SA = BM * 128, STAGE = SA + 16384;
+  static_assert(WM == 2 || A_KC, "256-row tiles need a K-contiguous A image");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];  // [stage][A image | B image]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 1, wn = wv & 1;  // wave-uniform (SGPR)
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -600,61 +671,23 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, 
   const LA la = la_.bind(z);
   const LB lb = lb_.bind(z);
   const EPI epi = epi_.bind(z);
-  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int m0 = tm * BM, n0 = tn * GBN;
   const int kbeg = split * kchunk, kend = min(K, kbeg + kchunk);
   const int nk = (kend - kbeg + GBK16 - 1) / GBK16;
 
-  // Fast path for dense operands: k-invariant per-lane offsets, uniform per-tile advance
-  // (K-contiguous: +k0 elements; MN-contiguous: +k0 rows). Generic gather otherwise and
-  // for a partial last K tile.
-  int offA[4] = {0, 0, 0, 0}, offB[4] = {0, 0, 0, 0};
-  bool fastA = false, fastB = false;
-  if constexpr (LA::kLinear) {
-    fastA = la.lin_ok(A_KC);
+  // Fast path: per-lane source state computed once (k-invariant), a uniform per-tile advance
+  // (loader::fast_src). Generic gather when the loader declines and for a partial K tile.
+  typename LA::Pre preA[PA];
+  typename LB::Pre preB[PB];
+  const bool fastA = la.fast_ok(A_KC), fastB = lb.fast_ok(B_KC);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) offA[i] = la.lin_off(A_KC, wv * 4 + i, lane, m0);
-  }
-  if constexpr (LB::kLinear) {
-    fastB = lb.lin_ok(B_KC);
+  for (int i = 0; i < PA; ++i) preA[i] = la.pre(A_KC, wv * PA + i, lane, m0);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) offB[i] = lb.lin_off(B_KC, wv * 4 + i, lane, n0);
-  }
+  for (int i = 0; i < PB; ++i) preB[i] = lb.pre(B_KC, wv * PB + i, lane, n0);
   auto issue = [&](int stage, int k0) {
     const bool full = k0 + GBK16 <= kend;
-    char* ia = smem[stage][0];
-    char* ib = smem[stage][1];
-    if constexpr (LA::kLinear) {
-      if (fastA && full) {
-        const auto* base = la.p + (A_KC ? (long)k0 : (long)k0 * la.ld);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          __builtin_amdgcn_global_load_lds((const void*)(base + offA[i]),
-                                           (__attribute__((address_space(3))) void*)(ia + (wv * 4 + i) * 1024), 16,
-                                           0, 0);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) glds_piece(la, z, A_KC, ia, wv * 4 + i, lane, m0, k0, kend);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) glds_piece(la, z, A_KC, ia, wv * 4 + i, lane, m0, k0, kend);
-    }
-    if constexpr (LB::kLinear) {
-      if (fastB && full) {
-        const auto* base = lb.p + (B_KC ? (long)k0 : (long)k0 * lb.ld);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          __builtin_amdgcn_global_load_lds((const void*)(base + offB[i]),
-                                           (__attribute__((address_space(3))) void*)(ib + (wv * 4 + i) * 1024), 16,
-                                           0, 0);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) glds_piece(lb, z, B_KC, ib, wv * 4 + i, lane, n0, k0, kend);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) glds_piece(lb, z, B_KC, ib, wv * 4 + i, lane, n0, k0, kend);
-    }
+    glds_operand<PA>(la, z, A_KC, smem + stage * STAGE, wv, lane, m0, k0, kend, fastA && full, preA);
+    glds_operand<PB>(lb, z, B_KC, smem + stage * STAGE + SA, wv, lane, n0, k0, kend, fastB && full, preB);
   };
 
   f32x16 acc[2][2];
@@ -681,13 +714,15 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, 
     const int cur = kt & 1;
     if (kt + 1 < nk) {
       issue(cur ^ 1, kbeg + (kt + 1) * GBK16);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this tile's 8 pieces have landed
+      // this tile's PA + PB pieces have landed (the next tile's stay in flight)
+      if constexpr (PA + PB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __builtin_amdgcn_s_barrier();                         // ... for every wave's pieces
-    const char* ia = smem[cur][0];
-    const char* ib = smem[cur][1];
+    __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
+    const char* ia = smem + cur * STAGE;
+    const char* ib = ia + SA;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       bf16x8 fa[2], fb[2];
@@ -725,11 +760,19 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_glds_kernel(LA la_, LB lb_, 
       }
     }
   }
-  epilogue_tile((float*)&smem[0][0][0] + wv * (32 * EP_LD), acc, epi, z, split, m0 + wm * 64, n0 + wn * 64, M, N,
-                lane);
+  epilogue_tile((float*)smem + wv * (32 * EP_LD), acc, epi, z, split, m0 + wm * 64, n0 + wn * 64, M, N, lane);
 }
 
 // ----------------------------------------------------------------------------- launcher
+// IVIT_GEMM_WIDE=1 puts large-M K-contiguous bf16 GEMMs on 256x128 tiles. Off by default:
+// measured on MI355X it wins on square shapes (4096^3: 882 -> 960 TF/s) but loses 2-8 % on the
+// M = 36 008, K <= 1536 token GEMMs of this model (one workgroup per CU hides less of the
+// short-K prologue/epilogue than two).
+inline bool gemm_wide_tiles() {
+  const char* v = getenv("IVIT_GEMM_WIDE");
+  return v && v[0] == '1';
+}
+
 // dtype_bf16: which kernel. batch: number of z. splits: split-K factor (kchunk multiple
 // of the K tile). Grid: x = tiles (XCD-remapped), y = batch * splits.
 template <bool A_KC, bool B_KC, class LA, class LB, class EPI>
@@ -746,10 +789,18 @@ int launch_gemm(bool bf16_path, const LA& la, const LB& lb, const EPI& epi, int 
     if (epi.bslab && !(bf16_path && LA::kGlds && LB::kGlds)) return IVIT_ERR_UNSUPPORTED;
   }
   if (bf16_path) {
-    if constexpr (LA::kGlds && LB::kGlds)
-      hipLaunchKernelGGL((gemm_bf16_glds_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N,
-                         K, tilesM, tilesN, splits, kchunk);
-    else
+    if constexpr (LA::kGlds && LB::kGlds) {
+      if constexpr (A_KC && !BiasOnes<EPI>::v) {
+        if (gemm_wide_tiles() && M >= 4096 && splits == 1) {  // 256x128 tiles, 8 waves
+          const int tM = ivit_cdiv(M, 256);
+          hipLaunchKernelGGL((gemm_bf16_glds_kernel<LA, LB, EPI, A_KC, B_KC, 4>), dim3(tM * tilesN, batch), dim3(512),
+                             0, st, la, lb, epi, M, N, K, tM, tilesN, 1, kchunk);
+          return 0;
+        }
+      }
+      hipLaunchKernelGGL((gemm_bf16_glds_kernel<LA, LB, EPI, A_KC, B_KC, 2>), grid, dim3(256), 0, st, la, lb, epi, M,
+                         N, K, tilesM, tilesN, splits, kchunk);
+    } else
       hipLaunchKernelGGL((gemm_bf16_kernel<LA, LB, EPI, A_KC, B_KC>), grid, dim3(256), 0, st, la, lb, epi, M, N, K,
                          tilesM, tilesN, splits, kchunk);
   } else

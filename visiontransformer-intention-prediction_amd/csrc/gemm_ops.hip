@@ -98,11 +98,26 @@ extern "C" int ivit_colsum(const void* X, int x_dtype, long ld, long rpb, long r
   return 0;
 }
 
+// Split-K factor from a wave-quantisation cost model: with `slots` resident workgroups (two
+// 128x128 workgroups per CU), time ~ rounds(tiles*s / slots) * (ktiles/s + c0), c0 ~ 4 K-tiles
+// of per-workgroup prologue/epilogue. Measured on MI355X (tools/gemm_bench.py): one slightly
+// over-full round costs more than a shorter, fuller one (e.g. 576 vs 288 workgroups).
 static int splitk_choice(long tiles, long K, int bk) {
-  // aim for >= ~512 workgroups, each keeping >= 8 K-tiles of work
-  int s = 1;
-  while (tiles * s < 512 && K / ((long)bk * (s * 2)) >= 8) s *= 2;
-  return s;
+  static const long slots = [] {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) cus = 256;
+    return 2L * cus;
+  }();
+  const double kt = (double)((K + bk - 1) / bk);
+  int best = 1;
+  double best_cost = 1e30;
+  for (int s = 1; s <= 128; ++s) {
+    if (s > 1 && kt / s < 8.0) break;
+    const double rounds = (double)((tiles * s + slots - 1) / slots);
+    const double cost = rounds * (kt / s + 4.0);
+    if (cost < best_cost - 1e-9) { best_cost = cost; best = s; }
+  }
+  return best;
 }
 
 // ----------------------------------------------------------------------------- linear
