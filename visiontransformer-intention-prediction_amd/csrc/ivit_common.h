@@ -164,8 +164,10 @@ __global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict
                                                          float* out0, int C0, float* out1, int acc) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
   float s = 0.f;
-  if (c < C)
+  if (c < C) {
+#pragma unroll 4
     for (int b = ph; b < nb; b += 16) s += part[(long)b * pstride + c];
+  }
   __shared__ float red[16][64];
   red[ph][threadIdx.x & 63] = s;
   __syncthreads();

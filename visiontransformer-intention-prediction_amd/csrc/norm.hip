@@ -310,24 +310,47 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(int mode, const void* X
   }
 }
 
-__global__ void bn_mean_kernel(const float* __restrict__ part, int nb, long M, int C, float* mean) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Column sums of the per-block partials, 64 columns x 16 row phases per 1024-thread block
+// (the partial lists are hundreds of rows long: one thread per column left them latency-bound).
+IVIT_DEV float bn_colsum16(const float* __restrict__ part, int nb, long pstride, long off, int c, bool valid,
+                           float (*red)[64]) {
+  const int ph = threadIdx.x >> 6, lc = threadIdx.x & 63;
   float s = 0.f;
-  for (int k = 0; k < nb; ++k) s += part[(k * 2) * C + c];
-  mean[c] = s / (float)M;
+  if (valid) {
+#pragma unroll 4
+    for (int k = ph; k < nb; k += 16) s += part[(long)k * pstride + off + c];
+  }
+  red[ph][lc] = s;
+  __syncthreads();
+  float t = 0.f;
+  if (ph == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][lc];
+  }
+  __syncthreads();
+  return t;
 }
 
-__global__ void bn_var_kernel(const float* __restrict__ part, int nb, long M, int C, const float* mean, float* invstd,
-                              float* run_mean, float* run_var, float mom, float eps) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int k = 0; k < nb; ++k) s += part[(k * 2) * C + c];
-  const float var = s / (float)M;
-  invstd[c] = 1.0f / sqrtf(var + eps);
-  if (run_mean) run_mean[c] = (1.f - mom) * run_mean[c] + mom * mean[c];
-  if (run_var) run_var[c] = (1.f - mom) * run_var[c] + mom * (M > 1 ? s / (float)(M - 1) : var);
+__global__ __launch_bounds__(1024) void bn_mean_kernel(const float* __restrict__ part, int nb, long M, int C,
+                                                       float* mean) {
+  __shared__ float red[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s = bn_colsum16(part, nb, 2L * C, 0, c, c < C, red);
+  if (threadIdx.x < 64 && c < C) mean[c] = s / (float)M;
+}
+
+__global__ __launch_bounds__(1024) void bn_var_kernel(const float* __restrict__ part, int nb, long M, int C,
+                                                      const float* mean, float* invstd, float* run_mean,
+                                                      float* run_var, float mom, float eps) {
+  __shared__ float red[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s = bn_colsum16(part, nb, 2L * C, 0, c, c < C, red);
+  if (threadIdx.x < 64 && c < C) {
+    const float var = s / (float)M;
+    invstd[c] = 1.0f / sqrtf(var + eps);
+    if (run_mean) run_mean[c] = (1.f - mom) * run_mean[c] + mom * mean[c];
+    if (run_var) run_var[c] = (1.f - mom) * run_var[c] + mom * (M > 1 ? s / (float)(M - 1) : var);
+  }
 }
 
 __global__ void bn_apply_kernel(const void* X, int xdt, long M, int C, const float* __restrict__ mean,
@@ -358,16 +381,18 @@ __global__ void bn_bwd_apply_kernel(const void* X, int xdt, const void* Y, int y
   stv(dX, dxdt, i, is * g[c] * (dz - m1 - xh * m2));
 }
 
-__global__ void bn_bwd_final_kernel(const float* __restrict__ part, int nb, int C, float* sums, float* dg, float* db,
-                                    int acc) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f, t = 0.f;
-  for (int k = 0; k < nb; ++k) { s += part[(k * 2) * C + c]; t += part[(k * 2 + 1) * C + c]; }
-  sums[c] = s;
-  sums[C + c] = t;
-  if (db) db[c] = acc ? db[c] + s : s;
-  if (dg) dg[c] = acc ? dg[c] + t : t;
+__global__ __launch_bounds__(1024) void bn_bwd_final_kernel(const float* __restrict__ part, int nb, int C,
+                                                            float* sums, float* dg, float* db, int acc) {
+  __shared__ float red[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const float s = bn_colsum16(part, nb, 2L * C, 0, c, c < C, red);
+  const float t = bn_colsum16(part, nb, 2L * C, C, c, c < C, red);
+  if (threadIdx.x < 64 && c < C) {
+    sums[c] = s;
+    sums[C + c] = t;
+    if (db) db[c] = acc ? db[c] + s : s;
+    if (dg) dg[c] = acc ? dg[c] + t : t;
+  }
 }
 
 }  // namespace
@@ -455,10 +480,10 @@ extern "C" int ivit_bn_stats(const void* X, int x_dtype, long M, long C, float* 
   float* part = (float*)work;
   hipLaunchKernelGGL(bn_partial_kernel, g, dim3(256), 0, st, 0, X, x_dtype, nullptr, 0, nullptr, 0, M, (int)C,
                      nullptr, nullptr, 0, part);
-  hipLaunchKernelGGL(bn_mean_kernel, dim3(ivit_cdiv(C, 256)), dim3(256), 0, st, part, nb, M, (int)C, mean);
+  hipLaunchKernelGGL(bn_mean_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, M, (int)C, mean);
   hipLaunchKernelGGL(bn_partial_kernel, g, dim3(256), 0, st, 1, X, x_dtype, nullptr, 0, nullptr, 0, M, (int)C, mean,
                      nullptr, 0, part);
-  hipLaunchKernelGGL(bn_var_kernel, dim3(ivit_cdiv(C, 256)), dim3(256), 0, st, part, nb, M, (int)C, mean, invstd,
+  hipLaunchKernelGGL(bn_var_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, M, (int)C, mean, invstd,
                      run_mean, run_var, momentum, eps);
   IVIT_LAUNCH_CHECK();
   return 0;
@@ -484,7 +509,7 @@ extern "C" int ivit_bn_bwd(const void* X, int x_dtype, const void* Y, int y_dtyp
   float* sums = part + (long)nb * 2 * C;
   hipLaunchKernelGGL(bn_partial_kernel, dim3(ivit_cdiv(C, 64), nb), dim3(256), 0, st, 2, X, x_dtype, Y, y_dtype, dY,
                      dy_dtype, M, (int)C, mean, invstd, relu, part);
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ivit_cdiv(C, 256)), dim3(256), 0, st, part, nb, (int)C, sums, dg, db,
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, (int)C, sums, dg, db,
                      accumulate);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ivit_cdiv(M * C, 256)), dim3(256), 0, st, X, x_dtype, Y, y_dtype, dY,
                      dy_dtype, M, (int)C, mean, invstd, g, sums, relu, dX, dx_dtype, dR);

@@ -48,13 +48,14 @@ def init_distributed(backend: str | None = None):
 
 
 class _Bucket:
-    __slots__ = ("params", "flat", "ready", "work")
+    __slots__ = ("params", "flat", "ready", "work", "events")
 
     def __init__(self, params, flat):
         self.params = params
         self.flat = flat
         self.ready = 0
         self.work = None
+        self.events = []
 
 
 class GradBuckets:
@@ -125,8 +126,32 @@ class GradBuckets:
             raise RuntimeError("GradBuckets: a parameter's .grad was replaced outside the bucket "
                                "(use GradBuckets.zero_grad(), not optimizer.zero_grad(set_to_none=True))")
         b.ready += 1
-        if b.ready == len(b.params) and self.world > 1:
+        if self.world == 1:
+            return
+        if b.flat.is_cuda:
+            # the two ViT streams produce gradients on two HIP streams (model_vit.stream_tokens):
+            # the bucket's collective waits for each parameter's producer, not just the last one
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(b.flat.device))
+            b.events.append(ev)
+        if b.ready == len(b.params):
+            self._launch(b)
+
+    def _launch(self, b):
+        if b.flat.is_cuda:
+            comm = self._comm_stream(b.flat.device)
+            for ev in b.events:
+                comm.wait_event(ev)
+            b.events = []
+            with torch.cuda.stream(comm):
+                b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+        else:
             b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+
+    def _comm_stream(self, device):
+        if getattr(self, "_comm", None) is None:
+            self._comm = torch.cuda.Stream(device)
+        return self._comm
 
     def finish(self):
         """Launch any bucket that did not fill (unused parameters), wait, and average."""
@@ -136,12 +161,18 @@ class GradBuckets:
             return
         for b in self.buckets:
             if b.work is None:
-                b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+                if b.flat.is_cuda:  # unused parameters: everything queued so far is final
+                    b.events = [torch.cuda.current_stream(b.flat.device).record_event()]
+                self._launch(b)
         inv = 1.0 / self.world
         for b in self.buckets:
             b.work.wait()
             b.work = None
             b.ready = 0
+            b.events = []
+        if getattr(self, "_comm", None) is not None:
+            torch.cuda.current_stream(self._comm.device).wait_stream(self._comm)
+        for b in self.buckets:
             b.flat.mul_(inv)
 
     def remove(self):

@@ -125,8 +125,30 @@ class TwoStreamViTBackbone(nn.Module):
     def _cdt(self):
         return BF16 if getattr(self, "compute_dtype", torch.float32) == torch.bfloat16 else F32
 
+    concurrent_streams = True
+
     def stream_tokens(self, lidar_bev, map_bev):
-        return self.vit_lidar.forward_tokens(lidar_bev), self.vit_map.forward_tokens(map_bev)
+        """The LiDAR and map ViTs are independent until the fusion block: run them on two HIP
+        streams so their kernels fill each other's gaps (tile tails, barriers, prologues).
+        Autograd replays each backward op on its forward op's stream, so the two backward
+        passes overlap the same way; backward() syncs them back to the caller's stream."""
+        if not (self.concurrent_streams and lidar_bev.is_cuda):
+            return self.vit_lidar.forward_tokens(lidar_bev), self.vit_map.forward_tokens(map_bev)
+        main = torch.cuda.current_stream(lidar_bev.device)
+        s1, s2 = _side_streams(lidar_bev.device)
+        s1.wait_stream(main)
+        s2.wait_stream(main)
+        with torch.cuda.stream(s1):
+            tl = self.vit_lidar.forward_tokens(lidar_bev)
+        with torch.cuda.stream(s2):
+            tm = self.vit_map.forward_tokens(map_bev)
+        main.wait_stream(s1)
+        main.wait_stream(s2)
+        lidar_bev.record_stream(s1)
+        map_bev.record_stream(s2)
+        tl.record_stream(main)
+        tm.record_stream(main)
+        return tl, tm
 
     def forward(self, lidar_bev, map_bev):
         """model_vit.py:134-142 → fused feature map (B, C, Hf, Wf) f32."""
@@ -138,6 +160,17 @@ class TwoStreamViTBackbone(nn.Module):
         meta = (B, Hf, Wf, self._cdt(), self.training, 0, 0, self.fusion_layers, tuple(names))
         feat = ops.NeckFn.apply(tl, tm, meta, *tens)[0]
         return feat.reshape(B, Hf, Wf, -1).permute(0, 3, 1, 2)
+
+
+_SIDE_STREAMS = {}
+
+
+def _side_streams(device):
+    """Two persistent side streams per device for the LiDAR / map ViT streams."""
+    key = torch.device(device).index
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = (torch.cuda.Stream(device), torch.cuda.Stream(device))
+    return _SIDE_STREAMS[key]
 
 
 def _lookup(root, names):
