@@ -13,6 +13,8 @@ plus single-op Functions used by the standalone module forwards.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from _lib import ACT_GELU, ACT_NONE, BF16, F32, dt, lib, ptr, stream, tdtype, workspace
@@ -261,6 +263,45 @@ class PatchEmbedFn(torch.autograd.Function):
         return None, dw, db, dpos, dcls, None
 
 
+# Off by default: measured on MI355X with the two ViT streams already concurrent, the extra
+# fork costs 7 % (65.0 -> 69.5 ms/step, bench.py A/B in one call). IVIT_WGRAD_FORK=1 enables it.
+WGRAD_FORK = os.environ.get("IVIT_WGRAD_FORK", "0") == "1"
+_FORK_STREAMS = {}
+
+
+class _WgradFork:
+    """A side stream (one per calling stream) for weight-gradient GEMMs: each call waits for
+    the work queued so far on the calling stream, runs on the side stream, and join() makes the
+    calling stream wait for all of it. Tensors crossing streams are record_stream()-ed so the
+    caching allocator never hands their memory out early."""
+
+    def __init__(self, device):
+        self.cur = torch.cuda.current_stream(device)
+        key = (device.index, self.cur.cuda_stream)
+        if key not in _FORK_STREAMS:
+            _FORK_STREAMS[key] = torch.cuda.Stream(device)
+        self.side = _FORK_STREAMS[key]
+        self.outs = []
+
+    def run(self, fn, *args):
+        self.side.wait_stream(self.cur)
+        with torch.cuda.stream(self.side):
+            out = fn(*args)
+        self.outs += [t for t in out if t is not None]
+        return out
+
+    def join(self, inputs):
+        self.cur.wait_stream(self.side)
+        for t in inputs:
+            t.record_stream(self.side)
+        for t in self.outs:
+            t.record_stream(self.cur)
+
+
+def _wgrad(fork, dy, x, cdt):
+    return linear_wgrad(dy, x, cdt) if fork is None else fork.run(linear_wgrad, dy, x, cdt)
+
+
 class ViTBlockFn(torch.autograd.Function):
     """timm Block: x + dp1(proj(attn(norm1 x))); x + dp2(fc2(gelu(fc1(norm2 x)))).
     x: (B*N, D) f32 residual stream; GEMM operands in the compute dtype (f32 or bf16)."""
@@ -288,19 +329,25 @@ class ViTBlockFn(torch.autograd.Function):
         cd = tdtype(cdt)
         dx2 = dx2.contiguous()
         D = x.shape[1]
+        # The weight gradients are off the critical path: they run on a forked stream and
+        # overlap the dgrad chain (notably the attention backward); joined before returning.
+        fork = _WgradFork(dx2.device) if dx2.is_cuda and WGRAD_FORK else None
         dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
         dh = linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
-        dW2, db2 = linear_wgrad(dx2s, a, cdt)
+        g2 = _wgrad(fork, dx2s, a, cdt)
         dln2 = linear_dgrad(dh, w1, cdt, torch.float32)
-        dW1, db1 = linear_wgrad(dh, ln2, cdt)
+        g1 = _wgrad(fork, dh, ln2, cdt)
         dx1, dx1s, dg2, dbe2 = layernorm_bwd(x1, n2w, m2, r2, dln2, dres=dx2, dx=torch.empty_like(dx2), xs_dtype=cd,
                                              row_scale=s1, rps=N)
         do = linear_dgrad(dx1s, wp, cdt, cd)
-        dWp, dbp = linear_wgrad(dx1s, o, cdt)
+        gp = _wgrad(fork, dx1s, o, cdt)
         dqkv = attn_bwd(qkv, o, do, lse, B, N, H, cdt)
         dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
-        dWq, dbq = linear_wgrad(dqkv, ln1, cdt)
+        gq = _wgrad(fork, dqkv, ln1, cdt)
         dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
+        if fork is not None:
+            fork.join((dx2s, dh, dx1s, dqkv, a, ln2, o, ln1))
+        (dW2, db2), (dW1, db1), (dWp, dbp), (dWq, dbq) = g2, g1, gp, gq
         return dx0, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, None, None, None
 
 
