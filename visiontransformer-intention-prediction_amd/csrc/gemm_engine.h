@@ -661,8 +661,9 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void gemm_bf16_glds_kern
   constexpr int BM = 64 * WM, NW = 2 * WM;
   constexpr int PA = BM / 8 / NW, PB = 16 / NW;  // 1-KiB pieces per wave per K tile
   constexpr int SA = BM * 128, STAGE = SA + 16384;
+  constexpr int NS = WM == 2 ? 2 : 3;  // LDS stages: the 256-row tile keeps two K tiles in flight
   static_assert(WM == 2 || A_KC, "256-row tiles need a K-contiguous A image");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];  // [stage][A image | B image]
+  __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];  // [stage][A image | B image]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 1, wn = wv & 1;  // wave-uniform (SGPR)
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
@@ -710,15 +711,28 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void gemm_bf16_glds_kern
   }
 
   if (nk > 0) issue(0, kbeg);
+  if constexpr (NS == 3) {
+    if (nk > 1) issue(1, kbeg + GBK16);
+  }
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      issue(cur ^ 1, kbeg + (kt + 1) * GBK16);
-      // this tile's PA + PB pieces have landed (the next tile's stay in flight)
-      if constexpr (PA + PB == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cur = NS == 2 ? (kt & 1) : kt % 3;
+    if constexpr (NS == 2) {
+      if (kt + 1 < nk) {
+        issue(cur ^ 1, kbeg + (kt + 1) * GBK16);
+        // this tile's PA + PB pieces have landed (the next tile's stay in flight)
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {  // 6 pieces per tile per wave; tiles kt+1 and kt+2 stay in flight
+      if (kt + 2 < nk) {
+        issue((kt + 2) % 3, kbeg + (kt + 2) * GBK16);
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      } else if (kt + 1 < nk) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     __builtin_amdgcn_s_barrier();  // ... for every wave's pieces
     const char* ia = smem + cur * STAGE;

@@ -26,13 +26,17 @@ def pack_gt(gt_list, device):
     ok = [isinstance(g, dict) and "boxes_xywha" in g and "intentions" in g for g in gt_list]
     counts = [int(g["boxes_xywha"].shape[0]) if o else 0 for g, o in zip(gt_list, ok)]
     G = max(1, max(counts) if counts else 1)
-    gt = torch.zeros((B, G, 5), dtype=torch.float32)
-    gi = torch.zeros((B, G), dtype=torch.int32)
+    # pinned staging so the three copies are truly asynchronous (no host/GPU drain per step)
+    pin = torch.device(device).type == "cuda"
+    gt = torch.zeros((B, G, 5), dtype=torch.float32, pin_memory=pin)
+    gi = torch.zeros((B, G), dtype=torch.int32, pin_memory=pin)
     for b, (g, o, n) in enumerate(zip(gt_list, ok, counts)):
         if o and n:
             gt[b, :n] = g["boxes_xywha"].detach().float().cpu()
             gi[b, :n] = g["intentions"].detach().cpu().to(torch.int32)
     ng = torch.tensor(counts, dtype=torch.int32)
+    if pin:
+        ng = ng.pin_memory()
     return (gt.to(device, non_blocking=True), ng.to(device, non_blocking=True), gi.to(device, non_blocking=True))
 
 

@@ -19,7 +19,9 @@ class FusedAdamW(torch.optim.Optimizer):
         key = tuple(t.data_ptr() for t in tensors)
         tab = self._tables.get(key)
         if tab is None:
-            tab = torch.tensor(key, dtype=torch.int64).to(device)
+            # pinned staging + non_blocking: a pageable H2D copy would stall the host until the
+            # GPU drains (a bubble every step when gradient buffers move)
+            tab = torch.tensor(key, dtype=torch.int64).pin_memory().to(device, non_blocking=True)
             if len(self._tables) > 64:
                 self._tables.clear()
             self._tables[key] = tab
@@ -65,6 +67,6 @@ class FusedAdamW(torch.optim.Optimizer):
         key = ("sizes",) + tuple(p.numel() for p in ps)
         tab = self._tables.get(key)
         if tab is None:
-            tab = torch.tensor([p.numel() for p in ps], dtype=torch.int64).to(device)
+            tab = torch.tensor([p.numel() for p in ps], dtype=torch.int64).pin_memory().to(device, non_blocking=True)
             self._tables[key] = tab
         return tab
