@@ -38,11 +38,38 @@ def step_flops(B, H, W, depth=12, D=384, C_l=290, C_m=9, planes=512, A=5, K=8, a
     fusion = 2 * Np * planes * (9 * cin + 9 * planes + cin + 9 * planes + 9 * planes)
     heads = 2 * Np * 9 * planes * A * (7 + K)
     fwd = vit + patch + adapters + fusion + heads
-    return B * (3 * fwd - patch), B * (3 * vit)
+    return B * (3 * fwd - patch), B * (3 * vit), B * fwd
+
+
+ROOF_KERNEL = "attn_fwd_bf16_v4_kernel<4"  # the kernel ivit_attn_fwd launches by default (bf16)
 
 
 def attn_fwd_flops(B, N, H, Dh=64):
     return 4.0 * B * H * N * N * Dh
+
+
+def attn_fwd_bytes(B, N, H, Dh=64):
+    """Algorithmic HBM bytes of one attention-forward launch: qkv read once (bf16), out (bf16) + lse (f32) written."""
+    return B * N * 3 * H * Dh * 2 + B * N * H * Dh * 2 + B * H * N * 4
+
+
+def pmc_traffic(kernel_prefix):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary
+    (profiles/*_pmc_hbm.json, written by tools/pmc_summary.py from separate rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes of this same bench command, gfx950 corrections applied)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_hbm.json")))
+    if not files:
+        return None, None
+    try:
+        with open(files[-1]) as fh:
+            kern = json.load(fh)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    for name, v in kern.items():
+        if name.startswith(kernel_prefix) and v.get("hbm_bytes_avg") is not None:
+            return float(v["hbm_bytes_avg"]), os.path.relpath(files[-1], HERE)
+    return None, None
 
 
 def cpu_baseline(seconds_budget=25.0):
@@ -85,7 +112,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch (BASELINE config 2/3: 8)")
+    ap.add_argument("--mode", choices=["train", "eval"], default="train",
+                    help="train: configs 2/3/5 (fwd+loss+bwd+AdamW); eval: config 4 (inference + decode + NMS)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (configs 2/3/5: 8; config 4: 32)")
     ap.add_argument("--grid", type=str, default="400x720")
     ap.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -109,26 +138,38 @@ def main():
     from trainer import Trainer
 
     H, W = (int(v) for v in args.grid.split("x"))
-    B = args.batch
+    train = args.mode == "train"
+    B = args.batch if args.batch is not None else (8 if train else 32)
     cd = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
-    model = model_vit.IntentNetViT(backbone_cfg={"img_size": (H, W)}).to(dev).set_compute_dtype(cd).train()
-    net = model
-    if world > 1 and args.ddp == "torch":
-        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
-                                                        gradient_as_bucket_view=True, broadcast_buffers=False)
-    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
-    lf = L.DetectionIntentionLoss(use_rotated_iou=False, apply_intention_downsampling=True)
+    model = model_vit.IntentNetViT(backbone_cfg={"img_size": (H, W)}).to(dev).set_compute_dtype(cd)
+    model.train(train)
     anchors = utils.generate_anchors(H, W, 8, device=dev)
     # inputs resident in HBM before the timed region (SURVEY.md §8d primary placement)
     batch = synthetic_batch(B, (H, W), torch.Generator().manual_seed(1234 + rank), device=dev)
-    trainer = Trainer(net, lf, opt, anchors, world=world if args.ddp == "buckets" else 1,
-                      bucket_mb=args.bucket_mb, check_nan=False)
-    if trainer.buckets is None and world > 1 and args.ddp == "buckets":
-        raise RuntimeError("gradient buckets missing for world > 1")
+    if train:
+        net = model
+        if world > 1 and args.ddp == "torch":
+            net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], bucket_cap_mb=args.bucket_mb,
+                                                            gradient_as_bucket_view=True, broadcast_buffers=False)
+        opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+        lf = L.DetectionIntentionLoss(use_rotated_iou=False, apply_intention_downsampling=True)
+        trainer = Trainer(net, lf, opt, anchors, world=world if args.ddp == "buckets" else 1,
+                          bucket_mb=args.bucket_mb, check_nan=False)
+        if trainer.buckets is None and world > 1 and args.ddp == "buckets":
+            raise RuntimeError("gradient buckets missing for world > 1")
 
-    def step():
-        return trainer.step(batch)
+        def step():
+            return trainer.step(batch)
+    else:
+        kept = []
+
+        def step():  # eval_vit.py:144-180: forward, sigmoid >= 0.1, decode, NMS(0.2), argmax intention
+            with torch.inference_mode():
+                cls, box, it = model(batch["lidar_bev"], batch["map_bev"])
+                preds = utils.postprocess_batch(cls, box, it, anchors, 0.1, 0.2)
+            kept.append(sum(int(p["pred_scores"].numel()) for p in preds))
+            return {"loss": torch.zeros(())}
 
     for _ in range(args.warmup):
         step()
@@ -155,31 +196,48 @@ def main():
     gb = B * world
     value = gb * args.steps / el
     ms = el / args.steps * 1e3
-    fl_step, fl_vit = step_flops(B, H, W)
+    fl_step, fl_vit, fl_fwd = step_flops(B, H, W)
+    if not train:
+        fl_step = fl_fwd
     N = (H // 8) * (W // 8) + 1
     afl = attn_fwd_flops(B, N, 6)
     achieved = afl / (attn_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if cd == torch.bfloat16 else 157.3
+    # PMC traffic was collected on the default train configuration only
+    default_cfg = train and (H, W) == (400, 720) and B == 8 and cd == torch.bfloat16
+    traffic, traffic_src = pmc_traffic(ROOF_KERNEL) if default_cfg else (None, None)
+    if train:
+        workload = f"IntentNetViT train step (fwd+loss+bwd+AdamW), {args.dtype}, {H}x{W}, batch {B}/GPU"
+        metric = "BEV samples/sec (fwd+bwd) IntentNetViT at 1/2/4/8 MI355X; attn MFMA util %"
+    else:
+        workload = (f"IntentNetViT eval_vit.py inference (fwd + sigmoid/threshold 0.1 + decode + NMS 0.2 + argmax), "
+                    f"{args.dtype}, {H}x{W}, batch {B}/GPU")
+        metric = "BEV samples/sec inference (eval_vit.py path) IntentNetViT on MI355X"
     out = {
-        "metric": "BEV samples/sec (fwd+bwd) IntentNetViT at 1/2/4/8 MI355X; attn MFMA util %",
+        "metric": metric,
         "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.dtype, "data": "synthetic (random BEV rasters U[0,1)/Bernoulli(0.1), 20 random GT/sample; "
                                      "random-init weights)",
-        "config": {"workload": f"IntentNetViT train step (fwd+loss+bwd+AdamW), {args.dtype}, {H}x{W}, "
-                               f"batch {B}/GPU", "global_batch": gb, "per_gpu_batch": B, "grid": [H, W],
+        "config": {"workload": workload, "global_batch": gb, "per_gpu_batch": B, "grid": [H, W],
                    "tokens_per_stream": N, "parallelism": f"dp{world}"},
-        "roofline": {"kernel": "attn_fwd_bf16_v4_kernel<4> (ivit_attn_fwd)", "bound": "mfma",
+        "roofline": {"kernel": ROOF_KERNEL + "> (ivit_attn_fwd)", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": None,
+                     "frac": round(achieved / peak, 4), "traffic": traffic,
                      "per_launch": f"4*B*H*N^2*64 = {afl:.4g} flop (B={B}, H=6, N={N}); {attn_ms:.4f} ms avg over "
-                                   f"{len(ops.KernelTimer.records.get('attn_fwd', []))} launches (HIP events)"},
+                                   f"{len(ops.KernelTimer.records.get('attn_fwd', []))} launches (HIP events)",
+                     "traffic_note": (f"HBM bytes per launch from {traffic_src} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                                      f"gfx950-corrected); algorithmic bytes {attn_fwd_bytes(B, N, 6):.4g}")
+                     if traffic is not None else "no PMC summary for this configuration"},
         "step_mfma": {"achieved": round(fl_step * world / el * args.steps / 1e12 / world, 2), "unit": "TFLOP/s/GPU",
                       "frac": round(fl_step / (el / args.steps) / 1e12 / peak, 4),
                       "flops_per_step_per_gpu": fl_step},
-        "loss": loss_v,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if train:
+        out["loss"] = loss_v
+    else:
+        out["kept_boxes_per_step"] = kept[-1] if kept else 0
+    if rank == 0 and world == 1 and train and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -194,6 +194,34 @@ def test_full_grid_bf16_train_step_finite():
     assert not torch.equal(w0, m.det_head.conv.weight.detach())
 
 
+def test_large_grid_bf16_train_step_finite():
+    """BASELINE config 5 (2x BEV resolution, 800x1440: 100x180 patches, N = 18001 tokens,
+    90 000 anchors), B=1, bf16 train step: finite loss and gradients, anchors at the 2x grid."""
+    import loss as L
+    import utils
+    import model_vit
+    from optim import FusedAdamW
+    from synthetic import synthetic_batch
+    H, W = 800, 1440
+    torch.manual_seed(0)
+    m = model_vit.IntentNetViT(backbone_cfg={"img_size": (H, W)}).to(DEV).set_compute_dtype(torch.bfloat16).train()
+    batch = synthetic_batch(1, (H, W), torch.Generator().manual_seed(1234), device=DEV)
+    anchors = utils.generate_anchors(H, W, 8, device=DEV)
+    assert anchors.shape == (90000, 5)
+    ra = O.generate_anchors(H, W)
+    assert torch.equal(anchors.cpu(), ra)
+    opt = FusedAdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    c, b, i = m(batch["lidar_bev"], batch["map_bev"])
+    assert c.shape == (1, 90000, 1) and b.shape == (1, 90000, 6) and i.shape == (1, 90000, 8)
+    d = L.DetectionIntentionLoss()(c, b, i, anchors, batch["gt_list"])
+    d["loss"].backward()
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(d["loss"]).item() and d["num_pos_anchors"] > 0
+    for n, p in m.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all().item(), n
+
+
 def test_full_grid_fp32_forward_vs_oracle():
     cfg = model_cfg()
     lidar, mp, _ = O.synthetic_batch(1, seed=1234)

@@ -119,6 +119,30 @@ def test_attention(B, N, H, cd):
         assert _rel(d[:, i], g[:, i]) < (1e-4 if cdt == F32 else 3e-2), ("qkv"[i], _rel(d[:, i], g[:, i]))
 
 
+def test_attention_large_grid_bf16():
+    """BASELINE config 5 sequence length (800x1440 grid: N = 100*180 + 1 = 18001), bf16 flash
+    kernels vs an f32 torch reference on the device (scores materialised per head)."""
+    import ops
+    from _lib import BF16
+    B, N, H = 1, 18001, 2
+    q = (torch.randn(B * N, 3 * H * 64, device=DEV)).to(torch.bfloat16)
+    o, lse = ops.attn_fwd(q, B, N, H, BF16)
+    dod = torch.randn(B * N, H * 64, device=DEV).to(torch.bfloat16)
+    dq = ops.attn_bwd(q, o, dod, lse, B, N, H, BF16).float()
+    qr = q.float().requires_grad_(True)
+    qq, kk, vv = qr.reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (qq @ kk.transpose(-1, -2)) / 8.0
+    oref = (torch.softmax(s, -1) @ vv).transpose(1, 2).reshape(B * N, H * 64)
+    lref = torch.logsumexp(s, -1)
+    assert _rel(o.float(), oref.detach()) < 2e-2
+    assert _rel(lse, lref.detach()) < 1e-4
+    oref.backward(dod.float())
+    g = qr.grad.reshape(B * N, 3, H * 64)
+    d = dq.reshape(B * N, 3, H * 64)
+    for i in range(3):
+        assert _rel(d[:, i], g[:, i]) < 3e-2, ("qkv"[i], _rel(d[:, i], g[:, i]))
+
+
 @pytest.mark.parametrize("k", [1, 3])
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
 def test_conv_nhwc(k, cd):
