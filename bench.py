@@ -41,7 +41,7 @@ def step_flops(B, H, W, depth=12, D=384, C_l=290, C_m=9, planes=512, A=5, K=8, a
     return B * (3 * fwd - patch), B * (3 * vit), B * fwd
 
 
-ROOF_KERNEL = "attn_fwd_bf16_v4_kernel<4"  # the kernel ivit_attn_fwd launches by default (bf16)
+ROOF_KERNEL = "attn_fwd_bf16_v5_kernel<4"  # the kernel ivit_attn_fwd launches by default (bf16)
 
 
 def attn_fwd_flops(B, N, H, Dh=64):

@@ -108,7 +108,10 @@ def test_attention(B, N, H, cd):
     oref, lref = _attn_ref(qr, B, N, H)
     tol = 1e-5 if cdt == F32 else 2e-2
     assert _rel(o.float(), oref.detach()) < tol
-    assert _rel(lse, lref.detach()) < 1e-5
+    # bf16 path: the row sums l are accumulated on the MFMA pipe over the bf16-rounded
+    # probabilities (exactly the weights P.V uses), so lse = m + log l carries their rounding
+    # (~1e-4 relative at N <= 4501); the f32 path sums f32 probabilities.
+    assert _rel(lse, lref.detach()) < (1e-5 if cdt == F32 else 3e-4)
     do = torch.randn(B * N, H * 64)
     dod = ops.cast(do.to(DEV), cd)
     oref.backward(dod.float().cpu().double())

@@ -31,23 +31,27 @@ def rnd(*shape):
 
 
 rows = []
-for name, m, n, k, act in [("qkv", M, 1152, 384, ACT_NONE), ("fc1+gelu", M, 1536, 384, ACT_GELU),
-                           ("proj", M, 384, 384, ACT_NONE), ("fc2", M, 384, 1536, ACT_NONE),
-                           ("sq4096", 4096, 4096, 4096, ACT_NONE)]:
-    x, w = rnd(m, k), rnd(n, k)
-    b = torch.zeros(n, device="cuda")
-    fl = 2.0 * m * n * k
-    ms = timeit(lambda: ops.linear_fwd(x, w, b, BF16, act=act))
-    rows.append((f"fwd   {name}", m, n, k, ms, fl))
-    dy = rnd(m, n)
-    ms = timeit(lambda: ops.linear_dgrad(dy, w, BF16, torch.bfloat16))
-    rows.append((f"dgrad {name}", m, k, n, ms, fl))
-    ms = timeit(lambda: ops.linear_wgrad(dy, x, BF16, want_bias=True))
-    rows.append((f"wgrad {name}", n, k, m, ms, fl))
+VARIANTS = os.environ.get("GEMM_VARIANTS", "").split(",") if os.environ.get("GEMM_VARIANTS") else [None]
+for var in VARIANTS:
+  if var is not None:
+    os.environ["IVIT_GEMM_PERSIST"] = var
+  for name, m, n, k, act in [("qkv", M, 1152, 384, ACT_NONE), ("fc1+gelu", M, 1536, 384, ACT_GELU),
+                             ("proj", M, 384, 384, ACT_NONE), ("fc2", M, 384, 1536, ACT_NONE),
+                             ("sq4096", 4096, 4096, 4096, ACT_NONE)]:
+      x, w = rnd(m, k), rnd(n, k)
+      b = torch.zeros(n, device="cuda")
+      fl = 2.0 * m * n * k
+      ms = timeit(lambda: ops.linear_fwd(x, w, b, BF16, act=act))
+      rows.append((f"fwd   {name} p{var}", m, n, k, ms, fl))
+      dy = rnd(m, n)
+      ms = timeit(lambda: ops.linear_dgrad(dy, w, BF16, torch.bfloat16))
+      rows.append((f"dgrad {name} p{var}", m, k, n, ms, fl))
+      ms = timeit(lambda: ops.linear_wgrad(dy, x, BF16, want_bias=True))
+      rows.append((f"wgrad {name} p{var}", n, k, m, ms, fl))
 if len(sys.argv) > 1 and sys.argv[1] == "resid":
     x, w = rnd(M, 1536), rnd(384, 1536)
     r = torch.randn(M, 384, device="cuda")
     ms = timeit(lambda: ops.linear_fwd(x, w, torch.zeros(384, device="cuda"), BF16, resid=r))
     rows.append(("fwd   fc2+resid", M, 384, 1536, ms, 2.0 * M * 384 * 1536))
 for name, m, n, k, ms, fl in rows:
-    print(f"{name:16s} M={m:6d} N={n:5d} K={k:6d}  {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TF/s")
+    print(f"{name:22s} M={m:6d} N={n:5d} K={k:6d}  {ms * 1e3:8.1f} us  {fl / ms / 1e9:7.1f} TF/s")

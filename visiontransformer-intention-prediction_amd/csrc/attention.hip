@@ -568,6 +568,268 @@ __global__ __launch_bounds__(64 * W, MINB) void attn_fwd_bf16_v4_kernel(const bf
   }
 }
 
+// ------------------------------------------------------------------------- forward v5 (bf16)
+// Software-pipelined across key tiles, so the matrix pipe and the softmax VALU of ONE wave
+// overlap (at head dim 64 the softmax is as long as the two products of a tile):
+//   step j:  S_{j+1} = K_{j+1} Q^T  (8 MFMA)   ||  P_j = exp2(c2 S_j - m), cvt     (VALU)
+//            O^T += V_j^T P_j^T, l += 1^T P_j^T  (8 + 4 MFMA) ||  rowmax(S_{j+1})  (VALU)
+// One barrier per key tile: K runs two tiles ahead and V one (both double-buffered: K_j is dead
+// once S_j exists, V_j once P_j V_j is issued). Lazy rescale: the running max m only moves when
+// a tile's max exceeds it by more than TAU (log2 units), so P <= 2^TAU (exact in f32 / bf16
+// range) and the O rescale branch is rare; O / l and lse = m + log2 l are unchanged by it.
+constexpr float TAU = 8.0f;
+
+// One v_max3_f32 (fmaxf on MFMA outputs makes the compiler canonicalise each operand with an
+// extra v_max first: 3 instructions for what one does; scores are never NaN here).
+IVIT_DEV float vmax3(float a, float b, float c) {
+  float d;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+IVIT_DEV void qk_tile(const char* kimg, const bf16x8 (&qf)[4], f32x16 (&s)[2], int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    s[t] = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s[t], 0, 0, 0);
+    }
+  }
+}
+
+template <bool MASK>
+IVIT_DEV float tile_rowmax(f32x16 (&s)[2], int kbase, int N, int lane) {
+  const int hl = lane >> 5;
+  float a = NEG_BIG, b = NEG_BIG;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (MASK) {
+        const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (key >= N) s[t][r] = NEG_BIG;
+      }
+      if (r & 1) b = fmaxf(b, s[t][r]);  // two chains: v_max3-friendly and half the latency
+      else a = fmaxf(a, s[t][r]);
+    }
+  return half_swap_max(fmaxf(a, b));
+}
+
+// One steady-state step of the pipelined forward in a hand-fixed instruction order: every chunk
+// is closed by sched_barrier(0) and LDS operands are read two chunks ahead, so each MFMA gap
+// carries about the VALU the gap can hide (cdna_hip_programming.md: <= ~24 issue cycles):
+//   A : 8 x { K fragment read, 1 QK^T MFMA of S_{j+1}, exp + cvt of 2 scores of P_j (t = 0) }
+//   B1: 6 x { V reads, 1 P.V / row-sum MFMA (t = 0), exp + cvt of 2-3 scores of P_j (t = 1) }
+//   B2: 6 x { V reads, 1 P.V / row-sum MFMA (t = 1), ~6 values of rowmax(S_{j+1}) }
+// Returns the scaled row max of S_{j+1}.
+IVIT_DEV float fwd_step_fenced(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], const f32x16 (&cur)[2],
+                               f32x16 (&nxt)[2], f32x16& o0, f32x16& o1, f32x16& lacc, const bf16x8& ones, float m,
+                               float c2, int lane) {
+  const int hl = lane >> 5;
+  auto kfrag = [&](int i) {
+    return *(const bf16x8*)(kimg + t_off(32 * (i >> 2) + (lane & 31), 2 * (i & 3) + hl));
+  };
+  bf16x8 p[4];
+  auto ex = [&](int i) {  // score i of P_j: t = i >> 4, register i & 15
+    p[i >> 3][i & 7] = (bf16)fast_exp2(fmaf(cur[i >> 4][i & 15], c2, -m));
+  };
+  const f32x16 zero = zero16();
+  bf16x8 ka[8];
+  ka[0] = kfrag(0);
+  ka[1] = kfrag(1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i + 2 < 8) ka[i + 2] = kfrag(i + 2);
+    const int t = i >> 2, ks = i & 3;
+    nxt[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[i], qf[ks], ks == 0 ? zero : nxt[t], 0, 0, 0);
+    ex(2 * i);
+    ex(2 * i + 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // V^T operands: vf[2 * (2t + ss) + half]
+  bf16x8 vf[8];
+  auto vread = [&](int f) { vf[f] = tr_acc_order(vimg, 16 * (f >> 1), 32 * (f & 1), lane); };
+  vread(0);
+  vread(1);
+  __builtin_amdgcn_sched_barrier(0);
+  // B1: P(t=0) . V, exp of t = 1 (scores 16..31: 3,3,3,3,2,2 per chunk)
+  constexpr int e0[7] = {16, 19, 22, 25, 28, 30, 32};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int g = k / 3, which = k % 3;  // p[g]; which: o0 / o1 / row sum
+    if (k == 0) vread(2);
+    if (k == 1) vread(3);
+    if (k == 3) vread(4);
+    if (k == 4) vread(5);
+    if (which == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g], p[g], o0, 0, 0, 0);
+    else if (which == 1) o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g + 1], p[g], o1, 0, 0, 0);
+    else lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[g], lacc, 0, 0, 0);
+#pragma unroll
+    for (int i = e0[k]; i < e0[k + 1]; ++i) ex(i);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // B2: P(t=1) . V, rowmax of S_{j+1} (32 values, 6 per chunk)
+  float a = NEG_BIG, bm = NEG_BIG;
+#pragma unroll
+  for (int k = 6; k < 12; ++k) {
+    const int g = k / 3, which = k % 3;
+    if (k == 6) vread(6);
+    if (k == 7) vread(7);
+    if (which == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g], p[g], o0, 0, 0, 0);
+    else if (which == 1) o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g + 1], p[g], o1, 0, 0, 0);
+    else lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[g], lacc, 0, 0, 0);
+    const int v0 = 6 * (k - 6);
+#pragma unroll
+    for (int v = v0; v < v0 + 6 && v < 32; v += 2) {
+      if ((v >> 1) & 1) bm = vmax3(bm, nxt[v >> 4][v & 15], nxt[v >> 4][(v & 15) + 1]);
+      else a = vmax3(a, nxt[v >> 4][v & 15], nxt[v >> 4][(v & 15) + 1]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return half_swap_max(fmaxf(a, bm)) * c2;
+}
+
+// SCHED: the steady-state step (next tile full) runs fwd_step_fenced.
+template <int W, bool SCHED = false>
+__global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v5_kernel(const bf16* __restrict__ qkv, int N, int H,
+                                                                        bf16* __restrict__ out,
+                                                                        float* __restrict__ lse, float c2) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int q = blockIdx.x * (32 * W) + wv * 32 + (lane & 31);
+  bf16x8 qf[4];
+  load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  int off[8 / W];
+#pragma unroll
+  for (int i = 0; i < 8 / W; ++i) off[i] = dma_off<W>(i, wv, lane, ld);
+  auto issue1 = [&](const bf16* base, int kt, char* img) {  // one 64-key tile of K or V
+    if (kt < nfull) {
+      const bf16* src = base + (long)kt * AK * ld;
+#pragma unroll
+      for (int i = 0; i < 8 / W; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(src + off[i]),
+                                         (__attribute__((address_space(3))) void*)(img + (wv * (8 / W) + i) * 1024),
+                                         16, 0, 0);
+    } else {
+      tile_glds_w<W>(base, ld, kt * AK, N, img, wv, lane);
+    }
+  };
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+
+  // prologue: S_0 and its max; K_1 in flight
+  issue1(Kb, 0, smem[0][0]);
+  issue1(Vb, 0, smem[0][1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (nt > 1) issue1(Kb, 1, smem[1][0]);
+  f32x16 sc[2], sn[2];
+  qk_tile(smem[0][0], qf, sc, lane);
+  float m = (nfull > 0 ? tile_rowmax<false>(sc, 0, N, lane) : tile_rowmax<true>(sc, 0, N, lane)) * c2;
+  f32x16 o0 = zero16(), o1 = zero16(), lacc = zero16();
+
+  // NX = 1: the next tile exists and is full (branch-free body); NX = 3: generic (tail steps)
+  auto body = [&](auto stage, auto nxmode, int j, f32x16(&cur)[2], f32x16(&nxt)[2]) {
+    constexpr int S = decltype(stage)::value;  // V_j in smem[S][1], K_{j+1} in smem[S^1][0]
+    constexpr int NX = decltype(nxmode)::value;
+    const bool more = NX == 1 || j + 1 < nt;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // K_{j+1}, V_j landed for every wave; step j-1's reads are done
+    if (j + 2 < nt) issue1(Kb, j + 2, smem[S][0]);
+    if (more) issue1(Vb, j + 1, smem[S ^ 1][1]);
+    if constexpr (SCHED && NX == 1) {
+      const float mt = fwd_step_fenced(smem[S ^ 1][0], smem[S][1], qf, cur, nxt, o0, o1, lacc, ones, m, c2, lane);
+      const bool moved = mt > m + TAU;
+      if (__any(moved)) {
+        const float mn = moved ? mt : m;
+        const float alpha = fast_exp2(m - mn);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+        lacc[0] *= alpha;
+        m = mn;
+      }
+      return;
+    }
+    if (more) qk_tile(smem[S ^ 1][0], qf, nxt, lane);
+    bf16x8 p[4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)fast_exp2(fmaf(cur[t][8 * ss + e], c2, -m));
+        p[2 * t + ss] = v;
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int rb = 32 * t + 16 * ss;
+        const bf16x8 va0 = tr_acc_order(smem[S][1], rb, 0, lane);
+        const bf16x8 va1 = tr_acc_order(smem[S][1], rb, 32, lane);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, p[2 * t + ss], o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, p[2 * t + ss], o1, 0, 0, 0);
+        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[2 * t + ss], lacc, 0, 0, 0);
+      }
+    if (more) {
+      const float mt = (NX == 1 || j + 1 < nfull ? tile_rowmax<false>(nxt, (j + 1) * AK, N, lane)
+                                                 : tile_rowmax<true>(nxt, (j + 1) * AK, N, lane)) * c2;
+      const bool moved = mt > m + TAU;
+      if (__any(moved)) {
+        const float mn = moved ? mt : m;
+        const float alpha = fast_exp2(m - mn);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+        lacc[0] *= alpha;  // only element 0 is read back
+        m = mn;
+      }
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I3 = std::integral_constant<int, 3>;
+  int j = 0;
+  for (; j + 2 < nfull; j += 2) {  // steps j, j+1: both next tiles (j+1, j+2) are full
+    body(I0{}, I1{}, j, sc, sn);
+    body(I1{}, I1{}, j + 1, sn, sc);
+  }
+  for (; j < nt; ++j) {  // at most three tail steps, generic body (NX = 3: decided at run time)
+    if (j & 1) body(I1{}, I3{}, j, sn, sc);
+    else body(I0{}, I3{}, j, sc, sn);
+  }
+  if (q < N) {
+    const float l = lacc[0];
+    const float inv = 1.f / l;
+    bf16* orow = out + ((long)b * N + q) * D + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      Pack4 a, c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a.h[e] = (bf16)(o0[4 * g + e] * inv);
+        c.h[e] = (bf16)(o1[4 * g + e] * inv);
+      }
+      const int d = 8 * g + 4 * hl;
+      *(uint2*)(orow + d) = a.u;
+      *(uint2*)(orow + 32 + d) = c.u;
+    }
+    if (hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
+  }
+}
+
 // ------------------------------------------------------------------------- dK, dV (bf16)
 // (register-staged variant, IVIT_ATTN_DKV_VARIANT=1; rows from the padded lse2 / delta arrays)
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* __restrict__ qkv,
@@ -753,6 +1015,8 @@ IVIT_DEV void dq_tile(const char* kimg, const char* vimg, const bf16x8 (&qf)[4],
 
 // dQ: 4 waves x 32 queries; K/V tiles by LDS-DMA (k-invariant offsets, ragged tail guarded),
 // tile loop unrolled by two so the LDS stage is a compile-time constant.
+// V3ROWS: the row constants come from attn_rows_v3_kernel (lsn = -lse sqrt(Dh), dln = -delta).
+template <bool V3ROWS = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __restrict__ qkv,
                                                                 const bf16* __restrict__ dout,
                                                                 const float* __restrict__ lse2p,
@@ -773,8 +1037,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
   bf16x8 qf[4], gf[4];
   load_row_frags(Qb + (long)q * ld, qv, lane, qf);
   load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
-  const float lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
-  const float dlt = qv ? deltap[(long)z * Npad + q] : 0.f;
+  float lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
+  float dlt = qv ? deltap[(long)z * Npad + q] : 0.f;
+  if (V3ROWS) {
+    lse2 = qv ? -lse2 * c2 : 1e30f;  // -lsn * c2 = lse * log2(e)
+    dlt = -dlt;
+  }
   f32x16 a0 = zero16(), a1 = zero16();
   const int nt = (N + AK - 1) / AK, nfull = N / AK;
   int off[2];
@@ -958,6 +1226,179 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
   }
 }
 
+// ------------------------------------------------------------------------- backward v3 (bf16)
+// Row constants as the initial accumulators (cdna_hip_programming.md, attention backward):
+// lsn = -lse * sqrt(Dh), so S' = Q K^T + lsn and P = exp2(c2 S') with no subtraction, and
+// dln = -delta, so dS = P * (dO V^T + dln) is one multiply. Padding rows (n >= N, up to Npad):
+// lsn = -1e30 (P = 0 exactly), dln = 0.
+__global__ void attn_rows_v3_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                                    const float* __restrict__ lse, int B, int N, int Npad, int H, float rs,
+                                    float* __restrict__ lsn, float* __restrict__ dln) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long i = t >> 3;  // (z, padded row)
+  const int part = (int)(t & 7);
+  if (i >= (long)B * H * Npad) return;
+  const int z = (int)(i / Npad), n = (int)(i - (long)z * Npad);
+  float s = 0.f;
+  if (n < N) {
+    const int b = z / H, h = z - b * H, D = H * 64;
+    const long off = ((long)b * N + n) * D + h * 64 + part * 8;
+    Pack8 x, y;
+    x.u = *(const uint4*)(o + off);
+    y.u = *(const uint4*)(dout + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s = fmaf(bf2f(x.h[j]), bf2f(y.h[j]), s);
+  }
+  s += __shfl_xor(s, 1, 8);
+  s += __shfl_xor(s, 2, 8);
+  s += __shfl_xor(s, 4, 8);
+  if (part == 0) {
+    dln[i] = -s;
+    lsn[i] = n < N ? -lse[(long)z * N + n] * rs : -1e30f;
+  }
+}
+
+// dK / dV v3: 4 waves x 32 keys; the query sweep is software-pipelined by 32-query halves —
+// S', dP' of half u+1 (8 MFMA) are issued ahead of P, dS of half u (VALU) and its dV, dK
+// products (8 MFMA), so one wave's matrix and vector pipes overlap. Q / dO tiles and their row
+// constants arrive by LDS-DMA into a 3-stage ring: tile j+2 is issued at the top of step j
+// and waited for one full step later; one barrier per 64-query tile.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __restrict__ qkv,
+                                                                 const bf16* __restrict__ dout,
+                                                                 const float* __restrict__ lsnp,
+                                                                 const float* __restrict__ dlnp, int N, int Npad,
+                                                                 int H, bf16* __restrict__ dqkv, float c2,
+                                                                 float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[3][2][8192];  // [stage][Q|dO]
+  __shared__ __attribute__((aligned(16))) float srow[3][2][AK];    // [stage][lsn|dln]
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const bf16* Gb = dout + (long)b * N * D + h * 64;
+  const float* L = lsnp + (long)z * Npad;
+  const float* Dl = dlnp + (long)z * Npad;
+  const int key = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  bf16x8 kf[4], vf[4];
+  load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
+  load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
+  f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  int offq[2], offg[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    offq[i] = dma_off<4>(i, wv, lane, ld);
+    offg[i] = dma_off<4>(i, wv, lane, D);
+  }
+  auto issue = [&](int qt, int S) {
+    char* qimg = smem[S][0];
+    char* gimg = smem[S][1];
+    if (qt < nfull) {
+      const bf16* qb = Qb + (long)qt * AK * ld;
+      const bf16* gb = Gb + (long)qt * AK * D;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int piece = wv * 2 + i;
+        __builtin_amdgcn_global_load_lds((const void*)(qb + offq[i]),
+                                         (__attribute__((address_space(3))) void*)(qimg + piece * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(gb + offg[i]),
+                                         (__attribute__((address_space(3))) void*)(gimg + piece * 1024), 16, 0, 0);
+      }
+    } else {
+      tile_glds_w<4>(Qb, ld, qt * AK, N, qimg, wv, lane);
+      tile_glds_w<4>(Gb, D, qt * AK, N, gimg, wv, lane);
+    }
+    if (wv == 0) {  // 64 lsn + 64 dln floats (the padded arrays cover every tile row)
+      __builtin_amdgcn_global_load_lds((const void*)(L + qt * AK + lane),
+                                       (__attribute__((address_space(3))) void*)(&srow[S][0][0]), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(Dl + qt * AK + lane),
+                                       (__attribute__((address_space(3))) void*)(&srow[S][1][0]), 4, 0, 0);
+    }
+  };
+  // S' and dP' of query half t of the tile in stage S (rows = queries, lane = key)
+  auto sdp = [&](int S, int t, f32x16& s, f32x16& dp) {
+    const char* qimg = smem[S][0];
+    const char* gimg = smem[S][1];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // rows 8g + 4h .. +3 = registers 4g .. 4g+3
+      const float4 l4 = *(const float4*)(&srow[S][0][32 * t + 8 * g + 4 * hl]);
+      const float4 d4 = *(const float4*)(&srow[S][1][32 * t + 8 * g + 4 * hl]);
+      s[4 * g] = l4.x; s[4 * g + 1] = l4.y; s[4 * g + 2] = l4.z; s[4 * g + 3] = l4.w;
+      dp[4 * g] = d4.x; dp[4 * g + 1] = d4.y; dp[4 * g + 2] = d4.z; dp[4 * g + 3] = d4.w;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 qa = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      const bf16x8 ga = *(const bf16x8*)(gimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[ks], dp, 0, 0, 0);
+    }
+  };
+  // P, dS of half t (from S', dP' in cs, cdp) and its dV^T += dO^T P, dK^T += Q^T dS products
+  auto update = [&](int S, int t, const f32x16& cs, const f32x16& cdp) {
+    const char* qimg = smem[S][0];
+    const char* gimg = smem[S][1];
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      bf16x8 pa, da;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float p = fast_exp2(cs[8 * ss + e] * c2);
+        pa[e] = (bf16)p;
+        da[e] = (bf16)(p * cdp[8 * ss + e]);
+      }
+      const int rb = 32 * t + 16 * ss;
+      const bf16x8 g0 = tr_acc_order(gimg, rb, 0, lane);
+      const bf16x8 g1 = tr_acc_order(gimg, rb, 32, lane);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, g0, dv0, 0, 0, 0);
+      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, g1, dv1, 0, 0, 0);
+      const bf16x8 q0 = tr_acc_order(qimg, rb, 0, lane);
+      const bf16x8 q1 = tr_acc_order(qimg, rb, 32, lane);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, q0, dk0, 0, 0, 0);
+      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, q1, dk1, 0, 0, 0);
+    }
+  };
+  f32x16 sA, dpA, sB, dpB;
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  sdp(0, 0, sA, dpA);
+  auto step = [&](auto stage, int j) {
+    constexpr int S = decltype(stage)::value;
+    if (j > 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // tile j+1 landed for every wave; step j-1's reads are done
+    }
+    if (j + 2 < nt) issue(j + 2, (S + 2) % 3);
+    sdp(S, 1, sB, dpB);   // half (j, 1) ahead of ...
+    update(S, 0, sA, dpA);  // ... half (j, 0)
+    if (j + 1 < nt) sdp((S + 1) % 3, 0, sA, dpA);  // half (j+1, 0) ahead of ...
+    update(S, 1, sB, dpB);                           // ... half (j, 1)
+  };
+  for (int j = 0; j < nt; j += 3) {
+    step(std::integral_constant<int, 0>{}, j);
+    if (j + 1 < nt) step(std::integral_constant<int, 1>{}, j + 1);
+    if (j + 2 < nt) step(std::integral_constant<int, 2>{}, j + 2);
+  }
+  const int kw = blockIdx.x * AQ + wv * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    if (kk < N) {
+      bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
+      row[D + (lane & 31)] = (bf16)(dk0[r] * scale);
+      row[D + 32 + (lane & 31)] = (bf16)(dk1[r] * scale);
+      row[2 * D + (lane & 31)] = (bf16)dv0[r];
+      row[2 * D + 32 + (lane & 31)] = (bf16)dv1[r];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- f32 row kernels
 // S rows (already scaled) -> P = softmax, zero padding columns; lse = max + log(sum).
 __global__ void softmax_rows_kernel(float* __restrict__ S, long ldS, int N, float* __restrict__ lse) {
@@ -1062,7 +1503,7 @@ extern "C" int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H,
   if (B * N * H == 0) return 0;
   if (dtype == IVIT_BF16) {
     const char* ev = getenv("IVIT_ATTN_FWD_VARIANT");
-    const int variant = ev ? atoi(ev) : 5;
+    const int variant = ev ? atoi(ev) : 10;
     if (variant == 1) {
       dim3 g(ivit_cdiv(N, AQ), B * H);
       hipLaunchKernelGGL(attn_fwd_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H, (bf16*)out,
@@ -1078,6 +1519,14 @@ extern "C" int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H,
     } else if (variant == 5) {
       dim3 g(ivit_cdiv(N, 128), B * H);
       hipLaunchKernelGGL(attn_fwd_bf16_v4_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
+    } else if (variant == 9) {  // software-pipelined (S_{j+1} || softmax_j), lazy rescale
+      dim3 g(ivit_cdiv(N, 128), B * H);
+      hipLaunchKernelGGL(attn_fwd_bf16_v5_kernel<4>, g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
+    } else if (variant == 10) {  // v5 with the interleave pinned by sched_group_barrier
+      dim3 g(ivit_cdiv(N, 128), B * H);
+      hipLaunchKernelGGL((attn_fwd_bf16_v5_kernel<4, true>), g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
                          (bf16*)out, lse, scale * LOG2E);
     } else if (variant == 8) {  // v4 with the row sums on the MFMA pipe
       dim3 g(ivit_cdiv(N, 128), B * H);
@@ -1132,8 +1581,14 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
     const long Npad = (N + AK - 1) / AK * AK;
     float* lse2p = (float*)work;
     float* deltap = lse2p + B * H * Npad;
-    hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad * 8, 256)), dim3(256), 0, st,
-                       (const bf16*)out, (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
+    const bool v3 = dkv_variant == 3;  // v3: row constants as initial accumulators, pipelined dK/dV
+    if (v3)
+      hipLaunchKernelGGL(attn_rows_v3_kernel, dim3(ivit_cdiv(B * H * Npad * 8, 256)), dim3(256), 0, st,
+                         (const bf16*)out, (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H,
+                         sqrtf((float)Dh), lse2p, deltap);
+    else
+      hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad * 8, 256)), dim3(256), 0, st,
+                         (const bf16*)out, (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
     // dQ and dK/dV are independent: optionally run dQ on a library-owned side stream so the two
     // latency-bound kernels overlap (the caller's stream waits for it before returning).
     hipStream_t sq = st;
@@ -1143,11 +1598,18 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
       hipStreamWaitEvent(side->stream, side->fork, 0);
       sq = side->stream;
     }
-    hipLaunchKernelGGL(attn_bwd_dq_v2_kernel, g, dim3(256), 0, sq, (const bf16*)qkv, (const bf16*)dout, lse2p, deltap,
-                       (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    if (v3)
+      hipLaunchKernelGGL(attn_bwd_dq_v2_kernel<true>, g, dim3(256), 0, sq, (const bf16*)qkv, (const bf16*)dout, lse2p,
+                         deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    else
+      hipLaunchKernelGGL(attn_bwd_dq_v2_kernel<false>, g, dim3(256), 0, sq, (const bf16*)qkv, (const bf16*)dout, lse2p,
+                         deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
     if (side) hipEventRecord(side->join, sq);
     if (dkv_variant == 1)
       hipLaunchKernelGGL(attn_bwd_dkv_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
+                         deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    else if (v3)
+      hipLaunchKernelGGL(attn_bwd_dkv_v3_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
                          deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
     else
       hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
