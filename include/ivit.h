@@ -52,6 +52,17 @@ long ivit_patch_embed_wgrad_workspace(long B, long C, long H, long W, long D);
 int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* img, long B, long C, long H, long W, long D,
                            float* dW, float* dbias, float* dpos, float* dcls, int accumulate, void* work,
                            long work_bytes, void* stream);
+/* bf16 throughput path of the same PatchEmbed: one coalesced pass over the f32 raster writes the
+ * bf16 patch matrix cols[b*Np + gy*Wp + gx][(c*8 + ky)*8 + kx] = img[b][c][8gy+ky][8gx+kx]
+ * (full 128-B rows per (patch, channel)); the forward and the weight gradient then stream it
+ * as dense GEMM operands by LDS-DMA instead of re-gathering the raster. Same outputs and
+ * workspace as ivit_patch_embed_fwd / _wgrad with dtype IVIT_BF16.                          */
+int ivit_patch_im2col(const float* img, long B, long C, long H, long W, void* cols, void* stream);
+int ivit_patch_embed_fwd_cols(const void* cols, long B, long C, long H, long W, const void* Wt, const float* bias,
+                              const float* pos, const float* cls, long D, float* out, void* stream);
+int ivit_patch_embed_wgrad_cols(const void* dtok, const void* cols, long B, long C, long H, long W, long D,
+                                float* dW, float* dbias, float* dpos, float* dcls, int accumulate, void* work,
+                                long work_bytes, void* stream);
 
 /* ---- k x k stride-1 "same" convolution on NHWC maps (BasicBlock conv3x3/conv1x1,
  *      model_vit.py:12-17; DetectionHead/IntentionHead conv, heads.py:16,37).

@@ -197,6 +197,18 @@ def test_patch_embed(cd):
         assert _rel(p.grad, r.grad) < tol
 
 
+def test_patch_im2col_bitexact():
+    """bf16 patch matrix (the throughput path's GEMM operand) is exactly the rearranged, rounded raster."""
+    from _lib import lib, ptr, stream
+    B, C, H, W = 2, 290, 16, 24
+    img = torch.rand(B, C, H, W, device=DEV)
+    Np = (H // 8) * (W // 8)
+    cols = torch.empty((B * Np, C * 64), dtype=torch.bfloat16, device=DEV)
+    assert lib.ivit_patch_im2col(ptr(img), B, C, H, W, ptr(cols), stream()) == 0
+    ref = img.reshape(B, C, H // 8, 8, W // 8, 8).permute(0, 2, 4, 1, 3, 5).reshape(B * Np, C * 64)
+    assert torch.equal(cols.cpu(), ref.to(torch.bfloat16).cpu())
+
+
 def test_batchnorm_train():
     import ops
     M, C = 1000, 96

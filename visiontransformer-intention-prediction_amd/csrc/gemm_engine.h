@@ -667,7 +667,11 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void gemm_bf16_glds_kern
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 1, wn = wv & 1;  // wave-uniform (SGPR)
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int tm = lin / tilesN, tn = lin - tm * tilesN;
+  // Group the smaller tile dimension innermost: the workgroups an XCD runs together then share
+  // the panel of the larger operand through its L2 (tm-major when tilesM >= tilesN). For the
+  // LiDAR patch-embed weight gradient (3 x 145 tiles, B = 1.34 GB) tm-major re-read B 3 times.
+  const bool tmin = tilesN > tilesM;
+  const int tm = tmin ? lin % tilesM : lin / tilesN, tn = tmin ? lin / tilesM : lin - (lin / tilesN) * tilesN;
   const int z = blockIdx.y / splits, split = blockIdx.y - z * splits;
   const LA la = la_.bind(z);
   const LB lb = lb_.bind(z);

@@ -320,6 +320,80 @@ extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* 
                      stream);
 }
 
+// bf16 patch matrix. One workgroup per (b, c, gy) = 8 consecutive raster rows (8*W floats,
+// contiguous in NCHW); unit u = gx*8 + ky reads one 32-B run (kx = 0..7) and writes it as one
+// 16-B bf16 chunk, so 8 consecutive lanes fill the full 128-B row segment of patch (b, gy, gx),
+// channel c: coalesced reads, whole-line writes.
+__global__ __launch_bounds__(256) void patch_im2col_kernel(const float* __restrict__ img, int C, int H, int W,
+                                                           bf16* __restrict__ cols) {
+  const int Hp = H / 8, Wp = W / 8;
+  const long blk = blockIdx.x;  // (b * C + c) * Hp + gy
+  const int gy = (int)(blk % Hp);
+  const long bc = blk / Hp;
+  const int c = (int)(bc % C);
+  const long b = bc / C;
+  const float* src = img + (bc * H + (long)gy * 8) * W;
+  const long K = (long)C * 64;
+  bf16* dst = cols + (b * Hp * Wp + (long)gy * Wp) * K + c * 64;
+  for (int u = threadIdx.x; u < Wp * 8; u += 256) {
+    const int gx = u >> 3, ky = u & 7;
+    const float* p = src + (long)ky * W + gx * 8;
+    const float4 a = *(const float4*)p, q = *(const float4*)(p + 4);
+    *(uint4*)(dst + (long)gx * K + ky * 8) = f32x8_to_bf16x8(a, q);
+  }
+}
+
+extern "C" int ivit_patch_im2col(const float* img, long B, long C, long H, long W, void* cols, void* stream) {
+  IVIT_CHECK_ARG(H % 8 == 0 && W % 8 == 0, "ivit_patch_im2col: H, W must be multiples of the patch (8)");
+  if (B * C * H * W == 0) return 0;
+  hipStream_t st = ivit_stream(stream);
+  hipLaunchKernelGGL(patch_im2col_kernel, dim3((unsigned)(B * C * (H / 8))), dim3(256), 0, st, img, (int)C, (int)H,
+                     (int)W, (bf16*)cols);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_patch_embed_fwd_cols(const void* cols, long B, long C, long H, long W, const void* Wt,
+                                         const float* bias, const float* pos, const float* cls, long D, float* out,
+                                         void* stream) {
+  IVIT_CHECK_ARG(H % 8 == 0 && W % 8 == 0, "ivit_patch_embed_fwd_cols: H, W must be multiples of the patch (8)");
+  hipStream_t st = ivit_stream(stream);
+  const int Np = (int)((H / 8) * (W / 8));
+  const long K = C * 64;
+  LdDense<bf16> la{(const bf16*)cols, K, (int)(B * Np), (int)K, 0, 0, 0, {}};
+  LdDense<bf16> lb{(const bf16*)Wt, K, (int)D, (int)K, 0, 0, 0, {}};
+  EpiPatch e{out, Np, (int)D, bias, pos};
+  int rc = launch_gemm<true, true>(true, la, lb, e, (int)(B * Np), (int)D, (int)K, 1, 1, st);
+  if (rc) return rc;
+  const long Ntok = Np + 1;
+  hipLaunchKernelGGL(cls_rows_kernel, dim3(ivit_cdiv(B * D, 256)), dim3(256), 0, st, out, B, Ntok, D, cls, pos);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_patch_embed_wgrad_cols(const void* dtok, const void* cols, long B, long C, long H, long W, long D,
+                                           float* dW, float* dbias, float* dpos, float* dcls, int accumulate,
+                                           void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(work_bytes >= ivit_patch_embed_wgrad_workspace(B, C, H, W, D), "patch wgrad: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  const long Np = (H / 8) * (W / 8), Ntok = Np + 1, K = C * 64;
+  const int splits = (int)wgrad_splits(D, K, B * Np, true);
+  float* slab = (float*)work;
+  LdDense<bf16> la{(const bf16*)dtok, D, (int)(B * Np), (int)D, (int)Np, Ntok, 1, {}};  // A[d][m], token rows
+  LdDense<bf16> lb{(const bf16*)cols, K, (int)(B * Np), (int)K, 0, 0, 0, {}};          // B[m][k]
+  EpiSlab e{slab, D, K};
+  int rc = launch_gemm<false, false>(true, la, lb, e, (int)D, (int)K, (int)(B * Np), 1, splits, st);
+  if (rc) return rc;
+  const long n = D * K;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dW, accumulate);
+  hipLaunchKernelGGL(pos_grad_kernel<bf16>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const bf16*)dtok, B,
+                     Ntok, D, dpos, dcls, accumulate);
+  IVIT_LAUNCH_CHECK();
+  char* cw = (char*)work + (long)splits * n * 4;
+  return ivit_colsum(dtok, IVIT_BF16, D, Np, Ntok, 1, B * Np, D, dbias, accumulate, cw,
+                     ivit_colsum_workspace(B * Np, D), stream);
+}
+
 // ----------------------------------------------------------------------------- NHWC convolution
 template <typename S, typename O>
 static int conv_fwd_t(const void* X, long B, long H, long W, long Cin, const void* Wp, const float* bias, long Cout,

@@ -242,24 +242,38 @@ class PatchEmbedFn(torch.autograd.Function):
         Ntok = (H // 8) * (W // 8) + 1
         wc = cast(w.reshape(D, C * 64), tdtype(cdt))
         out = torch.empty((B * Ntok, D), dtype=torch.float32, device=img.device)
-        lib.ivit_patch_embed_fwd(cdt, ptr(img), B, C, H, W, ptr(wc), ptr(b), ptr(pos), ptr(cls), D, ptr(out), stream())
-        ctx.save_for_backward(img)
+        if cdt == BF16:
+            # bf16: one coalesced pass writes the bf16 patch matrix; forward and weight gradient
+            # stream it by LDS-DMA (saved for backward instead of the f32 raster)
+            cols = torch.empty((B * (Ntok - 1), C * 64), dtype=torch.bfloat16, device=img.device)
+            lib.ivit_patch_im2col(ptr(img), B, C, H, W, ptr(cols), stream())
+            lib.ivit_patch_embed_fwd_cols(ptr(cols), B, C, H, W, ptr(wc), ptr(b), ptr(pos), ptr(cls), D, ptr(out),
+                                          stream())
+            ctx.save_for_backward(cols)
+        else:
+            lib.ivit_patch_embed_fwd(cdt, ptr(img), B, C, H, W, ptr(wc), ptr(b), ptr(pos), ptr(cls), D, ptr(out),
+                                     stream())
+            ctx.save_for_backward(img)
         ctx.meta = (B, C, H, W, D, cdt, w.shape)
         return out
 
     @staticmethod
     def backward(ctx, dtok):
-        (img,) = ctx.saved_tensors
+        (src,) = ctx.saved_tensors
         B, C, H, W, D, cdt, wshape = ctx.meta
         dtok = cast(dtok.contiguous(), tdtype(cdt))
         Ntok = (H // 8) * (W // 8) + 1
-        dw = torch.empty(wshape, dtype=torch.float32, device=img.device)
-        db = torch.empty((D,), dtype=torch.float32, device=img.device)
-        dpos = torch.empty((1, Ntok, D), dtype=torch.float32, device=img.device)
-        dcls = torch.empty((1, 1, D), dtype=torch.float32, device=img.device)
-        ws = workspace(lib.ivit_patch_embed_wgrad_workspace(B, C, H, W, D), img.device)
-        lib.ivit_patch_embed_wgrad(cdt, ptr(dtok), ptr(img), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos), ptr(dcls), 0,
-                                   ptr(ws), ws.numel(), stream())
+        dw = torch.empty(wshape, dtype=torch.float32, device=src.device)
+        db = torch.empty((D,), dtype=torch.float32, device=src.device)
+        dpos = torch.empty((1, Ntok, D), dtype=torch.float32, device=src.device)
+        dcls = torch.empty((1, 1, D), dtype=torch.float32, device=src.device)
+        ws = workspace(lib.ivit_patch_embed_wgrad_workspace(B, C, H, W, D), src.device)
+        if cdt == BF16:
+            lib.ivit_patch_embed_wgrad_cols(ptr(dtok), ptr(src), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos),
+                                            ptr(dcls), 0, ptr(ws), ws.numel(), stream())
+        else:
+            lib.ivit_patch_embed_wgrad(cdt, ptr(dtok), ptr(src), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos),
+                                       ptr(dcls), 0, ptr(ws), ws.numel(), stream())
         return None, dw, db, dpos, dcls, None
 
 
