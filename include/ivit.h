@@ -138,6 +138,12 @@ int ivit_merge_heads_grad(const float* dcls, const float* dbox, const float* din
 int ivit_adamw(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
                void* const* exp_avg_sq, const long* sizes, long max_size, float lr, float beta1, float beta2,
                float eps, float weight_decay, float bc1, float bc2_sqrt, void* stream);
+/* Same update, and shadows[t] (bf16, may be null per tensor) receives bf16(p_new): the
+ * compute-dtype copies the next forward reads (replaces one cast launch per weight per step). */
+int ivit_adamw_shadow(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
+                      void* const* exp_avg_sq, void* const* shadows, const long* sizes, long max_size, float lr,
+                      float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2_sqrt,
+                      void* stream);
 
 /* ---- Detection / intention loss (loss.py:58-206): assignment + focal + Smooth-L1 + CE. ----- */
 /* gt: [B, Gmax, 5] f32 padded, ngt[B] int32, gint[B, Gmax] int32. keep: [B, NA] f32 0/1 (dominant

@@ -251,6 +251,28 @@ def test_adamw_matches_torch():
         assert _rel(q.detach(), p.detach()) < 1e-6
 
 
+def test_adamw_refreshes_bf16_weight_shadows():
+    """ops.cast_weight's cached bf16 copy is rewritten by the AdamW launch (ivit_adamw_shadow),
+    so after every step it equals bf16(p) exactly; a parameter without a shadow is unaffected."""
+    import ops
+    from optim import FusedAdamW
+    ps = [torch.randn(1152, 384, device=DEV, requires_grad=True), torch.randn(300, device=DEV, requires_grad=True)]
+    opt = FusedAdamW(ps, lr=1e-2, weight_decay=1e-2)
+    sh = ops.cast_weight(ps[0], torch.bfloat16)
+    assert ops.cast_weight(ps[0], torch.bfloat16) is sh
+    for _ in range(3):
+        for p in ps:
+            p.grad = torch.randn_like(p)
+        opt.step()
+        assert ops.shadow_of(ps[0]) is sh
+        assert torch.equal(sh, ps[0].detach().to(torch.bfloat16))
+    assert ops.shadow_of(ps[1]) is None
+    with torch.no_grad():
+        ps[0].mul_(0.5)  # an in-place change outside the optimizer invalidates the shadow
+    assert ops.shadow_of(ps[0]) is None
+    assert torch.equal(ops.cast_weight(ps[0], torch.bfloat16), ps[0].detach().to(torch.bfloat16))
+
+
 def test_geometry_golden():
     from conftest import golden
     import utils

@@ -72,15 +72,18 @@ __global__ void merge_heads_kernel(const float* dcls, const float* dbox, const f
 // torch _multi_tensor_adamw (foreach=True, amsgrad=False, maximize=False):
 //   p *= 1 - lr*wd ; m = lerp(m, g, 1-b1) ; v = v*b2 + (1-b2) g^2
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// shadows (optional): per tensor a bf16 copy of the updated parameter (nullptr: none) — the
+// compute-dtype weights the next forward reads, refreshed here instead of by per-step casts.
 __global__ void adamw_kernel(void* const* params, void* const* grads, void* const* ms, void* const* vs,
                              const long* sizes, float lr, float b1, float b2, float eps, float wd, float bc1,
-                             float bc2s) {
+                             float bc2s, void* const* shadows) {
   const int t = blockIdx.y;
   const long n = sizes[t];
   float* p = (float*)params[t];
   const float* g = (const float*)grads[t];
   float* m = (float*)ms[t];
   float* v = (float*)vs[t];
+  bf16* sh = shadows ? (bf16*)shadows[t] : nullptr;
   const float step = lr / bc1;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float gi = g[i];
@@ -93,6 +96,7 @@ __global__ void adamw_kernel(void* const* params, void* const* grads, void* cons
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
+    if (sh) sh[i] = (bf16)pi;
   }
 }
 
@@ -152,7 +156,22 @@ extern "C" int ivit_adamw(long n_tensors, void* const* params, void* const* grad
   int gx = ivit_cdiv(max_size, 256);
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
-                     exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt);
+                     exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, (void* const*)nullptr);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_adamw_shadow(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
+                                 void* const* exp_avg_sq, void* const* shadows, const long* sizes, long max_size,
+                                 float lr, float beta1, float beta2, float eps, float weight_decay, float bc1,
+                                 float bc2_sqrt, void* stream) {
+  if (n_tensors <= 0) return 0;
+  IVIT_CHECK_ARG(n_tensors < 65536, "ivit_adamw_shadow: too many tensors");
+  IVIT_CHECK_ARG(shadows != nullptr, "ivit_adamw_shadow: shadow table is null");
+  int gx = ivit_cdiv(max_size, 256);
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
+                     exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, shadows);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -24,7 +24,7 @@ class _LinearFn(torch.autograd.Function):
         shp = x.shape
         cd = torch.bfloat16 if cdt == BF16 else torch.float32
         x2 = ops.cast(x.reshape(-1, shp[-1]).contiguous(), cd)
-        wc = ops.cast(w, cd)
+        wc = ops.cast_weight(w, cd)
         y, _ = ops.linear_fwd(x2, wc, b, cdt, out_dtype=torch.float32)
         ctx.save_for_backward(x2, wc)
         ctx.cdt, ctx.shp = cdt, shp

@@ -14,8 +14,8 @@ plus single-op Functions used by the standalone module forwards.
 from __future__ import annotations
 
 import os
-
 import torch
+from torch.utils.weak import WeakIdKeyDictionary
 
 from _lib import ACT_GELU, ACT_NONE, BF16, F32, dt, lib, ptr, stream, tdtype, workspace
 
@@ -30,6 +30,32 @@ def cast(x, dtype):
     y = torch.empty(x.shape, dtype=dtype, device=x.device)
     lib.ivit_cast(ptr(x), dt(x), ptr(y), dt(y), x.numel(), stream())
     return y
+
+
+# Compute-dtype (bf16) copies of f32 parameters, kept across steps: FusedAdamW refreshes them in
+# its own launch (ivit_adamw_shadow) when it updates the parameter, so a training step casts no
+# weights. Any other in-place change of a parameter bumps its version counter and re-casts.
+_SHADOWS = WeakIdKeyDictionary()
+
+
+def cast_weight(w, dtype):
+    """cast(w, dtype) for a parameter, cached across steps (see _SHADOWS)."""
+    if w.dtype == dtype or not w.is_cuda or not w.is_contiguous():
+        return cast(w, dtype)
+    e = _SHADOWS.get(w)
+    if e is not None and e[0] == w._version and e[1].dtype == dtype and e[1].shape == w.shape:
+        return e[1]
+    y = cast(w, dtype)
+    _SHADOWS[w] = (w._version, y)
+    return y
+
+
+def shadow_of(p):
+    """The live bf16 shadow of parameter p (None if there is none or it is stale)."""
+    e = _SHADOWS.get(p)
+    if e is None or e[0] != p._version or e[1].dtype != torch.bfloat16 or e[1].shape != p.shape:
+        return None
+    return e[1]
 
 
 # ------------------------------------------------------------------------------ primitives
@@ -240,7 +266,7 @@ class PatchEmbedFn(torch.autograd.Function):
         B, C, H, W = img.shape
         D = w.shape[0]
         Ntok = (H // 8) * (W // 8) + 1
-        wc = cast(w.reshape(D, C * 64), tdtype(cdt))
+        wc = cast_weight(w, tdtype(cdt)).reshape(D, C * 64)
         out = torch.empty((B * Ntok, D), dtype=torch.float32, device=img.device)
         if cdt == BF16:
             # bf16: one coalesced pass writes the bf16 patch matrix; forward and weight gradient
@@ -324,7 +350,7 @@ class ViTBlockFn(torch.autograd.Function):
     def forward(ctx, x, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, s1, s2, meta):
         B, N, H, cdt, eps = meta
         cd = tdtype(cdt)
-        wq, wp, w1, w2 = cast(qkvw, cd), cast(pw, cd), cast(f1w, cd), cast(f2w, cd)
+        wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
         ln1, m1, r1 = layernorm_fwd(x, n1w, n1b, eps, cd)
         qkv, _ = linear_fwd(ln1, wq, qkvb, cdt)
         o, lse = attn_fwd(qkv, B, N, H, cdt)
@@ -391,7 +417,7 @@ class NeckFn(torch.autograd.Function):
             y, mf, rf = layernorm_fwd(t, P[f"vit_{s}.norm.weight"], P[f"vit_{s}.norm.bias"], 1e-6, torch.float32,
                                       rowmap=rm, M=M)
             z, ma, ra = layernorm_fwd(y, P[f"adapter_{s}.0.weight"], P[f"adapter_{s}.0.bias"], 1e-5, cd)
-            wa = cast(P[f"adapter_{s}.1.weight"], cd)
+            wa = cast_weight(P[f"adapter_{s}.1.weight"], cd)
             linear_fwd(z, wa, P[f"adapter_{s}.1.bias"], cdt, act=ACT_GELU, out=cat[:, c0:c0 + C],
                        pre=pre[:, c0:c0 + C])
             saved[s] = (t, y, mf, rf, z, ma, ra, wa)

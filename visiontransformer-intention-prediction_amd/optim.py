@@ -7,6 +7,7 @@ import math
 
 import torch
 
+import ops
 from _lib import lib, ptr, stream
 
 
@@ -59,9 +60,28 @@ class FusedAdamW(torch.optim.Optimizer):
                 sizes = self._table_sizes(ps, dev)
                 bc1 = 1.0 - b1 ** step
                 bc2s = math.sqrt(1.0 - b2 ** step)
-                lib.ivit_adamw(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(sizes), max(p.numel() for p in ps),
-                               group["lr"], b1, b2, group["eps"], group["weight_decay"], bc1, bc2s, stream())
+                # live bf16 compute copies (ops.cast_weight) are refreshed in the same launch
+                shadows = [ops.shadow_of(p) for p in ps]
+                if any(s is not None for s in shadows):
+                    tsh = self._table_ptrs([s.data_ptr() if s is not None else 0 for s in shadows], dev)
+                    lib.ivit_adamw_shadow(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(tsh), ptr(sizes),
+                                          max(p.numel() for p in ps), group["lr"], b1, b2, group["eps"],
+                                          group["weight_decay"], bc1, bc2s, stream())
+                else:
+                    lib.ivit_adamw(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(sizes),
+                                   max(p.numel() for p in ps), group["lr"], b1, b2, group["eps"],
+                                   group["weight_decay"], bc1, bc2s, stream())
         return loss
+
+    def _table_ptrs(self, ptrs, device):
+        key = ("ptrs",) + tuple(ptrs)
+        tab = self._tables.get(key)
+        if tab is None:
+            tab = torch.tensor(ptrs, dtype=torch.int64).pin_memory().to(device, non_blocking=True)
+            if len(self._tables) > 64:
+                self._tables.clear()
+            self._tables[key] = tab
+        return tab
 
     def _table_sizes(self, ps, device):
         key = ("sizes",) + tuple(p.numel() for p in ps)
