@@ -46,7 +46,7 @@ IVIT_DEV void tile_glds(const bf16* base, long ld, int r0, int nrows, char* img,
     const int row = piece * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz128(row);
     const void* src = (r0 + row < nrows) ? (const void*)(base + (long)(r0 + row) * ld + c * 8) : (const void*)g_zero16;
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
+    glds<16>(src, img + piece * 1024);
   }
 }
 IVIT_DEV void tile_sstore(char* img, int tid, const uint4 (&r)[2]) {
@@ -421,7 +421,7 @@ IVIT_DEV void tile_glds_w(const bf16* base, long ld, int r0, int nrows, char* im
     const int row = piece * 8 + (lane >> 3);
     const int c = (lane & 7) ^ swz128(row);
     const void* src = (r0 + row < nrows) ? (const void*)(base + (long)(r0 + row) * ld + c * 8) : (const void*)g_zero16;
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
+    glds<16>(src, img + piece * 1024);
   }
 }
 
@@ -521,10 +521,8 @@ __global__ __launch_bounds__(64 * W, MINB) void attn_fwd_bf16_v4_kernel(const bf
 #pragma unroll
       for (int i = 0; i < 8 / W; ++i) {
         const int piece = wv * (8 / W) + i;
-        __builtin_amdgcn_global_load_lds((const void*)(kb + off[i]),
-                                         (__attribute__((address_space(3))) void*)(kimg + piece * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(vb + off[i]),
-                                         (__attribute__((address_space(3))) void*)(vimg + piece * 1024), 16, 0, 0);
+        glds<16>((kb + off[i]), kimg + piece * 1024);
+        glds<16>((vb + off[i]), vimg + piece * 1024);
       }
     } else {
       tile_glds_w<W>(Kb, ld, kt * AK, N, kimg, wv, lane);
@@ -718,9 +716,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v5_kernel(const b
       const bf16* src = base + (long)kt * AK * ld;
 #pragma unroll
       for (int i = 0; i < 8 / W; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(src + off[i]),
-                                         (__attribute__((address_space(3))) void*)(img + (wv * (8 / W) + i) * 1024),
-                                         16, 0, 0);
+        glds<16>((src + off[i]), img + (wv * (8 / W) + i) * 1024);
     } else {
       tile_glds_w<W>(base, ld, kt * AK, N, img, wv, lane);
     }
@@ -1055,10 +1051,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int piece = wv * 2 + i;
-        __builtin_amdgcn_global_load_lds((const void*)(kb + off[i]),
-                                         (__attribute__((address_space(3))) void*)(kimg + piece * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(vb + off[i]),
-                                         (__attribute__((address_space(3))) void*)(vimg + piece * 1024), 16, 0, 0);
+        glds<16>((kb + off[i]), kimg + piece * 1024);
+        glds<16>((vb + off[i]), vimg + piece * 1024);
       }
     } else {
       tile_glds_w<4>(Kb, ld, kt * AK, N, kimg, wv, lane);
@@ -1182,20 +1176,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int piece = wv * 2 + i;
-        __builtin_amdgcn_global_load_lds((const void*)(qb + offq[i]),
-                                         (__attribute__((address_space(3))) void*)(qimg + piece * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(gb + offg[i]),
-                                         (__attribute__((address_space(3))) void*)(gimg + piece * 1024), 16, 0, 0);
+        glds<16>((qb + offq[i]), qimg + piece * 1024);
+        glds<16>((gb + offg[i]), gimg + piece * 1024);
       }
     } else {
       tile_glds_w<4>(Qb, ld, qt * AK, N, qimg, wv, lane);
       tile_glds_w<4>(Gb, D, qt * AK, N, gimg, wv, lane);
     }
     if (wv == 0) {  // 64 lse2 + 64 delta floats (the padded arrays cover every tile row)
-      __builtin_amdgcn_global_load_lds((const void*)(L + qt * AK + lane),
-                                       (__attribute__((address_space(3))) void*)(&srow[S][0][0]), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(Dl + qt * AK + lane),
-                                       (__attribute__((address_space(3))) void*)(&srow[S][1][0]), 4, 0, 0);
+      glds<4>((L + qt * AK + lane), &srow[S][0][0]);
+      glds<4>((Dl + qt * AK + lane), &srow[S][1][0]);
     }
   };
   auto step = [&](auto stage, int qt) {
@@ -1303,20 +1293,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __r
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int piece = wv * 2 + i;
-        __builtin_amdgcn_global_load_lds((const void*)(qb + offq[i]),
-                                         (__attribute__((address_space(3))) void*)(qimg + piece * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void*)(gb + offg[i]),
-                                         (__attribute__((address_space(3))) void*)(gimg + piece * 1024), 16, 0, 0);
+        glds<16>((qb + offq[i]), qimg + piece * 1024);
+        glds<16>((gb + offg[i]), gimg + piece * 1024);
       }
     } else {
       tile_glds_w<4>(Qb, ld, qt * AK, N, qimg, wv, lane);
       tile_glds_w<4>(Gb, D, qt * AK, N, gimg, wv, lane);
     }
     if (wv == 0) {  // 64 lsn + 64 dln floats (the padded arrays cover every tile row)
-      __builtin_amdgcn_global_load_lds((const void*)(L + qt * AK + lane),
-                                       (__attribute__((address_space(3))) void*)(&srow[S][0][0]), 4, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)(Dl + qt * AK + lane),
-                                       (__attribute__((address_space(3))) void*)(&srow[S][1][0]), 4, 0, 0);
+      glds<4>((L + qt * AK + lane), &srow[S][0][0]);
+      glds<4>((Dl + qt * AK + lane), &srow[S][1][0]);
     }
   };
   // S' and dP' of query half t of the tile in stage S (rows = queries, lane = key)

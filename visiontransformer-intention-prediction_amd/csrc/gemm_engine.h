@@ -621,8 +621,7 @@ IVIT_DEV void glds_piece(const L& ld, int z, bool kc, char* img, int piece, int 
     const int kk = k0 + row;
     src = kk < kend ? ld.src8(z, kk, o0 + c * 8) : nullptr;
   }
-  __builtin_amdgcn_global_load_lds(src ? src : (const void*)g_zero16,
-                                   (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
+  glds<16>(src ? src : (const void*)g_zero16, img + piece * 1024);
 }
 
 // One operand's P pieces of a K tile for this wave: fast (precomputed per-lane state) or the
@@ -635,8 +634,7 @@ IVIT_DEV void glds_operand(const L& ld, int z, bool kc, char* img, int wv, int l
     for (int i = 0; i < P; ++i) {
       const void* src = ld.fast_src(pre[i], kc, k0);
       if constexpr (L::kMayZero) src = src ? src : (const void*)g_zero16;
-      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + (wv * P + i) * 1024), 16,
-                                       0, 0);
+      glds<16>(src, img + (wv * P + i) * 1024);
     }
   } else {
 #pragma unroll

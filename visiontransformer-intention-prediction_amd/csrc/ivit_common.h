@@ -36,6 +36,25 @@ void ivit_set_error(const char* fmt, ...);
 static inline hipStream_t ivit_stream(void* s) { return (hipStream_t)s; }
 static inline int ivit_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// ---------------------------------------------------------------- LDS DMA
+// global_load_lds_dword{,x4}: each lane's BYTES land at lds + lane * BYTES (lds wave-uniform,
+// it goes to M0). Issued as inline asm, not __builtin_amdgcn_global_load_lds: with the builtin
+// the compiler's waitcnt pass assumes every later ds_read_b64_tr_b16 may alias an outstanding
+// DMA and puts s_waitcnt vmcnt(0) before it, which drains the NEXT tile's prefetch in every
+// K step of the MN-contiguous GEMMs and of the attention kernels. Every kernel here retires its
+// DMAs with explicit counted vmcnt waits + s_barrier, so the compiler needs no view of them.
+// M0 is written only here (tools/check_m0.py verifies the emitted code); s_nop 0 covers the
+// M0-write -> LDS-DMA hazard.
+template <int BYTES>
+IVIT_DEV void glds(const void* src, void* lds) {
+  static_assert(BYTES == 16 || BYTES == 4, "global_load_lds: 4 or 16 bytes per lane");
+  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  if constexpr (BYTES == 16)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(a) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(a) : "memory");
+}
+
 // ---------------------------------------------------------------- numerics
 IVIT_DEV float bf2f(bf16 x) { return (float)x; }
 IVIT_DEV bf16 f2bf(float x) { return (bf16)x; }
