@@ -44,3 +44,16 @@ for rnd in range(2):
         err = float((d.float() - dref).abs().max() / dref.abs().max())
         ms = timeit(lambda: ops.attn_bwd(qkv, o, dout, lse, B, N, H, BF16))
         print(f"bwd variant {bv} (rows+dq+dkv): {ms:.3f} ms  {2.5 * fl / ms / 1e9:.1f} TF/s algorithmic  rel diff vs first={err:.3g}")
+if os.environ.get("TORCH_SDPA", "1") == "1":  # vendor yardstick: torch SDPA (ROCm flash backend) on the same shape
+    import torch.nn.functional as F
+    q, k, v = (qkv.view(B, N, 3, H, 64)[:, :, i].transpose(1, 2).contiguous() for i in range(3))
+    g = dout.view(B, N, H, 64).transpose(1, 2).contiguous()
+    try:
+        ms = timeit(lambda: F.scaled_dot_product_attention(q, k, v))
+        print(f"torch sdpa fwd: {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+        qr, kr, vr = (t.clone().requires_grad_(True) for t in (q, k, v))
+        out = F.scaled_dot_product_attention(qr, kr, vr)
+        ms = timeit(lambda: torch.autograd.grad(out, (qr, kr, vr), g, retain_graph=True))
+        print(f"torch sdpa bwd: {ms:.3f} ms  {2.5 * fl / ms / 1e9:.1f} TF/s algorithmic")
+    except Exception as ex:  # noqa: BLE001
+        print("torch sdpa unavailable:", type(ex).__name__, str(ex)[:200])

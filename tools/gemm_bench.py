@@ -48,6 +48,14 @@ for var in VARIANTS:
       rows.append((f"dgrad {name} p{var}", m, k, n, ms, fl))
       ms = timeit(lambda: ops.linear_wgrad(dy, x, BF16, want_bias=True))
       rows.append((f"wgrad {name} p{var}", n, k, m, ms, fl))
+if "torch" in sys.argv[1:]:  # vendor-library yardstick (hipBLASLt via torch.mm), same shapes, no epilogue
+    for name, m, n, k in [("qkv", M, 1152, 384), ("fc1", M, 1536, 384), ("proj", M, 384, 384), ("fc2", M, 384, 1536),
+                          ("sq4096", 4096, 4096, 4096)]:
+        x, w, dy = rnd(m, k), rnd(n, k), rnd(m, n)
+        fl = 2.0 * m * n * k
+        rows.append((f"torch fwd   {name}", m, n, k, timeit(lambda: torch.mm(x, w.t())), fl))
+        rows.append((f"torch dgrad {name}", m, k, n, timeit(lambda: torch.mm(dy, w)), fl))
+        rows.append((f"torch wgrad {name}", n, k, m, timeit(lambda: torch.mm(dy.t(), x)), fl))
 if len(sys.argv) > 1 and sys.argv[1] == "resid":
     x, w = rnd(M, 1536), rnd(384, 1536)
     r = torch.randn(M, 384, device="cuda")
