@@ -12,6 +12,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -58,7 +59,9 @@ def pmc_traffic(kernel_prefix):
     (profiles/*_pmc_hbm.json, written by tools/pmc_summary.py from separate rocprofv3
     FETCH_SIZE / WRITE_SIZE passes of this same bench command, gfx950 corrections applied)."""
     import glob
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_hbm.json")))
+    # newest = highest round / version number (natural order: r01_v10 after r01_v9)
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_hbm.json")),
+                   key=lambda p: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(p))])
     if not files:
         return None, None
     try:
