@@ -173,6 +173,22 @@ long ivit_nms_workspace(long n);
 int ivit_nms(const float* boxes_xywha, const float* scores, long n, double iou_thr, long* keep, long* count,
              void* work, long work_bytes, void* stream);
 
+/* ---- LiDAR BEV voxelisation ----------------------------------------
+ * Replaces utils.create_intentnet_lidar_bev (utils.py:62-106) and, when sweep_tf is given, the
+ * per-sweep transform_points(pts, rel_tf) of dataset.py:319-340 (utils.py:27-33) in one pass.
+ * points: [P, ld] f32 (points_f64 = 0) or f64 rows, x y z in columns 0..2; intensity: [P] f32.
+ * Sweep s owns rows sweep_start[s] .. sweep_start[s+1]-1 (int64 prefix offsets, n_sweeps + 1);
+ * max_points >= the largest sweep. sweep_tf: [n_sweeps, 4, 4] f64 row-major or null (points
+ * already in the current ego frame). Sweep s scatters into planes sweep_plane[s] ..
+ * sweep_plane[s] + height_channels - 1 of bev ([planes, H, W] f32), which the caller zero-fills
+ * (np.zeros in the reference): bev[c, floor(off_y - x/voxel), floor(off_x + y/voxel)] =
+ * max(bev, intensity) for z in [z_min, z_max), c = clip(floor((z - z_min)/z_range * C)).
+ * z_range = z_max - z_min as the caller computes it (constants.py). f64 binning, bit-exact. */
+int ivit_lidar_bev(const void* points, int points_f64, long ld, const float* intensity, const long* sweep_start,
+                   long n_sweeps, long max_points, const double* sweep_tf, const int* sweep_plane, float* bev,
+                   long H, long W, long height_channels, double voxel, double off_x, double off_y, double z_min,
+                   double z_max, double z_range, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -410,3 +410,49 @@ def synthetic_batch(B, img_size=(400, 720), lidar_ch=290, map_ch=9, seed=1234, G
         ints = torch.randint(0, 8, (G,), generator=g)
         gts.append({"boxes_xywha": boxes.float(), "intentions": ints.long()})
     return lidar, mp, gts
+
+
+# --------------------------------------------------------------------------------------
+# LiDAR BEV voxelisation + sweep ego transform
+# --------------------------------------------------------------------------------------
+BEV_H, BEV_W, Z_MIN, Z_MAX, HEIGHT_CH, SWEEPS = 400, 720, -2.0, 3.8, 29, 10  # constants.py:28,40-43
+
+
+def sweep_rel_transform(ego_pose, sweep_pose):
+    """dataset.py:290-300 + :327-339: rel_tf = inv(world_SE3_ego) @ world_SE3_sweep, each SE3 from
+    (tx, ty, tz, qx, qy, qz, qw) (scipy Rotation.from_quat, scalar-last)."""
+    from scipy.spatial.transform import Rotation
+    def se3(p):
+        m = np.eye(4)
+        m[:3, :3] = Rotation.from_quat(list(p[3:7])).as_matrix()
+        m[:3, 3] = list(p[:3])
+        return m
+    return np.linalg.inv(se3(ego_pose)) @ se3(sweep_pose)
+
+
+def transform_points_np(points, tf):
+    """utils.py:27-33: (T @ [x y z 1]^T)^T[:, :3] in f64 (numpy matmul, as the reference)."""
+    if points.shape[0] == 0:
+        return np.empty((0, 3), dtype=points.dtype)
+    h = np.hstack((points[:, :3], np.ones((points.shape[0], 1))))
+    return (tf @ h.T).T[:, :3]
+
+
+def lidar_bev_np(points_list, intensity_list, num_sweeps=SWEEPS, H=BEV_H, W=BEV_W):
+    """utils.py:62-106: per sweep i, cells (floor(W/2 + y/0.2), floor(3H/4 - x/0.2)) inside the grid with
+    z in [Z_MIN, Z_MAX) take max(cell, intensity) in channel i*29 + clip(floor((z-Z_MIN)/(Z_MAX-Z_MIN)*29))."""
+    bev = np.zeros((HEIGHT_CH * num_sweeps, H, W), dtype=np.float32)
+    for i in range(min(len(points_list), len(intensity_list))):
+        p, v = points_list[i], intensity_list[i]
+        if p is None or v is None or p.shape[0] == 0:
+            continue
+        x, y, z = p[:, 0], p[:, 1], p[:, 2]
+        px = np.floor(W / 2.0 + y / VOXEL).astype(np.int64)          # utils.py:80
+        py = np.floor(H * 3.0 / 4.0 - x / VOXEL).astype(np.int64)    # utils.py:81
+        ok = (px >= 0) & (px < W) & (py >= 0) & (py < H) & (z >= Z_MIN) & (z < Z_MAX)
+        if not ok.any():
+            continue
+        hz = np.clip(np.floor((z[ok] - Z_MIN) / (Z_MAX - Z_MIN) * HEIGHT_CH).astype(np.int64), 0, HEIGHT_CH - 1)
+        flat = ((i * HEIGHT_CH + hz) * H + py[ok]) * W + px[ok]
+        np.maximum.at(bev.reshape(-1), flat, v[ok].astype(np.float32))  # utils.py:99-104 (order-free max)
+    return bev

@@ -188,6 +188,77 @@ def gen_geometry():
     print("geometry: loss", rec["loss_full"], "ds", rec["loss_full_ds"], "nms keeps", keeps)
 
 
+def _sparse(bev):
+    flat = bev.reshape(-1)
+    nz = np.flatnonzero(flat != 0)  # NaN != 0: NaN cells are kept
+    return nz.astype(np.int64), flat[nz]
+
+
+def gen_lidar_bev():
+    """utils.create_intentnet_lidar_bev / transform_points (utils.py:27-33, 62-106) on seeded sweeps.
+    Case A: the dataset path (dataset.py:290-347) -- 10 sweeps of sweep-frame f32 points, rel_tf from
+    poses (host restatement O.sweep_rel_transform), the reference's transform_points, then its
+    voxeliser; sweep 3 missing, sweep 5 empty, duplicate cells, zero / negative intensities.
+    Case B: f32 points handed in directly (f32 binning), 2 sweeps, exact grid / z boundaries, NaN."""
+    import utils as ref_utils
+    from scipy.spatial.transform import Rotation
+    rng = np.random.default_rng(21)
+    rec = {}
+    ego = np.array([100.0, -50.0, 1.2] + list(Rotation.from_euler("xyz", [0.01, -0.02, 0.3]).as_quat()))
+    pts_all, ints_all, counts, tfs, pts_ego, ints = [], [], [], [], [], []
+    for i in range(10):
+        if i == 3:
+            counts.append(-1)
+            pts_ego.append(None)
+            ints.append(None)
+            tfs.append(np.eye(4))
+            continue
+        n = 0 if i == 5 else 4000
+        p = np.stack([rng.uniform(-30, 90, n), rng.uniform(-80, 80, n), rng.uniform(-3.5, 5.5, n)], 1).astype(np.float32)
+        v = rng.uniform(0, 255, n).astype(np.float32)
+        if n:
+            v[rng.random(n) < 0.02] = 0.0
+            v[rng.random(n) < 0.01] *= -1.0
+            p[50:100] = p[:50]  # the same cells hit twice with different intensities
+        sw = ego.copy()
+        sw[:3] += rng.normal(0, 2.0, 3)
+        sw[3:] = Rotation.from_euler("xyz", [rng.normal(0, 0.01), rng.normal(0, 0.01),
+                                             0.3 + rng.normal(0, 0.05)]).as_quat()
+        tf = O.sweep_rel_transform(ego, sw)
+        counts.append(n)
+        pts_all.append(p)
+        ints_all.append(v)
+        tfs.append(tf)
+        pts_ego.append(ref_utils.transform_points(p, tf))
+        ints.append(v)
+    bev = ref_utils.create_intentnet_lidar_bev(pts_ego, ints)
+    mine = O.lidar_bev_np(pts_ego, ints)
+    assert np.array_equal(mine, bev), "oracle restatement != reference voxeliser"
+    rec.update(a_points=np.concatenate(pts_all), a_intensity=np.concatenate(ints_all), a_counts=np.array(counts),
+               a_tf=np.stack(tfs), a_ego_points_sample=np.concatenate([q for q in pts_ego if q is not None])[::97])
+    rec["a_idx"], rec["a_val"] = _sparse(bev)
+    rec["a_shape"] = np.array(bev.shape)
+    # case B: f32 points straight in, boundaries of the f32 binning
+    edge = np.array([[60.0, 0.0, 0.0], [-20.0, 0.0, 0.0], [0.0, 72.0, 0.0], [0.0, -72.0, 0.0],
+                     [0.0, 0.0, 3.8], [0.0, 0.0, -2.0], [0.0, 0.0, 3.7999], [10.0, 10.0, -1.0],
+                     [59.9, 71.9, 1.0], [-19.9, -71.9, 2.0], [0.1, 0.1, 0.0], [np.nan, 0.0, 0.0]], np.float32)
+    pb = [np.concatenate([edge, np.stack([rng.uniform(-25, 65, 3000), rng.uniform(-75, 75, 3000),
+                                          rng.uniform(-2.5, 4.3, 3000)], 1).astype(np.float32)]),
+          np.stack([rng.uniform(-25, 65, 2000), rng.uniform(-75, 75, 2000), rng.uniform(-2.5, 4.3, 2000)],
+                   1).astype(np.float32)]
+    vb = [rng.uniform(0, 100, pb[0].shape[0]).astype(np.float32), rng.uniform(0, 100, 2000).astype(np.float32)]
+    vb[1][7] = np.nan
+    pb[1][7] = pb[1][8]  # NaN shares its cell with a finite value
+    bev_b = ref_utils.create_intentnet_lidar_bev(pb, vb, num_expected_sweeps=2)
+    mine = O.lidar_bev_np(pb, vb, num_sweeps=2)
+    assert np.array_equal(mine, bev_b, equal_nan=True), "oracle restatement != reference voxeliser (case B)"
+    rec.update(b_points0=pb[0], b_points1=pb[1], b_int0=vb[0], b_int1=vb[1], b_shape=np.array(bev_b.shape))
+    rec["b_idx"], rec["b_val"] = _sparse(bev_b)
+    np.savez_compressed(os.path.join(OUT, "lidar_bev.npz"), **rec)
+    print("lidar_bev: case A nonzero", rec["a_idx"].size, "case B nonzero", rec["b_idx"].size,
+          "NaN cells", int(np.isnan(rec["b_val"]).sum()))
+
+
 def cross_check_vit():
     """HF ViTModel (stand-in) vs the oracle's timm restatement, 12 blocks, real widths."""
     cfg = model_cfg(img_size=SMALL_IMG)
@@ -211,6 +282,11 @@ if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     refshim.install()
     torch.set_num_threads(8)
+    if len(sys.argv) > 1:  # python -m oracle.make_golden lidar_bev ...: only the named fixtures
+        for name in sys.argv[1:]:
+            globals()["gen_" + name]()
+        sys.exit(0)
     cross_check_vit()
     gen_model_small()
     gen_geometry()
+    gen_lidar_bev()

@@ -1,6 +1,7 @@
-"""Box geometry of the reference's utils.py (anchors, axis/rotated IoU, decode, NMS, AP)
-on the MI355X kernels. BEV rasterisation, ego transforms and augmentations (utils.py:22-225,
-394-517) belong to the Argoverse-2 data pipeline, which is outside this build's scope."""
+"""Box geometry of the reference's utils.py (anchors, axis/rotated IoU, decode, NMS, AP) and
+the LiDAR BEV voxelisation with its sweep ego transform (utils.py:27-33, 62-106; SURVEY.md §8f
+rank 1) on the MI355X kernels. Map rasterisation and augmentations (utils.py:108-225, 394-517)
+belong to the Argoverse-2 data pipeline, which is outside this build's scope."""
 from __future__ import annotations
 
 import numpy as np
@@ -8,7 +9,7 @@ import torch
 
 from _lib import lib, ptr, stream, workspace
 from constants import (ANCHOR_CONFIGS_PAPER, BEV_PIXEL_OFFSET_X, BEV_PIXEL_OFFSET_Y, GRID_HEIGHT_PX, GRID_WIDTH_PX,
-                       VOXEL_SIZE_M)
+                       LIDAR_HEIGHT_CHANNELS, LIDAR_SWEEPS, VOXEL_SIZE_M, Z_MAX, Z_MIN)
 
 
 def _dev(device):
@@ -121,3 +122,95 @@ def calculate_ap(recall: np.ndarray, precision: np.ndarray) -> float:
     mpre = np.maximum.accumulate(mpre[::-1])[::-1]
     i = np.where(mrec[1:] != mrec[:-1])[0]
     return float(np.sum((mrec[i + 1] - mrec[i]) * mpre[i + 1]))
+
+
+# ------------------------------------------------------------------------ LiDAR BEV (§8f rank 1)
+def transform_points(points: np.ndarray, transform_matrix: np.ndarray) -> np.ndarray:
+    """utils.py:27-33 (host numpy, f64): (T @ [p, 1]^T)^T[:, :3]. The device path fuses the same
+    transform into the voxelisation kernel (create_intentnet_lidar_bev(..., transforms=...))."""
+    if points.shape[0] == 0:
+        return np.empty((0, 3), dtype=points.dtype)
+    homogeneous_points = np.hstack((points[:, :3], np.ones((points.shape[0], 1))))
+    return (transform_matrix @ homogeneous_points.T).T[:, :3]
+
+
+def _sweep_rows(points, intensity):
+    """One sweep's (points [n, ld] f32/f64 contiguous, intensity [n] f32) as numpy, or None."""
+    if points is None or intensity is None:
+        return None
+    p = points.detach().cpu().numpy() if isinstance(points, torch.Tensor) else np.asarray(points)
+    v = intensity.detach().cpu().numpy() if isinstance(intensity, torch.Tensor) else np.asarray(intensity)
+    if p.shape[0] == 0:
+        return None
+    if p.ndim != 2 or p.shape[1] < 3:
+        raise ValueError(f"LiDAR points must be [n, >=3] (got {tuple(p.shape)})")
+    if v.shape[0] < p.shape[0]:
+        raise ValueError(f"intensity has {v.shape[0]} values for {p.shape[0]} points")
+    return p, v[: p.shape[0]].astype(np.float32)
+
+
+def lidar_bev_batch(samples, num_expected_sweeps: int = LIDAR_SWEEPS, out: torch.Tensor | None = None,
+                    device=None) -> torch.Tensor:
+    """Voxelise a batch of samples into [B, C * num_expected_sweeps, H, W] f32 on the GPU, one launch.
+
+    samples[b] = (points_list, intensity_list) or (points_list, intensity_list, transforms) with
+    the semantics of create_intentnet_lidar_bev (utils.py:62-106): sweep i fills channels
+    i*29 .. i*29+28; sweeps that are None or empty leave their channels zero; the number of
+    sweeps used is min(len(points_list), len(intensity_list)). transforms[i] (4x4, or None for
+    the whole sample) is the sweep's rel_tf of dataset.py:336-340, applied in the kernel in f64
+    exactly as transform_points does. `out` (zero-filled here) may be the batch's lidar_bev slot.
+    """
+    dev = _dev(device if out is None else out.device)
+    B = len(samples)
+    C = LIDAR_HEIGHT_CHANNELS * num_expected_sweeps
+    if out is None:
+        out = torch.zeros((B, C, GRID_HEIGHT_PX, GRID_WIDTH_PX), dtype=torch.float32, device=dev)
+    else:
+        if tuple(out.shape) != (B, C, GRID_HEIGHT_PX, GRID_WIDTH_PX) or out.dtype != torch.float32 \
+                or not out.is_contiguous():
+            raise ValueError(f"out must be contiguous f32 {(B, C, GRID_HEIGHT_PX, GRID_WIDTH_PX)}")
+        out.zero_()
+    groups = {}  # point dtype -> sweeps; f32 and f64 sweeps bin in their own precision (bev.hip)
+    with_tf = any(len(s) > 2 and s[2] is not None for s in samples)
+    for b, smp in enumerate(samples):
+        points_list, intensity_list = smp[0], smp[1]
+        transforms = smp[2] if len(smp) > 2 else None
+        n_loaded = min(len(points_list), len(intensity_list))
+        if n_loaded > num_expected_sweeps:
+            # the reference indexes past its raster (IndexError); refuse instead of dropping sweeps
+            raise ValueError(f"sample {b}: {n_loaded} sweeps > num_expected_sweeps={num_expected_sweeps}")
+        for i in range(n_loaded):
+            rows = _sweep_rows(points_list[i], intensity_list[i])
+            if rows is None:
+                continue
+            p, v = rows
+            if p.dtype not in (np.float32, np.float64):
+                p = p.astype(np.float64)
+            t = None
+            if with_tf:
+                t = np.eye(4) if transforms is None or transforms[i] is None else np.asarray(transforms[i], np.float64)
+                if t.shape != (4, 4):
+                    raise ValueError(f"sample {b} sweep {i}: transform must be 4x4")
+            groups.setdefault(p.dtype == np.float64, []).append((p, v, t, b * C + i * LIDAR_HEIGHT_CHANNELS))
+    h2d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev, non_blocking=True)  # noqa: E731
+    for f64, sw in groups.items():
+        starts = np.cumsum([0] + [p.shape[0] for p, _, _, _ in sw]).astype(np.int64)
+        ld = max(p.shape[1] for p, _, _, _ in sw)
+        allp = np.zeros((int(starts[-1]), ld), dtype=np.float64 if f64 else np.float32)
+        for (p, _, _, _), a, e in zip(sw, starts[:-1], starts[1:]):
+            allp[a:e, : p.shape[1]] = p
+        dp, dv, dst = h2d(allp), h2d(np.concatenate([v for _, v, _, _ in sw])), h2d(starts)
+        dpl = h2d(np.asarray([pl for _, _, _, pl in sw], np.int32))
+        dtf = h2d(np.stack([t for _, _, t, _ in sw])) if with_tf else None
+        lib.ivit_lidar_bev(ptr(dp), int(f64), ld, ptr(dv), ptr(dst), len(sw), int(np.diff(starts).max()), ptr(dtf),
+                           ptr(dpl), ptr(out), GRID_HEIGHT_PX, GRID_WIDTH_PX, LIDAR_HEIGHT_CHANNELS, VOXEL_SIZE_M,
+                           BEV_PIXEL_OFFSET_X, BEV_PIXEL_OFFSET_Y, Z_MIN, Z_MAX, Z_MAX - Z_MIN, stream())
+    return out
+
+
+def create_intentnet_lidar_bev(points_list, intensity_list, num_expected_sweeps: int = LIDAR_SWEEPS,
+                               transforms=None, device=None) -> torch.Tensor:
+    """utils.py:62-106 on the GPU: (29 * num_expected_sweeps, 400, 720) f32 device tensor (the
+    reference returns the same raster as a numpy array). transforms (optional): per-sweep 4x4
+    rel_tf, fusing dataset.py:340's transform_points into the same kernel."""
+    return lidar_bev_batch([(points_list, intensity_list, transforms)], num_expected_sweeps, device=device)[0]
