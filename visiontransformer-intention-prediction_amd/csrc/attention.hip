@@ -492,6 +492,15 @@ IVIT_DEV int dma_off(int i, int wv, int lane, long ld) {
   return (int)(row * ld) + c * 8;
 }
 
+// Consume register-loaded fragments before a tile loop. Without a use ahead of the loop the
+// compiler places the s_waitcnt for these loads at their first use INSIDE the loop, where it
+// runs every iteration and (counting only its own loads) also drains the next tile's in-flight
+// LDS DMA (tools/loop_waits.py lists such waits).
+IVIT_DEV void retire_loads(bf16x8 (&a)[4], bf16x8 (&b)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(a[i]), "v"(b[i]));
+}
+
 template <int W, int MINB = 8 / W, bool MSUM = false>
 __global__ __launch_bounds__(64 * W, MINB) void attn_fwd_bf16_v4_kernel(const bf16* __restrict__ qkv, int N, int H,
                                                                         bf16* __restrict__ out,
@@ -1159,6 +1168,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
   bf16x8 kf[4], vf[4];
   load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
   load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
+  retire_loads(kf, vf);
   f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
   const int nt = (N + AK - 1) / AK, nfull = N / AK;
   int offq[2], offg[2];
@@ -1276,6 +1286,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __r
   bf16x8 kf[4], vf[4];
   load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
   load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
+  retire_loads(kf, vf);
   f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
   const int nt = (N + AK - 1) / AK, nfull = N / AK;
   int offq[2], offg[2];
