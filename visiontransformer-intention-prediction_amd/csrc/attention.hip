@@ -97,18 +97,30 @@ IVIT_DEV f32x16 zero16() {
 }
 
 // ------------------------------------------------------------------------- forward (bf16)
+// (query or key block, b*H + h) of this workgroup. Workgroups reach the 8 XCDs round-robin in
+// flat dispatch order (x fastest); remapping the flat id gives each XCD a contiguous run of
+// blocks, i.e. whole (b, h) pairs, so each pair's K/V (or Q/dO) panel is fetched into ONE L2
+// and shared by its ~36 blocks. With blockIdx.y = (b, h) directly, a pair's blocks spread
+// over all 8 XCDs and every attention launch read its operands ~5x from HBM (PMC FETCH_SIZE).
+IVIT_DEV int2 attn_block_id() {
+  const int nb = gridDim.x;
+  const int flat = xcd_remap(blockIdx.x + blockIdx.y * nb, nb * gridDim.y);
+  return make_int2(flat % nb, flat / nb);
+}
+
 __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_kernel(const bf16* __restrict__ qkv, int N, int H,
                                                                bf16* __restrict__ out, float* __restrict__ lse,
                                                                float c2) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
-  const int q = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  const int q = bid.x * AQ + wv * 32 + (lane & 31);
 
   bf16x8 qf[4];
   load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
@@ -281,13 +293,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16_v2_kernel(const bf16* __
                                                                   float c2) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
-  const int qw = blockIdx.x * AQ2 + wv * 64;
+  const int qw = bid.x * AQ2 + wv * 64;
   bf16x8 qf[2][4];
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
@@ -431,13 +444,14 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v3_kernel(const b
                                                                         float* __restrict__ lse, float c2) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
-  const int q = blockIdx.x * (32 * W) + wv * 32 + (lane & 31);
+  const int q = bid.x * (32 * W) + wv * 32 + (lane & 31);
   bf16x8 qf[4];
   load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
   f32x16 o0 = zero16(), o1 = zero16();
@@ -508,13 +522,14 @@ __global__ __launch_bounds__(64 * W, MINB) void attn_fwd_bf16_v4_kernel(const bf
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
-  const int q = blockIdx.x * (32 * W) + wv * 32 + (lane & 31);
+  const int q = bid.x * (32 * W) + wv * 32 + (lane & 31);
   bf16x8 qf[4];
   load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
   f32x16 o0 = zero16(), o1 = zero16(), lacc = zero16();
@@ -707,13 +722,14 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v5_kernel(const b
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
-  const int q = blockIdx.x * (32 * W) + wv * 32 + (lane & 31);
+  const int q = bid.x * (32 * W) + wv * 32 + (lane & 31);
   bf16x8 qf[4];
   load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
   const int nt = (N + AK - 1) / AK, nfull = N / AK;
@@ -846,7 +862,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* _
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][Q|dO]
   __shared__ float srow[2][2][AK];                                  // [stage][lse2|delta]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane >> 5;
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
@@ -855,7 +872,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* _
   const bf16* Gb = dout + (long)b * N * D + h * 64;
   const float* L = lse2p + (long)z * Npad;
   const float* Dl = deltap + (long)z * Npad;
-  const int key = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  const int key = bid.x * AQ + wv * 32 + (lane & 31);
   bf16x8 kf[4], vf[4];
   load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
   load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
@@ -933,7 +950,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* _
     }
     __syncthreads();
   }
-  const int kw = blockIdx.x * AQ + wv * 32;
+  const int kw = bid.x * AQ + wv * 32;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;
@@ -1031,13 +1048,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
-  const int q = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  const int q = bid.x * AQ + wv * 32 + (lane & 31);
   const bool qv = q < N;
   bf16x8 qf[4], gf[4];
   load_row_frags(Qb + (long)q * ld, qv, lane, qf);
@@ -1085,7 +1103,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
     step(std::integral_constant<int, 0>{}, kt);
     if (kt + 1 < nt) step(std::integral_constant<int, 1>{}, kt + 1);
   }
-  const int qw = blockIdx.x * AQ + wv * 32;
+  const int qw = bid.x * AQ + wv * 32;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int qq = qw + (r & 3) + 8 * (r >> 2) + 4 * hl;
@@ -1155,7 +1173,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
   __shared__ __attribute__((aligned(16))) float srow[2][2][AK];    // [stage][lse2|delta]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
@@ -1164,7 +1183,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
   const bf16* Gb = dout + (long)b * N * D + h * 64;
   const float* L = lse2p + (long)z * Npad;
   const float* Dl = deltap + (long)z * Npad;
-  const int key = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  const int key = bid.x * AQ + wv * 32 + (lane & 31);
   bf16x8 kf[4], vf[4];
   load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
   load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
@@ -1212,7 +1231,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
     step(std::integral_constant<int, 0>{}, qt);
     if (qt + 1 < nt) step(std::integral_constant<int, 1>{}, qt + 1);
   }
-  const int kw = blockIdx.x * AQ + wv * 32;
+  const int kw = bid.x * AQ + wv * 32;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;
@@ -1273,7 +1292,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __r
   __shared__ __attribute__((aligned(16))) float srow[3][2][AK];    // [stage][lsn|dln]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int z = blockIdx.y, b = z / H, h = z - b * H;
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
   const bf16* Qb = qkv + (long)b * N * ld + h * 64;
@@ -1282,7 +1302,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __r
   const bf16* Gb = dout + (long)b * N * D + h * 64;
   const float* L = lsnp + (long)z * Npad;
   const float* Dl = dlnp + (long)z * Npad;
-  const int key = blockIdx.x * AQ + wv * 32 + (lane & 31);
+  const int key = bid.x * AQ + wv * 32 + (lane & 31);
   bf16x8 kf[4], vf[4];
   load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
   load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
@@ -1382,7 +1402,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __r
     if (j + 1 < nt) step(std::integral_constant<int, 1>{}, j + 1);
     if (j + 2 < nt) step(std::integral_constant<int, 2>{}, j + 2);
   }
-  const int kw = blockIdx.x * AQ + wv * 32;
+  const int kw = bid.x * AQ + wv * 32;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;

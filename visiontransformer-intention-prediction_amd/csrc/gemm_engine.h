@@ -664,13 +664,20 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void gemm_bf16_glds_kern
   __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];  // [stage][A image | B image]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 1, wn = wv & 1;  // wave-uniform (SGPR)
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  // Workgroups reach the XCDs round-robin in FLAT dispatch order (x fastest), so the remap runs
+  // over the flattened (tile, batch*split) id: each XCD gets a contiguous run of work items,
+  // tile-minor, i.e. whole splits — the K-chunk panels of one split are then fetched into one
+  // L2 and shared by its tiles. (Remapping blockIdx.x alone scattered every split's tiles over
+  // all 8 XCDs: split-K weight gradients read ~3x their operand bytes from HBM.)
+  const int tiles = tilesM * tilesN;
+  const int flat = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
+  const int zs = flat / tiles, lin = flat - zs * tiles;
   // Group the smaller tile dimension innermost: the workgroups an XCD runs together then share
   // the panel of the larger operand through its L2 (tm-major when tilesM >= tilesN). For the
   // LiDAR patch-embed weight gradient (3 x 145 tiles, B = 1.34 GB) tm-major re-read B 3 times.
   const bool tmin = tilesN > tilesM;
   const int tm = tmin ? lin % tilesM : lin / tilesN, tn = tmin ? lin / tilesM : lin - (lin / tilesN) * tilesN;
-  const int z = blockIdx.y / splits, split = blockIdx.y - z * splits;
+  const int z = zs / splits, split = zs - z * splits;
   const LA la = la_.bind(z);
   const LB lb = lb_.bind(z);
   const EPI epi = epi_.bind(z);
