@@ -240,9 +240,22 @@ struct LdConvWFlip {
 // apply8(z, split, m, n, v, nv): outputs (m, n .. n+nv-1), nv <= 8, m < M, n < N. The engine
 // hands each lane 8 consecutive columns (accumulators transposed through LDS), so stores are
 // 16-byte vectors whenever the destination is aligned.
+//
+// Two-phase form used by epilogue_tile: a lane's columns are the same for every row it
+// stores, so col() loads the per-column operands (bias) ONCE per tile, and row() issues the
+// per-row loads (residual, pre-activation, position rows) of all the lane's rows before any
+// of them is consumed; out8() then only computes and stores. (Per-call loads behind a
+// s_waitcnt made the epilogue a serial chain of ~8 exposed global-load latencies per wave.)
+struct NoCol {};
+struct NoRow {};
+struct Bias8 { float b[8]; };
+struct Row8 { float r[8]; };
+
 template <typename O>
 struct EpiStore {  // out = act(alpha*acc + bias[n]); optional pre-activation copy
   O* out; long ldo; BatchOff bo; const float* bias; int act; O* pre; float alpha;
+  using Col = Bias8;
+  using Row = NoRow;
   IVIT_DEV EpiStore bind(int z) const {
     EpiStore t = *this;
     const long o = bo.at(z);
@@ -250,12 +263,18 @@ struct EpiStore {  // out = act(alpha*acc + bias[n]); optional pre-activation co
     t.pre = pre ? pre + o : nullptr;
     return t;
   }
-  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
-    float x[8];
-    float bb[8];
-    if (bias) load8f(bias + n, bb, nv);
+  IVIT_DEV void col(int n, int nv, Col& c) const {
+    if (bias) load8f(bias + n, c.b, nv);
+    else {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = v[k] * alpha + (bias ? bb[k] : 0.f);
+      for (int k = 0; k < 8; ++k) c.b[k] = 0.f;
+    }
+  }
+  IVIT_DEV void row(int, int, int, Row&) const {}
+  IVIT_DEV void out8(int, int m, int n, const float (&v)[8], int nv, const Col& c, const Row&) const {
+    float x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = v[k] * alpha + c.b[k];
     const long o = (long)m * ldo + n;
     if (pre) store8(pre + o, x, nv);
     if (act == IVIT_ACT_GELU) {
@@ -267,32 +286,62 @@ struct EpiStore {  // out = act(alpha*acc + bias[n]); optional pre-activation co
     }
     store8(out + o, x, nv);
   }
+  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
+    Col c;
+    col(n, nv, c);
+    out8(0, m, n, v, nv, c, Row{});
+  }
 };
 
 struct EpiResid {  // out(f32) = res + scale[m / rps] * (acc + bias[n])
   float* out; long ldo; const float* res; long ldr; const float* bias; const float* scale; int rps;
+  using Col = Bias8;
+  struct Row { float r[8]; float s; };
   IVIT_DEV EpiResid bind(int) const { return *this; }
-  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
-    float bb[8], rr[8], x[8];
-    if (bias) load8f(bias + n, bb, nv);
-    load8f(res + (long)m * ldr + n, rr, nv);
-    const float s = scale ? scale[m / rps] : 1.f;
+  IVIT_DEV void col(int n, int nv, Col& c) const {
+    if (bias) load8f(bias + n, c.b, nv);
+    else {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = rr[k] + s * (v[k] + (bias ? bb[k] : 0.f));
+      for (int k = 0; k < 8; ++k) c.b[k] = 0.f;
+    }
+  }
+  IVIT_DEV void row(int m, int n, int nv, Row& r) const {
+    load8f(res + (long)m * ldr + n, r.r, nv);
+    r.s = scale ? scale[m / rps] : 1.f;
+  }
+  IVIT_DEV void out8(int, int m, int n, const float (&v)[8], int nv, const Col& c, const Row& r) const {
+    float x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = r.r[k] + r.s * (v[k] + c.b[k]);
     store8(out + (long)m * ldo + n, x, nv);
+  }
+  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
+    Col c;
+    Row r;
+    col(n, nv, c);
+    row(m, n, nv, r);
+    out8(0, m, n, v, nv, c, r);
   }
 };
 
 template <typename O, typename P>
 struct EpiGeluGrad {  // out = acc * gelu'(pre)
   O* out; long ldo; const P* pre; long ldp;
+  using Col = NoCol;
+  using Row = Row8;
   IVIT_DEV EpiGeluGrad bind(int) const { return *this; }
-  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
-    float pp[8], x[8];
-    load8f(pre + (long)m * ldp + n, pp, nv);
+  IVIT_DEV void col(int, int, Col&) const {}
+  IVIT_DEV void row(int m, int n, int nv, Row& r) const { load8f(pre + (long)m * ldp + n, r.r, nv); }
+  IVIT_DEV void out8(int, int m, int n, const float (&v)[8], int nv, const Col&, const Row& r) const {
+    float x[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = v[k] * gelu_grad_t<O>(pp[k]);
+    for (int k = 0; k < 8; ++k) x[k] = v[k] * gelu_grad_t<O>(r.r[k]);
     store8(out + (long)m * ldo + n, x, nv);
+  }
+  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
+    Row r;
+    row(m, n, nv, r);
+    out8(0, m, n, v, nv, Col{}, r);
   }
 };
 
@@ -302,34 +351,67 @@ struct EpiSlab {  // split-K partial slab [split][M][N] (f32)
   // gradient of a wgrad (colsum of dY) — computed on the MFMA pipe against a ones operand.
   static constexpr bool kBiasOnes = true;
   float* slab; long M, N; float* bslab = nullptr;
+  using Col = NoCol;
+  using Row = NoRow;
   IVIT_DEV EpiSlab bind(int) const { return *this; }
-  IVIT_DEV void apply8(int, int split, int m, int n, const float (&v)[8], int nv) const {
+  IVIT_DEV void col(int, int, Col&) const {}
+  IVIT_DEV void row(int, int, int, Row&) const {}
+  IVIT_DEV void out8(int split, int m, int n, const float (&v)[8], int nv, const Col&, const Row&) const {
     store8(slab + ((long)split * M + m) * N + n, v, nv);
+  }
+  IVIT_DEV void apply8(int, int split, int m, int n, const float (&v)[8], int nv) const {
+    out8(split, m, n, v, nv, Col{}, Row{});
   }
 };
 
 struct EpiPatch {  // token (b, 1 + p) of x(f32) = acc + bias[n] + pos[1 + p][n]
   float* out; int Np, D; const float* bias; const float* pos;
+  using Col = Bias8;
+  using Row = Row8;
   IVIT_DEV EpiPatch bind(int) const { return *this; }
-  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
+  IVIT_DEV void col(int n, int nv, Col& c) const { load8f(bias + n, c.b, nv); }
+  IVIT_DEV void row(int m, int n, int nv, Row& r) const {
+    const int p = m - (m / Np) * Np;
+    load8f(pos + (long)(1 + p) * D + n, r.r, nv);
+  }
+  IVIT_DEV void out8(int, int m, int n, const float (&v)[8], int nv, const Col& c, const Row& r) const {
     const int b = m / Np, p = m - b * Np;
     const long row = (long)b * (Np + 1) + 1 + p;
-    float bb[8], pp[8], x[8];
-    load8f(bias + n, bb, nv);
-    load8f(pos + (long)(1 + p) * D + n, pp, nv);
+    float x[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = v[k] + bb[k] + pp[k];
+    for (int k = 0; k < 8; ++k) x[k] = v[k] + c.b[k] + r.r[k];
     store8(out + row * D + n, x, nv);
+  }
+  IVIT_DEV void apply8(int, int, int m, int n, const float (&v)[8], int nv) const {
+    Col c;
+    Row r;
+    col(n, nv, c);
+    row(m, n, nv, r);
+    out8(0, m, n, v, nv, c, r);
   }
 };
 
 // Wave-local accumulator transpose through LDS (the staging buffers are free after the
-// main loop): 32-row halves of the wave's 64x64 tile, row stride 68 floats.
+// main loop): 32-row halves of the wave's 64x64 tile, row stride 68 floats. Lane l stores
+// columns nbase + 8(l & 7) .. +7 of rows (l >> 3) + 8t (t = 0..3) of each half: the column
+// operands are loaded once, the 8 rows' operands all before the first LDS write.
 constexpr int EP_LD = 68;
 template <class EPI>
 IVIT_DEV void epilogue_tile(float* ep, f32x16 (&acc)[2][2], const EPI& epi, int z, int split, int mbase, int nbase,
                             int M, int N, int lane) {
   const int h = lane >> 5;
+  const int c0 = (lane & 7) * 8, n = nbase + c0, nv = min(8, N - n);
+  const bool nok = n < N;
+  typename EPI::Col col;
+  if (nok) epi.col(n, nv, col);
+  typename EPI::Row rows[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int m = mbase + 32 * i + (lane >> 3) + 8 * t;
+      if (nok && m < M) epi.row(m, n, nv, rows[i][t]);
+    }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -338,17 +420,21 @@ IVIT_DEV void epilogue_tile(float* ep, f32x16 (&acc)[2][2], const EPI& epi, int 
       for (int r = 0; r < 16; ++r)
         ep[((r & 3) + 8 * (r >> 2) + 4 * h) * EP_LD + 32 * j + (lane & 31)] = acc[i][j][r];
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes are complete
+    float v[4][8];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int row = (lane >> 3) + 8 * t, c0 = (lane & 7) * 8;
-      float v[8];
+      const int row = (lane >> 3) + 8 * t;
       const float4 a = *(const float4*)(ep + row * EP_LD + c0);
       const float4 b = *(const float4*)(ep + row * EP_LD + c0 + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-      const int m = mbase + 32 * i + row, n = nbase + c0;
-      if (m < M && n < N) epi.apply8(z, split, m, n, v, min(8, N - n));
+      v[t][0] = a.x; v[t][1] = a.y; v[t][2] = a.z; v[t][3] = a.w;
+      v[t][4] = b.x; v[t][5] = b.y; v[t][6] = b.z; v[t][7] = b.w;
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int m = mbase + 32 * i + (lane >> 3) + 8 * t;
+      if (nok && m < M) epi.out8(split, m, n, v[t], nv, col, rows[i][t]);
+    }
   }
 }
 
