@@ -42,7 +42,9 @@ def step_flops(B, H, W, depth=12, D=384, C_l=290, C_m=9, planes=512, A=5, K=8, a
     return B * (3 * fwd - patch), B * (3 * vit), B * fwd
 
 
-ROOF_KERNEL = "attn_fwd_bf16_v5_kernel<4"  # the kernel ivit_attn_fwd launches by default (bf16)
+# the kernel the bf16 ViT blocks launch: v6 on the prescaled Q (ivit_attn_fwd_q2), v5 with IVIT_ATTN_Q2=0
+ROOF_KERNEL = ("attn_fwd_bf16_v6_kernel<4" if os.environ.get("IVIT_ATTN_Q2", "1") == "1" else "attn_fwd_bf16_v5_kernel<4")
+ROOF_ENTRY = "ivit_attn_fwd_q2" if ROOF_KERNEL.startswith("attn_fwd_bf16_v6") else "ivit_attn_fwd"
 
 
 def attn_fwd_flops(B, N, H, Dh=64):
@@ -224,7 +226,7 @@ def main():
                                      "random-init weights)",
         "config": {"workload": workload, "global_batch": gb, "per_gpu_batch": B, "grid": [H, W],
                    "tokens_per_stream": N, "parallelism": f"dp{world}"},
-        "roofline": {"kernel": ROOF_KERNEL + "> (ivit_attn_fwd)", "bound": "mfma",
+        "roofline": {"kernel": ROOF_KERNEL + f"> ({ROOF_ENTRY})", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "per_launch": f"4*B*H*N^2*64 = {afl:.4g} flop (B={B}, H=6, N={N}); {attn_ms:.4f} ms avg over "

@@ -37,6 +37,11 @@ const char* ivit_last_error(void);
 int ivit_linear_fwd(int dtype, const void* X, long ldx, const void* W, const float* bias, long M, long N, long K,
                     int act, void* Y, long ldy, int y_dtype, void* Ypre, const float* resid, long ldr,
                     const float* row_scale, long rows_per_scale, void* stream);
+/* Y = X W^T + bias with columns n < scale_cols multiplied by col_scale (after the bias): the
+ * fused qkv projection of timm Attention (attn.qkv, timm Attention.forward) writing its Q block
+ * pre-multiplied by log2(e)/sqrt(Dh) for ivit_attn_fwd_q2 / ivit_attn_bwd_q2. */
+int ivit_linear_fwd_qs(int dtype, const void* X, long ldx, const void* W, const float* bias, long M, long N, long K,
+                       void* Y, long ldy, int y_dtype, long scale_cols, float col_scale, void* stream);
 /* dX[M,K] = dY[M,N] W[N,K]  (optionally * gelu'(pre[M,K])). */
 int ivit_linear_dgrad(int dtype, const void* dY, long lddy, const void* W, long M, long N, long K, void* dX,
                       long lddx, int dx_dtype, const void* gelu_pre, long ldpre, void* stream);
@@ -89,6 +94,14 @@ int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H, long Dh, v
                   long work_bytes, void* stream);
 int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse, long B, long N,
                   long H, long Dh, void* dqkv, void* work, long work_bytes, void* stream);
+/* bf16 path with the Q block of qkv pre-multiplied by log2(e)/sqrt(Dh) (ivit_linear_fwd_qs):
+ * the kernels take exp2 of the raw MFMA output (the running max / -lse as the initial
+ * accumulator), no per-score scaling. Same outputs as ivit_attn_fwd / ivit_attn_bwd with dtype
+ * IVIT_BF16 on the unscaled q; dqkv is the gradient w.r.t. the UNSCALED q, k, v.            */
+int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh, void* out, float* lse, void* work,
+                     long work_bytes, void* stream);
+int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* dout, const float* lse, long B, long N, long H,
+                     long Dh, void* dqkv, void* work, long work_bytes, void* stream);
 
 /* ---- LayerNorm over the last dim D (timm norm1/norm2/norm eps 1e-6; adapters eps 1e-5).
  *      Input rows r -> (r / rpb) * rstride + roff + r % rpb (rpb = 0: identity) of X (f32).    */

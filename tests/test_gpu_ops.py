@@ -122,6 +122,40 @@ def test_attention(B, N, H, cd):
         assert _rel(d[:, i], g[:, i]) < (1e-4 if cdt == F32 else 3e-2), ("qkv"[i], _rel(d[:, i], g[:, i]))
 
 
+@pytest.mark.parametrize("B,N,H", [(1, 64, 1), (2, 257, 3), (1, 4501, 2)])
+def test_attention_q2_prescaled_path(B, N, H):
+    """bf16 ViT-block path: the qkv projection stores q * log2(e)/8 (ivit_linear_fwd_qs) and the
+    attention kernels run on it (ivit_attn_fwd_q2 / _bwd_q2). Outputs, lse and the gradient w.r.t.
+    the UNSCALED q, k, v against the f64 reference on the unscaled q (bf16 tolerances)."""
+    import ops
+    from _lib import BF16
+    D = H * 64
+    M, K = B * N, 96
+    x = torch.randn(M, K)
+    w = torch.randn(3 * D, K) / math.sqrt(K)
+    b = torch.randn(3 * D) * 0.1
+    xd, wd = ops.cast(x.to(DEV), torch.bfloat16), ops.cast(w.to(DEV), torch.bfloat16)
+    qkv_s = ops.qkv_fwd_q2(xd, wd, b.to(DEV), D)
+    qkv, _ = ops.linear_fwd(xd, wd, b.to(DEV), BF16)
+    ref_s = qkv.float().clone()
+    ref_s[:, :D] *= ops.Q2_SCALE
+    assert _rel(qkv_s.float(), ref_s) < 8e-3  # one bf16 rounding of (xW^T + b) * c on the Q block
+    qs = qkv.clone()
+    qs[:, :D] = (qkv[:, :D].float() * ops.Q2_SCALE).to(torch.bfloat16)
+    o, lse = ops.attn_fwd_q2(qs, B, N, H)
+    qr = qkv.float().cpu().double().requires_grad_(True)
+    oref, lref = _attn_ref(qr, B, N, H)
+    assert _rel(o.float(), oref.detach()) < 2e-2
+    assert _rel(lse, lref.detach()) < 6e-4  # the extra bf16 rounding of q * c (the f32 test rounds q once)
+    dod = ops.cast(torch.randn(B * N, D).to(DEV), torch.bfloat16)
+    oref.backward(dod.float().cpu().double())
+    dq = ops.attn_bwd_q2(qs, o, dod, lse, B, N, H)
+    g = qr.grad.reshape(B * N, 3, D)
+    d = dq.float().cpu().reshape(B * N, 3, D)
+    for i in range(3):
+        assert _rel(d[:, i], g[:, i]) < 3e-2, ("qkv"[i], _rel(d[:, i], g[:, i]))
+
+
 def test_attention_large_grid_bf16():
     """BASELINE config 5 sequence length (800x1440 grid: N = 100*180 + 1 = 18001), bf16 flash
     kernels vs an f32 torch reference on the device (scores materialised per head)."""

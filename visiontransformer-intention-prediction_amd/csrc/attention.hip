@@ -851,6 +851,237 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v5_kernel(const b
   }
 }
 
+// ------------------------------------------------------------------------- forward v6 (bf16)
+// v5 with the softmax scale and the running max folded into the matrix pipe: Q is prescaled by
+// c2 = log2(e)/sqrt(Dh) once (in f32, rounded to bf16 — one more bf16 rounding of Q, the
+// same size as the one the QKV GEMM output already carries), and every S chain starts from
+// the accumulator -m (a persistent register block), so the MFMA returns S' - m directly and
+// p = exp2(acc): the 32 v_fma_f32 per wave-tile (4 issue cycles each, of a VALU-issue-bound
+// step: tools/pmc_anatomy.py) disappear. When the lazy rescale moves m, the already computed
+// next tile is shifted by the same amount (rare).
+IVIT_DEV void qk_tile_c(const char* kimg, const bf16x8 (&qf)[4], const f32x16& init, f32x16 (&s)[2], int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], ks == 0 ? init : s[t], 0, 0, 0);
+    }
+  }
+}
+
+IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], const f32x16 (&cur)[2],
+                                f32x16 (&nxt)[2], f32x16& o0, f32x16& o1, f32x16& lacc, const bf16x8& ones,
+                                const f32x16& negm, int lane) {
+  const int hl = lane >> 5;
+  auto kfrag = [&](int i) {
+    return *(const bf16x8*)(kimg + t_off(32 * (i >> 2) + (lane & 31), 2 * (i & 3) + hl));
+  };
+  bf16x8 p[4];
+  auto ex = [&](int i) { p[i >> 3][i & 7] = (bf16)fast_exp2(cur[i >> 4][i & 15]); };
+  bf16x8 ka[8];
+  ka[0] = kfrag(0);
+  ka[1] = kfrag(1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i + 2 < 8) ka[i + 2] = kfrag(i + 2);
+    const int t = i >> 2, ks = i & 3;
+    nxt[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[i], qf[ks], ks == 0 ? negm : nxt[t], 0, 0, 0);
+    ex(2 * i);
+    ex(2 * i + 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  bf16x8 vf[8];
+  auto vread = [&](int f) { vf[f] = tr_acc_order(vimg, 16 * (f >> 1), 32 * (f & 1), lane); };
+  vread(0);
+  vread(1);
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr int e0[7] = {16, 19, 22, 25, 28, 30, 32};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const int g = k / 3, which = k % 3;
+    if (k == 0) vread(2);
+    if (k == 1) vread(3);
+    if (k == 3) vread(4);
+    if (k == 4) vread(5);
+    if (which == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g], p[g], o0, 0, 0, 0);
+    else if (which == 1) o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g + 1], p[g], o1, 0, 0, 0);
+    else lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[g], lacc, 0, 0, 0);
+#pragma unroll
+    for (int i = e0[k]; i < e0[k + 1]; ++i) ex(i);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float a = NEG_BIG, bm = NEG_BIG;
+#pragma unroll
+  for (int k = 6; k < 12; ++k) {
+    const int g = k / 3, which = k % 3;
+    if (k == 6) vread(6);
+    if (k == 7) vread(7);
+    if (which == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g], p[g], o0, 0, 0, 0);
+    else if (which == 1) o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g + 1], p[g], o1, 0, 0, 0);
+    else lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[g], lacc, 0, 0, 0);
+    const int v0 = 6 * (k - 6);
+#pragma unroll
+    for (int v = v0; v < v0 + 6 && v < 32; v += 2) {
+      if ((v >> 1) & 1) bm = vmax3(bm, nxt[v >> 4][v & 15], nxt[v >> 4][(v & 15) + 1]);
+      else a = vmax3(a, nxt[v >> 4][v & 15], nxt[v >> 4][(v & 15) + 1]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return half_swap_max(fmaxf(a, bm));  // max of S'_{j+1} - m
+}
+
+// PRE: prescale Q by c2 in the kernel (ivit_attn_fwd variant 11); otherwise the Q block of qkv
+// already holds q * c2 (ivit_attn_fwd_q2).
+template <int W, bool PRE>
+__global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const bf16* __restrict__ qkv, int N, int H,
+                                                                        bf16* __restrict__ out,
+                                                                        float* __restrict__ lse, float c2) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int q = bid.x * (32 * W) + wv * 32 + (lane & 31);
+  bf16x8 qf[4];
+  load_row_frags(Qb + (long)q * ld, q < N, lane, qf);
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) qf[i][e] = (bf16)((float)qf[i][e] * c2);
+  }
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  int off[8 / W];
+#pragma unroll
+  for (int i = 0; i < 8 / W; ++i) off[i] = dma_off<W>(i, wv, lane, ld);
+  auto issue1 = [&](const bf16* base, int kt, char* img) {
+    if (kt < nfull) {
+      const bf16* src = base + (long)kt * AK * ld;
+#pragma unroll
+      for (int i = 0; i < 8 / W; ++i) glds<16>((src + off[i]), img + (wv * (8 / W) + i) * 1024);
+    } else {
+      tile_glds_w<W>(base, ld, kt * AK, N, img, wv, lane);
+    }
+  };
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+
+  // prologue: S'_0 (from a zero accumulator), m = its row max, then S'_0 - m; K_1 in flight
+  issue1(Kb, 0, smem[0][0]);
+  issue1(Vb, 0, smem[0][1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (nt > 1) issue1(Kb, 1, smem[1][0]);
+  f32x16 sc[2], sn[2];
+  qk_tile_c(smem[0][0], qf, zero16(), sc, lane);
+  float m = nfull > 0 ? tile_rowmax<false>(sc, 0, N, lane) : tile_rowmax<true>(sc, 0, N, lane);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sc[t][r] -= m;
+  f32x16 negm;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) negm[r] = -m;
+  f32x16 o0 = zero16(), o1 = zero16(), lacc = zero16();
+
+  // after S'_{j+1} - m and its row max mt: move m lazily; the next tile is shifted with it
+  auto rescale = [&](float mt, f32x16(&nxt)[2]) {
+    const bool moved = mt > TAU;
+    if (__any(moved)) {
+      const float d = moved ? mt : 0.f;  // new m = m + d
+      const float alpha = fast_exp2(-d);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; }
+      lacc[0] *= alpha;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) nxt[t][r] -= d;
+      m += d;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) negm[r] = -m;
+    }
+  };
+  auto body = [&](auto stage, auto nxmode, int j, f32x16(&cur)[2], f32x16(&nxt)[2]) {
+    constexpr int S = decltype(stage)::value;  // V_j in smem[S][1], K_{j+1} in smem[S^1][0]
+    constexpr int NX = decltype(nxmode)::value;
+    const bool more = NX == 1 || j + 1 < nt;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (j + 2 < nt) issue1(Kb, j + 2, smem[S][0]);
+    if (more) issue1(Vb, j + 1, smem[S ^ 1][1]);
+    if constexpr (NX == 1) {
+      rescale(fwd_step_fenced6(smem[S ^ 1][0], smem[S][1], qf, cur, nxt, o0, o1, lacc, ones, negm, lane), nxt);
+      return;
+    }
+    if (more) qk_tile_c(smem[S ^ 1][0], qf, negm, nxt, lane);
+    bf16x8 p[4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)fast_exp2(cur[t][8 * ss + e]);
+        p[2 * t + ss] = v;
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const int rb = 32 * t + 16 * ss;
+        const bf16x8 va0 = tr_acc_order(smem[S][1], rb, 0, lane);
+        const bf16x8 va1 = tr_acc_order(smem[S][1], rb, 32, lane);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, p[2 * t + ss], o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, p[2 * t + ss], o1, 0, 0, 0);
+        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[2 * t + ss], lacc, 0, 0, 0);
+      }
+    if (more) {
+      const float mt = NX == 1 || j + 1 < nfull ? tile_rowmax<false>(nxt, (j + 1) * AK, N, lane)
+                                                : tile_rowmax<true>(nxt, (j + 1) * AK, N, lane);
+      rescale(mt, nxt);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I3 = std::integral_constant<int, 3>;
+  int j = 0;
+  for (; j + 2 < nfull; j += 2) {
+    body(I0{}, I1{}, j, sc, sn);
+    body(I1{}, I1{}, j + 1, sn, sc);
+  }
+  for (; j < nt; ++j) {
+    if (j & 1) body(I1{}, I3{}, j, sn, sc);
+    else body(I0{}, I3{}, j, sc, sn);
+  }
+  if (q < N) {
+    const float l = lacc[0];
+    const float inv = 1.f / l;
+    bf16* orow = out + ((long)b * N + q) * D + h * 64;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      Pack4 a, c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        a.h[e] = (bf16)(o0[4 * g + e] * inv);
+        c.h[e] = (bf16)(o1[4 * g + e] * inv);
+      }
+      const int d = 8 * g + 4 * hl;
+      *(uint2*)(orow + d) = a.u;
+      *(uint2*)(orow + 32 + d) = c.u;
+    }
+    if (hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
+  }
+}
+
 // ------------------------------------------------------------------------- dK, dV (bf16)
 // (register-staged variant, IVIT_ATTN_DKV_VARIANT=1; rows from the padded lse2 / delta arrays)
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_bf16_kernel(const bf16* __restrict__ qkv,
@@ -998,13 +1229,16 @@ __global__ void attn_rows_v2_kernel(const bf16* __restrict__ o, const bf16* __re
 }
 
 // One dQ tile step: keys kbase.. of the K/V images against this wave's 32 queries.
-template <bool MASK>
+// Q2: qf holds q * c2 and nl = -lse2 in every register: S' - lse2 comes straight out of the
+// MFMA chain (nl as its initial accumulator) and p = exp2 of it, no per-score FMA.
+template <bool MASK, bool Q2 = false>
 IVIT_DEV void dq_tile(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], const bf16x8 (&gf)[4], f32x16& a0,
-                      f32x16& a1, float lse2, float dlt, int kbase, int N, float c2, int lane) {
+                      f32x16& a1, float lse2, float dlt, int kbase, int N, float c2, int lane,
+                      const f32x16& nl = f32x16{}) {
   const int hl = lane >> 5;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    f32x16 s = zero16(), dp;
+    f32x16 s = Q2 ? nl : zero16(), dp;
 #pragma unroll
     for (int r = 0; r < 16; ++r) dp[r] = -dlt;  // row constant as the initial accumulator
 #pragma unroll
@@ -1016,7 +1250,7 @@ IVIT_DEV void dq_tile(const char* kimg, const char* vimg, const bf16x8 (&qf)[4],
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      float p = fast_exp2(fmaf(s[r], c2, -lse2));
+      float p = Q2 ? fast_exp2(s[r]) : fast_exp2(fmaf(s[r], c2, -lse2));
       if (MASK) {
         const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
         if (key >= N) p = 0.f;
@@ -1038,7 +1272,7 @@ IVIT_DEV void dq_tile(const char* kimg, const char* vimg, const bf16x8 (&qf)[4],
 // dQ: 4 waves x 32 queries; K/V tiles by LDS-DMA (k-invariant offsets, ragged tail guarded),
 // tile loop unrolled by two so the LDS stage is a compile-time constant.
 // V3ROWS: the row constants come from attn_rows_v3_kernel (lsn = -lse sqrt(Dh), dln = -delta).
-template <bool V3ROWS = false>
+template <bool V3ROWS = false, bool Q2 = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __restrict__ qkv,
                                                                 const bf16* __restrict__ dout,
                                                                 const float* __restrict__ lse2p,
@@ -1067,6 +1301,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
     dlt = -dlt;
   }
   f32x16 a0 = zero16(), a1 = zero16();
+  f32x16 nl;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) nl[r] = -lse2;
   const int nt = (N + AK - 1) / AK, nfull = N / AK;
   int off[2];
 #pragma unroll
@@ -1090,9 +1327,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
     constexpr int S = decltype(stage)::value;
     if (kt + 1 < nt) issue(kt + 1, smem[S ^ 1][0], smem[S ^ 1][1]);
     if (kt < nfull)
-      dq_tile<false>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane);
+      dq_tile<false, Q2>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane, nl);
     else
-      dq_tile<true>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane);
+      dq_tile<true, Q2>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane, nl);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
@@ -1545,6 +1782,10 @@ extern "C" int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H,
       dim3 g(ivit_cdiv(N, 128), B * H);
       hipLaunchKernelGGL((attn_fwd_bf16_v5_kernel<4, true>), g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
                          (bf16*)out, lse, scale * LOG2E);
+    } else if (variant == 11) {  // v6: prescaled Q, -m as the initial accumulator (no per-score FMA)
+      dim3 g(ivit_cdiv(N, 128), B * H);
+      hipLaunchKernelGGL((attn_fwd_bf16_v6_kernel<4, true>), g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
+                         (bf16*)out, lse, scale * LOG2E);
     } else if (variant == 8) {  // v4 with the row sums on the MFMA pipe
       dim3 g(ivit_cdiv(N, 128), B * H);
       hipLaunchKernelGGL((attn_fwd_bf16_v4_kernel<4, 2, true>), g, dim3(256), 0, st, (const bf16*)qkv, (int)N, (int)H,
@@ -1678,6 +1919,43 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
     EpiStore<float> e{dq + D, ldq, qoff, nullptr, IVIT_ACT_NONE, nullptr, scale};
     launch_gemm<false, false>(false, la, lb, e, (int)N, (int)Dh, (int)N, Z, 1, st);
   }
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+// ------------------------------------------------------------------------- Q-prescaled bf16 path
+extern "C" int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh, void* out, float* lse, void* work,
+                                long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(Dh == 64, "ivit_attn_fwd_q2: head dim must be 64 (got %ld)", Dh);
+  (void)work;
+  (void)work_bytes;
+  if (B * N * H == 0) return 0;
+  dim3 g(ivit_cdiv(N, 128), B * H);
+  hipLaunchKernelGGL((attn_fwd_bf16_v6_kernel<4, false>), g, dim3(256), 0, ivit_stream(stream), (const bf16*)qkv,
+                     (int)N, (int)H, (bf16*)out, lse, 1.0f);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+// With q' = q c2 in qkv: P = exp2(q'k - lse2) (c2 = 1 in the kernels); dQ = scale dS K as before
+// (the gradient w.r.t. the unscaled q); dK = ln2 dS^T q' = scale dS^T q.
+extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* dout, const float* lse, long B, long N,
+                                long H, long Dh, void* dqkv, void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(Dh == 64, "ivit_attn_bwd_q2: head dim must be 64 (got %ld)", Dh);
+  IVIT_CHECK_ARG(work_bytes >= ivit_attn_workspace(IVIT_BF16, B, N, H, Dh, 1), "ivit_attn_bwd_q2: workspace too small");
+  if (B * N * H == 0) return 0;
+  hipStream_t st = ivit_stream(stream);
+  const float scale = 1.0f / sqrtf((float)Dh);
+  dim3 g(ivit_cdiv(N, AQ), B * H);
+  const long Npad = (N + AK - 1) / AK * AK;
+  float* lse2p = (float*)work;
+  float* deltap = lse2p + B * H * Npad;
+  hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad * 8, 256)), dim3(256), 0, st, (const bf16*)out,
+                     (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
+  hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<false, true>), g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout,
+                     lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, scale);
+  hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p, deltap,
+                     (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, 0.69314718055994531f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -251,10 +251,15 @@ struct NoRow {};
 struct Bias8 { float b[8]; };
 struct Row8 { float r[8]; };
 
+// qcols > 0: columns n < qcols are additionally scaled by qscale (the attention's Q block of a
+// fused qkv projection stored as q * log2(e)/sqrt(Dh); ivit_linear_fwd_qs). qcols % 8 == 0,
+// so the factor is uniform over a lane's 8 columns.
+struct BiasS { float b[8]; float s; };
 template <typename O>
-struct EpiStore {  // out = act(alpha*acc + bias[n]); optional pre-activation copy
+struct EpiStore {  // out = act(alpha*acc + bias[n]) [* qscale for n < qcols]; optional pre-activation copy
   O* out; long ldo; BatchOff bo; const float* bias; int act; O* pre; float alpha;
-  using Col = Bias8;
+  int qcols = 0; float qscale = 1.f;
+  using Col = BiasS;
   using Row = NoRow;
   IVIT_DEV EpiStore bind(int z) const {
     EpiStore t = *this;
@@ -269,12 +274,13 @@ struct EpiStore {  // out = act(alpha*acc + bias[n]); optional pre-activation co
 #pragma unroll
       for (int k = 0; k < 8; ++k) c.b[k] = 0.f;
     }
+    c.s = n < qcols ? qscale : 1.f;
   }
   IVIT_DEV void row(int, int, int, Row&) const {}
   IVIT_DEV void out8(int, int m, int n, const float (&v)[8], int nv, const Col& c, const Row&) const {
     float x[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = v[k] * alpha + c.b[k];
+    for (int k = 0; k < 8; ++k) x[k] = (v[k] * alpha + c.b[k]) * c.s;
     const long o = (long)m * ldo + n;
     if (pre) store8(pre + o, x, nv);
     if (act == IVIT_ACT_GELU) {

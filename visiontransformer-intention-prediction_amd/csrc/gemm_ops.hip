@@ -124,7 +124,7 @@ static int splitk_choice(long tiles, long K, int bk) {
 template <typename S, typename O>
 static int linear_fwd_t(const void* X, long ldx, const void* W, const float* bias, long M, long N, long K, int act,
                         void* Y, long ldy, void* Ypre, const float* resid, long ldr, const float* rs, long rps,
-                        hipStream_t st) {
+                        hipStream_t st, long qcols = 0, float qscale = 1.f) {
   const bool bf = sizeof(S) == 2;
   LdDense<S> la{(const S*)X, ldx, (int)M, (int)K, 0, 0, 0, {}};
   LdDense<S> lb{(const S*)W, K, (int)N, (int)K, 0, 0, 0, {}};
@@ -132,8 +132,29 @@ static int linear_fwd_t(const void* X, long ldx, const void* W, const float* bia
     EpiResid e{(float*)Y, ldy, resid, ldr, bias, rs, (int)(rps > 0 ? rps : 1)};
     return launch_gemm<true, true>(bf, la, lb, e, M, N, K, 1, 1, st);
   }
-  EpiStore<O> e{(O*)Y, ldy, {}, bias, act, (O*)Ypre, 1.f};
+  EpiStore<O> e{(O*)Y, ldy, {}, bias, act, (O*)Ypre, 1.f, (int)qcols, qscale};
   return launch_gemm<true, true>(bf, la, lb, e, M, N, K, 1, 1, st);
+}
+
+extern "C" int ivit_linear_fwd_qs(int dtype, const void* X, long ldx, const void* W, const float* bias, long M, long N,
+                                  long K, void* Y, long ldy, int y_dtype, long scale_cols, float col_scale,
+                                  void* stream) {
+  IVIT_CHECK_ARG(K % 8 == 0 && ldx % 8 == 0, "ivit_linear_fwd_qs: K and ldx must be multiples of 8");
+  IVIT_CHECK_ARG(scale_cols >= 0 && scale_cols <= N && scale_cols % 8 == 0,
+                 "ivit_linear_fwd_qs: scale_cols must be a multiple of 8 in [0, N] (got %ld)", scale_cols);
+  hipStream_t st = ivit_stream(stream);
+  int rc;
+  if (dtype == IVIT_BF16)
+    rc = y_dtype == IVIT_BF16 ? linear_fwd_t<bf16, bf16>(X, ldx, W, bias, M, N, K, IVIT_ACT_NONE, Y, ldy, nullptr,
+                                                         nullptr, 0, nullptr, 0, st, scale_cols, col_scale)
+                              : linear_fwd_t<bf16, float>(X, ldx, W, bias, M, N, K, IVIT_ACT_NONE, Y, ldy, nullptr,
+                                                          nullptr, 0, nullptr, 0, st, scale_cols, col_scale);
+  else
+    rc = linear_fwd_t<float, float>(X, ldx, W, bias, M, N, K, IVIT_ACT_NONE, Y, ldy, nullptr, nullptr, 0, nullptr, 0,
+                                    st, scale_cols, col_scale);
+  if (rc) return rc;
+  IVIT_LAUNCH_CHECK();
+  return 0;
 }
 
 extern "C" int ivit_linear_fwd(int dtype, const void* X, long ldx, const void* W, const float* bias, long M, long N,

@@ -158,6 +158,43 @@ def attn_fwd(qkv, B, N, H, cdt):
     return out, lse
 
 
+# bf16 ViT blocks: the qkv projection writes its Q block as q * log2(e)/sqrt(64)
+# (ivit_linear_fwd_qs) and attention runs on the prescaled Q (ivit_attn_fwd_q2 / _bwd_q2):
+# no per-score scaling FMA in the forward and dQ kernels. IVIT_ATTN_Q2=0 restores the
+# unscaled form (A/B).
+ATTN_Q2 = os.environ.get("IVIT_ATTN_Q2", "1") == "1"
+Q2_SCALE = 1.4426950408889634 / 8.0  # log2(e) / sqrt(Dh), Dh = 64
+
+
+def qkv_fwd_q2(x, w, b, D):
+    """x w^T + b with columns < D (the Q block) multiplied by Q2_SCALE; bf16 out."""
+    M, K = x.shape[0], x.shape[-1]
+    N = w.shape[0]
+    out = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    lib.ivit_linear_fwd_qs(BF16, ptr(x), x.stride(0), ptr(w), ptr(b), M, N, K, ptr(out), out.stride(0), BF16, D,
+                           Q2_SCALE, stream())
+    return out
+
+
+def attn_fwd_q2(qkv, B, N, H):
+    D = H * 64
+    out = torch.empty((B * N, D), dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty((B, H, N), dtype=torch.float32, device=qkv.device)
+    ev = KernelTimer.span("attn_fwd")
+    lib.ivit_attn_fwd_q2(ptr(qkv), B, N, H, 64, ptr(out), ptr(lse), None, 0, stream())
+    if ev is not None:
+        ev.record()
+    return out, lse
+
+
+def attn_bwd_q2(qkv, out, dout, lse, B, N, H):
+    dqkv = torch.empty_like(qkv)
+    ws = workspace(lib.ivit_attn_workspace(BF16, B, N, H, 64, 1), qkv.device)
+    lib.ivit_attn_bwd_q2(ptr(qkv), ptr(out), ptr(dout), ptr(lse), B, N, H, 64, ptr(dqkv), ptr(ws), ws.numel(),
+                         stream())
+    return dqkv
+
+
 def attn_bwd(qkv, out, dout, lse, B, N, H, cdt):
     dqkv = torch.empty_like(qkv)
     ws = workspace(lib.ivit_attn_workspace(cdt, B, N, H, 64, 1), qkv.device)
@@ -352,14 +389,20 @@ class ViTBlockFn(torch.autograd.Function):
         cd = tdtype(cdt)
         wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
         ln1, m1, r1 = layernorm_fwd(x, n1w, n1b, eps, cd)
-        qkv, _ = linear_fwd(ln1, wq, qkvb, cdt)
-        o, lse = attn_fwd(qkv, B, N, H, cdt)
+        q2 = ATTN_Q2 and cdt == BF16
+        if q2:
+            qkv = qkv_fwd_q2(ln1, wq, qkvb, H * 64)
+            o, lse = attn_fwd_q2(qkv, B, N, H)
+        else:
+            qkv, _ = linear_fwd(ln1, wq, qkvb, cdt)
+            o, lse = attn_fwd(qkv, B, N, H, cdt)
         x1, _ = linear_fwd(o, wp, pb, cdt, resid=x, row_scale=s1, rps=N)
         ln2, m2, r2 = layernorm_fwd(x1, n2w, n2b, eps, cd)
         a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=True)
         x2, _ = linear_fwd(a, w2, f2b, cdt, resid=x1, row_scale=s2, rps=N)
         ctx.save_for_backward(x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2)
         ctx.meta = meta
+        ctx.q2 = q2
         return x2
 
     @staticmethod
@@ -381,7 +424,7 @@ class ViTBlockFn(torch.autograd.Function):
                                              row_scale=s1, rps=N)
         do = linear_dgrad(dx1s, wp, cdt, cd)
         gp = _wgrad(fork, dx1s, o, cdt)
-        dqkv = attn_bwd(qkv, o, do, lse, B, N, H, cdt)
+        dqkv = attn_bwd_q2(qkv, o, do, lse, B, N, H) if ctx.q2 else attn_bwd(qkv, o, do, lse, B, N, H, cdt)
         dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
         gq = _wgrad(fork, dqkv, ln1, cdt)
         dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
