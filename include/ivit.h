@@ -186,6 +186,17 @@ long ivit_nms_workspace(long n);
 int ivit_nms(const float* boxes_xywha, const float* scores, long n, double iou_thr, long* keep, long* count,
              void* work, long work_bytes, void* stream);
 
+/* ---- Detection mAP / intention matching (eval_vit.py:191-292, calculate_ap utils.py:564-575;
+ * SURVEY.md §8f rank 2). Sample s: iou rows = its predictions in score order (descending,
+ * stable), columns = its GTs: [npred[s], ngt[s]] f32 at iou + iou_off[s]; its predictions occupy
+ * pred_off[s] .. pred_off[s] + npred[s] - 1 of the [total_pred] outputs. Per (sample, threshold):
+ * ap[s * n_thr + t] (f64) with the reference's empty-set rules; tp[t * total_pred + p] (u8) the
+ * greedy TP flags; best_gt[p] (int32) the first-max GT of each prediction (intention pairs are
+ * the TPs at 0.5). work >= 8 * n_thr * total_pred bytes; max_gt <= 4096.                     */
+int ivit_det_match(const float* iou, const long* iou_off, const int* npred, const int* ngt, const long* pred_off,
+                   long n_samples, long total_pred, const float* thresholds, long n_thr, double* ap, int* best_gt,
+                   unsigned char* tp, void* work, long work_bytes, int max_gt, void* stream);
+
 /* ---- LiDAR BEV voxelisation ----------------------------------------
  * Replaces utils.create_intentnet_lidar_bev (utils.py:62-106) and, when sweep_tf is given, the
  * per-sweep transform_points(pts, rel_tf) of dataset.py:319-340 (utils.py:27-33) in one pass.

@@ -10,7 +10,7 @@ Differences, none in the numerics: ``--synthetic`` evaluates seeded synthetic BE
 — the worst case for NMS); checkpoints load with ``torch.load(weights_only=True)`` (the
 pickled ``BasicBlock`` class in ``backbone_cfg`` is allow-listed by name); post-processing runs
 on the device for the whole batch (utils.postprocess_batch); the mAP / intention matching
-walk is vectorised (metrics.py). The reference's undefined names (eval_vit.py:12-13,39,196,219)
+walk runs on the device for all samples in one launch (metrics.match_device, ivit_det_match). The reference's undefined names (eval_vit.py:12-13,39,196,219)
 come from constants.py / utils.py.
 """
 from __future__ import annotations
@@ -25,7 +25,7 @@ import model_vit
 from constants import (ANCHOR_CONFIGS_PAPER, DETECTION_IOU_THRESHOLDS, EVAL_USE_ROTATED_IOU, GRID_HEIGHT_PX,
                        GRID_WIDTH_PX, INTENTIONS_MAP_REV, IOU_THRESHOLD_FOR_INTENTION_MATCH, LIDAR_TOTAL_CHANNELS,
                        MAP_CHANNELS, NUM_INTENTION_CLASSES)
-from metrics import detection_map, intention_matches
+from metrics import detection_map_device as detection_map, intention_matches_device as intention_matches
 from model_vit import IntentNetViT
 from synthetic import SyntheticBEVLoader
 from utils import generate_anchors, postprocess_batch
