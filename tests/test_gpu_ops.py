@@ -66,6 +66,35 @@ def test_linear_fwd_dgrad_wgrad(M, N, K, cd):
     assert _rel(dw, dyd.float().cpu().double().T @ xd.float().cpu().double()) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(4133, 512, 1024), (2100, 384, 520), (4096, 1152, 768)])
+def test_linear_big_tiles(M, N, K, monkeypatch):
+    """gemm_bf16_big_kernel (256-row tiles, BN 256 / 128; KC and MN-contiguous B) through the
+    linear fwd / GELU / residual / dgrad / GELU-grad entry points, ragged M, N and K edges."""
+    import ops
+    from _lib import ACT_GELU, BF16
+    monkeypatch.setenv("IVIT_GEMM_BIG", "2")
+    x, w, b = _lin_case(M, N, K, torch.bfloat16)
+    xd, wd, bd = ops.cast(x.to(DEV), torch.bfloat16), ops.cast(w.to(DEV), torch.bfloat16), b.to(DEV)
+    xr, wr = xd.float().cpu().double(), wd.float().cpu().double()
+    ref = xr @ wr.T + b.double()
+    y, _ = ops.linear_fwd(xd, wd, bd, BF16, out_dtype=torch.float32)
+    assert _rel(y, ref) < 1e-5
+    a, pre = ops.linear_fwd(xd, wd, bd, BF16, act=ACT_GELU, want_pre=True)
+    assert _rel(pre.float(), ref) < 1e-2 and _rel(a.float(), F.gelu(ref)) < 1e-2
+    r = torch.randn(M, N).to(DEV)
+    yr, _ = ops.linear_fwd(xd, wd, bd, BF16, resid=r)
+    assert _rel(yr, r.cpu().double() + ref) < 1e-5
+    dyd = ops.cast(torch.randn(M, K).to(DEV), torch.bfloat16)   # dX[M, N] = dY[M, K] W[K, N] (MN-contiguous W)
+    w2 = ops.cast(torch.randn(K, N).to(DEV) / math.sqrt(K), torch.bfloat16)
+    dx = ops.linear_dgrad(dyd, w2, BF16, torch.float32)
+    assert _rel(dx, dyd.float().cpu().double() @ w2.float().cpu().double()) < 1e-5
+    prek = ops.cast(torch.randn(M, N).to(DEV), torch.bfloat16)
+    dxg = ops.linear_dgrad(dyd, w2, BF16, torch.float32, gelu_pre=prek)
+    hp = prek.float().cpu().double().requires_grad_(True)
+    F.gelu(hp).backward(dyd.float().cpu().double() @ w2.float().cpu().double())
+    assert _rel(dxg, hp.grad) < 1e-3
+
+
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
 def test_layernorm(cd):
     import ops
