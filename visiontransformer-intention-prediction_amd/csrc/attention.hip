@@ -1272,13 +1272,17 @@ IVIT_DEV void dq_tile(const char* kimg, const char* vimg, const bf16x8 (&qf)[4],
 // dQ: 4 waves x 32 queries; K/V tiles by LDS-DMA (k-invariant offsets, ragged tail guarded),
 // tile loop unrolled by two so the LDS stage is a compile-time constant.
 // V3ROWS: the row constants come from attn_rows_v3_kernel (lsn = -lse sqrt(Dh), dln = -delta).
-template <bool V3ROWS = false, bool Q2 = false>
+// ROWS: this kernel also forms its queries' row constants (replacing attn_rows_v2_kernel):
+// lse2 = lse * log2(e) and delta = rowsum(dO * O) from the dO fragments it already holds and
+// the O rows, and writes both (padded rows: 1e30 / 0) for the dK/dV kernel that follows.
+template <bool V3ROWS = false, bool Q2 = false, bool ROWS = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __restrict__ qkv,
                                                                 const bf16* __restrict__ dout,
-                                                                const float* __restrict__ lse2p,
-                                                                const float* __restrict__ deltap, int N, int Npad,
+                                                                float* __restrict__ lse2p,
+                                                                float* __restrict__ deltap, int N, int Npad,
                                                                 int H, bf16* __restrict__ dqkv, float c2,
-                                                                float scale) {
+                                                                float scale, const bf16* __restrict__ out = nullptr,
+                                                                const float* __restrict__ lse = nullptr) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1294,8 +1298,26 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
   bf16x8 qf[4], gf[4];
   load_row_frags(Qb + (long)q * ld, qv, lane, qf);
   load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
-  float lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
-  float dlt = qv ? deltap[(long)z * Npad + q] : 0.f;
+  float lse2, dlt;
+  if constexpr (ROWS) {
+    bf16x8 of[4];
+    load_row_frags(out + ((long)b * N + q) * D + h * 64, qv, lane, of);
+    float d = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf((float)of[i][e], (float)gf[i][e], d);
+    d = half_swap_sum(d);  // the other 32 of the 64 dims sit in lane ^ 32
+    lse2 = qv ? lse[(long)z * N + q] * LOG2E : 1e30f;
+    dlt = qv ? d : 0.f;
+    if (hl == 0 && q < Npad) {
+      lse2p[(long)z * Npad + q] = lse2;
+      deltap[(long)z * Npad + q] = dlt;
+    }
+  } else {
+    lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
+    dlt = qv ? deltap[(long)z * Npad + q] : 0.f;
+  }
   if (V3ROWS) {
     lse2 = qv ? -lse2 * c2 : 1e30f;  // -lsn * c2 = lse * log2(e)
     dlt = -dlt;
@@ -1950,10 +1972,10 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   const long Npad = (N + AK - 1) / AK * AK;
   float* lse2p = (float*)work;
   float* deltap = lse2p + B * H * Npad;
-  hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad * 8, 256)), dim3(256), 0, st, (const bf16*)out,
-                     (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
-  hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<false, true>), g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout,
-                     lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, scale);
+  // dQ also forms the row constants (lse2, delta) the dK/dV kernel reads: no rows kernel
+  hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<false, true, true>), g, dim3(256), 0, st, (const bf16*)qkv,
+                     (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, scale,
+                     (const bf16*)out, lse);
   hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p, deltap,
                      (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, 0.69314718055994531f);
   IVIT_LAUNCH_CHECK();
