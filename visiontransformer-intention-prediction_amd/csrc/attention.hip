@@ -1874,8 +1874,8 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
     hipStream_t sq = st;
     BwdSide* side = bwd_overlap() ? bwd_side_for(st) : nullptr;
     if (side) {
-      hipEventRecord(side->fork, st);
-      hipStreamWaitEvent(side->stream, side->fork, 0);
+      if (hipEventRecord(side->fork, st) != hipSuccess || hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess)
+        IVIT_CHECK_ARG(false, "ivit_attn_bwd: side-stream fork failed");
       sq = side->stream;
     }
     if (v3)
@@ -1884,7 +1884,7 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
     else
       hipLaunchKernelGGL(attn_bwd_dq_v2_kernel<false>, g, dim3(256), 0, sq, (const bf16*)qkv, (const bf16*)dout, lse2p,
                          deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
-    if (side) hipEventRecord(side->join, sq);
+    if (side && hipEventRecord(side->join, sq) != hipSuccess) IVIT_CHECK_ARG(false, "ivit_attn_bwd: side-stream join failed");
     if (dkv_variant == 1)
       hipLaunchKernelGGL(attn_bwd_dkv_bf16_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
                          deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
@@ -1894,7 +1894,8 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
     else
       hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
                          deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
-    if (side) hipStreamWaitEvent(st, side->join, 0);
+    if (side && hipStreamWaitEvent(st, side->join, 0) != hipSuccess)
+      IVIT_CHECK_ARG(false, "ivit_attn_bwd: side-stream join failed");
     IVIT_LAUNCH_CHECK();
     return 0;
   }
