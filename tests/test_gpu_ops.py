@@ -363,6 +363,32 @@ def test_nms_bitexact_golden():
         assert np.array_equal(keep.cpu().numpy(), z[f"nms{i}_keep"]), i
 
 
+def test_nms_batched_equals_per_sample_golden_and_oracle():
+    """ivit_nms_batched: all golden NMS cases (full 22 500, heavy ties, all-equal scores,
+    IoU == 0.2f, empty) plus random ragged sets in ONE batch, each bit-exact."""
+    from conftest import golden
+    from oracle import ivit_oracle as O
+    import utils
+    z = golden("geometry.npz")
+    bl, sl, want = [], [], []
+    for i in range(int(z["nms_cases"][0])):
+        bl.append(torch.from_numpy(z[f"nms{i}_boxes"]).to(DEV))
+        sl.append(torch.from_numpy(z[f"nms{i}_scores"]).to(DEV))
+        want.append(z[f"nms{i}_keep"])
+    g = torch.Generator().manual_seed(9)
+    for n in (1, 65, 700, 4097):
+        b = torch.stack([10 * torch.rand(n, generator=g), 10 * torch.rand(n, generator=g),
+                         0.5 + 2 * torch.rand(n, generator=g), 0.5 + 2 * torch.rand(n, generator=g),
+                         torch.zeros(n)], 1)
+        s = torch.round(torch.rand(n, generator=g) * 8) / 8
+        bl.append(b.to(DEV))
+        sl.append(s.to(DEV))
+        want.append(O.nms_numpy(b.numpy(), s.numpy(), 0.2))
+    keeps = utils.nms_batched(bl, sl, 0.2)
+    for i, (k, w) in enumerate(zip(keeps, want)):
+        assert np.array_equal(k.cpu().numpy(), w), i
+
+
 def test_nms_random_vs_oracle():
     from oracle import ivit_oracle as O
     import utils

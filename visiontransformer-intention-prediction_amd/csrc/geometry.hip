@@ -168,6 +168,146 @@ __global__ __launch_bounds__(256) void nms_scan_kernel(const unsigned long long*
   if (threadIdx.x == 0) *count = cnt_s;
 }
 
+// ---- batched NMS: sample s owns rows seg[s] .. seg[s+1]-1 of every per-row array and the
+// mask words mask_off[s] .. ; blockIdx.y (rank / sorted boxes / scan) or blockIdx.z (mask)
+// selects the sample, so all samples' kernels run in one launch each (the single-workgroup
+// scan of one sample no longer serialises the batch).
+__global__ void nms_rank_b_kernel(const float* __restrict__ scores, const long* __restrict__ seg,
+                                  int* __restrict__ order) {
+  __shared__ float tile[256];
+  const int sm = blockIdx.y;
+  const long o = seg[sm], n = seg[sm + 1] - o;
+  if ((long)blockIdx.x * 256 >= n) return;
+  const float* s = scores + o;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const float si = i < n ? s[i] : 0.f;
+  long rank = 0;
+  for (long j0 = 0; j0 < n; j0 += 256) {
+    __syncthreads();
+    if (j0 + threadIdx.x < n) tile[threadIdx.x] = s[j0 + threadIdx.x];
+    __syncthreads();
+    const int lim = (int)min((long)256, n - j0);
+    for (int k = 0; k < lim; ++k) {
+      const float sj = tile[k];
+      const long j = j0 + k;
+      rank += (sj > si) || (sj == si && j < i);
+    }
+  }
+  if (i < n) order[o + rank] = (int)i;
+}
+
+__global__ void nms_sorted_boxes_b_kernel(const float* __restrict__ b, const int* __restrict__ order,
+                                          const long* __restrict__ seg, float* __restrict__ sb) {
+  const int sm = blockIdx.y;
+  const long o = seg[sm], n = seg[sm + 1] - o;
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const float* q = b + (o + order[o + p]) * 5;
+  const float x1 = q[0] - q[2] / 2.f, y1 = q[1] - q[3] / 2.f, x2 = q[0] + q[2] / 2.f, y2 = q[1] + q[3] / 2.f;
+  float* d = sb + (o + p) * 5;
+  d[0] = x1;
+  d[1] = y1;
+  d[2] = x2;
+  d[3] = y2;
+  d[4] = (x2 - x1) * (y2 - y1);
+}
+
+__global__ void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
+                                  const long* __restrict__ mask_off, double thr,
+                                  unsigned long long* __restrict__ mask_all) {
+  const int sm = blockIdx.z;
+  const long o = seg[sm], n = seg[sm + 1] - o;
+  const int nw = (int)((n + 63) / 64);
+  const int cb = blockIdx.x, rb = blockIdx.y;
+  if (cb >= nw || rb >= nw || cb < rb) return;
+  const float* sb = sb_all + o * 5;
+  unsigned long long* mask = mask_all + mask_off[sm];
+  __shared__ float cbx[64][5];
+  const int t = threadIdx.x;
+  const long cj = (long)cb * 64 + t;
+  if (cj < n)
+    for (int k = 0; k < 5; ++k) cbx[t][k] = sb[cj * 5 + k];
+  __syncthreads();
+  const long i = (long)rb * 64 + t;
+  if (i >= n) return;
+  const float ix1 = sb[i * 5 + 0], iy1 = sb[i * 5 + 1], ix2 = sb[i * 5 + 2], iy2 = sb[i * 5 + 3],
+              ia = sb[i * 5 + 4];
+  unsigned long long bits = 0;
+  const int lim = (int)min((long)64, n - (long)cb * 64);
+  for (int k = 0; k < lim; ++k) {
+    const long j = (long)cb * 64 + k;
+    if (j <= i) continue;
+    const float xx1 = fmaxf(ix1, cbx[k][0]), yy1 = fmaxf(iy1, cbx[k][1]);
+    const float xx2 = fminf(ix2, cbx[k][2]), yy2 = fminf(iy2, cbx[k][3]);
+    const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+    const float inter = w * h;
+    const float ovr = inter / ((ia + cbx[k][4]) - inter);
+    if ((double)ovr > thr) bits |= 1ull << k;
+  }
+  mask[i * nw + cb] = bits;
+}
+
+__global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long long* __restrict__ mask_all,
+                                                         const long* __restrict__ seg,
+                                                         const long* __restrict__ mask_off,
+                                                         const int* __restrict__ order_all,
+                                                         long* __restrict__ keep_all, long* __restrict__ count) {
+  const int sm = blockIdx.x;
+  const long o = seg[sm], n = seg[sm + 1] - o;
+  const int nw = (int)((n + 63) / 64);
+  const unsigned long long* mask = mask_all + mask_off[sm];
+  const int* order = order_all + o;
+  long* keep = keep_all + o;
+  __shared__ unsigned long long removed[NMS_MAXW];
+  __shared__ unsigned long long kept_s;
+  __shared__ long cnt_s;
+  for (int w = threadIdx.x; w < nw; w += 256) removed[w] = 0ull;
+  if (threadIdx.x == 0) cnt_s = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (int c = 0; c < nw; ++c) {
+    if (threadIdx.x < 64) {
+      const long row = (long)c * 64 + lane;
+      const unsigned long long diag = row < n ? mask[row * nw + c] : 0ull;
+      unsigned long long w = removed[c];
+      unsigned long long kept = 0ull;
+      const int lim = (int)min((long)64, n - (long)c * 64);
+      for (int i = 0; i < lim; ++i) {
+        const unsigned long long d = __shfl(diag, i, 64);
+        if (!((w >> i) & 1ull)) {
+          kept |= 1ull << i;
+          w |= d;
+        }
+      }
+      const long base = cnt_s;
+      if ((kept >> lane) & 1ull) {
+        const unsigned long long below = lane ? (kept & ((1ull << lane) - 1ull)) : 0ull;
+        keep[base + __popcll(below)] = order[row];
+      }
+      if (lane == 0) {
+        kept_s = kept;
+        cnt_s = base + __popcll(kept);
+      }
+    }
+    __syncthreads();
+    const unsigned long long kept = kept_s;
+    if (kept) {
+      for (int wc = c + 1 + threadIdx.x; wc < nw; wc += 256) {
+        unsigned long long acc = removed[wc];
+        unsigned long long kb = kept;
+        while (kb) {
+          const int i = __ffsll((long long)kb) - 1;
+          kb &= kb - 1;
+          acc |= mask[((long)c * 64 + i) * nw + wc];
+        }
+        removed[wc] = acc;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) count[sm] = cnt_s;
+}
+
 }  // namespace
 
 extern "C" int ivit_generate_anchors(long bev_h, long bev_w, long stride, const float* cfgs, long A, float voxel,
@@ -232,6 +372,41 @@ extern "C" int ivit_nms(const float* boxes_xywha, const float* scores, long n, d
   hipLaunchKernelGGL(nms_sorted_boxes_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, boxes_xywha, order, n, sb);
   hipLaunchKernelGGL(nms_mask_kernel, dim3(nw, nw), dim3(64), 0, st, sb, n, nw, iou_thr, mask);
   hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(256), 0, st, mask, n, nw, order, keep, count);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+// Batched torchvision-CPU-exact NMS (eval_vit.py:170 per sample, all samples in one launch per
+// stage). seg: [S+1] int64 row offsets (device); mask_off: [S] int64 word offsets of each
+// sample's [n_s, ceil(n_s/64)] suppression mask (device). keep[seg[s] ..] receives sample s's kept
+// LOCAL indices in score order, count[s] their number. Workspace (bytes) >= 24 * total + 8 *
+// mask_words + 64.
+extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, const long* seg, const long* mask_off,
+                                long n_samples, long total, long max_n, long mask_words, double iou_thr, long* keep,
+                                long* count, void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(max_n <= 64L * NMS_MAXW, "ivit_nms_batched: n=%ld exceeds %d", max_n, 64 * NMS_MAXW);
+  IVIT_CHECK_ARG(n_samples < 65536, "ivit_nms_batched: too many samples (%ld)", n_samples);
+  IVIT_CHECK_ARG(work_bytes >= 24 * total + 8 * mask_words + 64, "ivit_nms_batched: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  if (n_samples <= 0) return 0;
+  if (max_n <= 0) {
+    (void)hipMemsetAsync(count, 0, sizeof(long) * n_samples, st);
+    IVIT_LAUNCH_CHECK();
+    return 0;
+  }
+  const int nwmax = (int)((max_n + 63) / 64);
+  char* w = (char*)work;
+  int* order = (int*)w;
+  w += (total * 4 + 15) / 16 * 16;
+  float* sb = (float*)w;
+  w += (total * 20 + 15) / 16 * 16;
+  unsigned long long* mask = (unsigned long long*)w;
+  const int gx = ivit_cdiv(max_n, 256);
+  hipLaunchKernelGGL(nms_rank_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, scores, seg, order);
+  hipLaunchKernelGGL(nms_sorted_boxes_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, boxes_xywha, order, seg, sb);
+  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(nwmax, nwmax, n_samples), dim3(64), 0, st, sb, seg, mask_off, iou_thr,
+                     mask);
+  hipLaunchKernelGGL(nms_scan_b_kernel, dim3(n_samples), dim3(256), 0, st, mask, seg, mask_off, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -90,6 +90,31 @@ def apply_nms(boxes_xywha: torch.Tensor, scores: torch.Tensor, iou_threshold: fl
     return keep[: int(count.item())]
 
 
+def nms_batched(boxes_list, scores_list, iou_threshold: float = 0.2):
+    """apply_nms for every sample of a batch: one launch per NMS stage for all samples
+    (ivit_nms_batched) and one host read of the kept counts. Returns per-sample kept LOCAL
+    indices (int64 device tensors, descending-score order, torchvision CPU semantics)."""
+    ns = [int(b.shape[0]) for b in boxes_list]
+    S, total = len(ns), sum(ns)
+    dev = boxes_list[0].device if S else torch.device("cuda")
+    if total == 0:
+        return [torch.empty((0,), dtype=torch.long, device=dev) for _ in ns]
+    seg = np.concatenate([[0], np.cumsum(ns)]).astype(np.int64)
+    words = [n * ((n + 63) // 64) for n in ns]
+    moff = np.concatenate([[0], np.cumsum(words)[:-1]]).astype(np.int64)
+    b = torch.cat([x.float() for x in boxes_list]).contiguous()
+    sc = torch.cat([x.float() for x in scores_list]).contiguous()
+    d_seg = torch.from_numpy(seg).to(dev, non_blocking=True)
+    d_moff = torch.from_numpy(moff).to(dev, non_blocking=True)
+    keep = torch.empty((total,), dtype=torch.int64, device=dev)
+    count = torch.empty((S,), dtype=torch.int64, device=dev)
+    ws = workspace(24 * total + 8 * sum(words) + 64, dev)
+    lib.ivit_nms_batched(ptr(b), ptr(sc), ptr(d_seg), ptr(d_moff), S, total, max(ns), sum(words),
+                         float(iou_threshold), ptr(keep), ptr(count), ptr(ws), ws.numel(), stream())
+    cnt = count.cpu().tolist()
+    return [keep[seg[i]: seg[i] + cnt[i]] for i in range(S)]
+
+
 def postprocess_batch(cls_logits: torch.Tensor, box_preds_rel: torch.Tensor, intent_logits: torch.Tensor,
                       anchors: torch.Tensor, conf_threshold: float = 0.1, nms_threshold: float = 0.2):
     """eval_vit.py:157-180 for a whole batch: sigmoid → score >= conf → decode → NMS → argmax
@@ -99,18 +124,23 @@ def postprocess_batch(cls_logits: torch.Tensor, box_preds_rel: torch.Tensor, int
     scores = torch.sigmoid(cls_logits.reshape(B, -1).float())
     box = box_preds_rel.reshape(B, scores.shape[1], -1)
     it = intent_logits.reshape(B, scores.shape[1], -1)
-    out = []
+    idxs, sfs, decs = [], [], []
     for b in range(B):
         idx = torch.nonzero(scores[b] >= conf_threshold).squeeze(1)
-        res = {"pred_scores": scores.new_empty((0,)), "pred_boxes_xywha": scores.new_empty((0, 5)),
-               "pred_intentions": torch.empty((0,), dtype=torch.long, device=scores.device)}
-        if idx.numel() > 0:
-            sf = scores[b].index_select(0, idx)
-            dec = decode_box_predictions(box[b].index_select(0, idx), anchors.index_select(0, idx))
-            keep = apply_nms(dec, sf, nms_threshold)
-            if keep.numel() > 0:
-                res = {"pred_scores": sf[keep], "pred_boxes_xywha": dec[keep],
-                       "pred_intentions": torch.argmax(it[b].index_select(0, idx)[keep], dim=-1)}
+        idxs.append(idx)
+        sfs.append(scores[b].index_select(0, idx))
+        decs.append(decode_box_predictions(box[b].index_select(0, idx), anchors.index_select(0, idx))
+                    if idx.numel() > 0 else scores.new_empty((0, 5)))
+    keeps = nms_batched(decs, sfs, nms_threshold)  # all samples' NMS in one batched launch per stage
+    out = []
+    for b in range(B):
+        keep = keeps[b]
+        if keep.numel() > 0:
+            res = {"pred_scores": sfs[b][keep], "pred_boxes_xywha": decs[b][keep],
+                   "pred_intentions": torch.argmax(it[b].index_select(0, idxs[b])[keep], dim=-1)}
+        else:
+            res = {"pred_scores": scores.new_empty((0,)), "pred_boxes_xywha": scores.new_empty((0, 5)),
+                   "pred_intentions": torch.empty((0,), dtype=torch.long, device=scores.device)}
         out.append(res)
     return out
 
