@@ -398,8 +398,13 @@ class ViTBlockFn(torch.autograd.Function):
             o, lse = attn_fwd(qkv, B, N, H, cdt)
         x1, _ = linear_fwd(o, wp, pb, cdt, resid=x, row_scale=s1, rps=N)
         ln2, m2, r2 = layernorm_fwd(x1, n2w, n2b, eps, cd)
-        a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=True)
+        # inference (torch.inference_mode): nothing is saved, and fc1 skips its pre-activation copy
+        infer = torch.is_inference_mode_enabled()
+        a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=not infer)
         x2, _ = linear_fwd(a, w2, f2b, cdt, resid=x1, row_scale=s2, rps=N)
+        if infer:
+            ctx.meta, ctx.q2 = meta, q2
+            return x2
         ctx.save_for_backward(x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2)
         ctx.meta = meta
         ctx.q2 = q2
