@@ -221,6 +221,29 @@ int ivit_nms_batched(const float* boxes_xywha, const float* scores, const long* 
                      long n_samples, long total, long max_n, long mask_words, double iou_thr, long* keep,
                      long* count, void* work, long work_bytes, void* stream);
 
+/* ---- BEV augmentation passes ----------------------------------------
+ * Replaces the raster side of utils.augment_bev (utils.py:500-517): random_flip_bev's np.flip
+ * (:399-401), random_rotate_bev's per-channel cv2.warpAffine (:425-438), random_scale_bev's
+ * per-channel cv2.resize + centre crop / pad (:455-474) and random_bev_dropout's rectangles
+ * (:483-493). passes: device array of n_passes ivit_bev_pass entries (192 B each); entry i reads
+ * the [C, H, W] f32 stack at src and writes the one at dst (distinct buffers). All stacks share
+ * H x W; max_planes >= every entry's C (C = 0 skips the entry). The caller draws the random
+ * parameters (python `random`, the reference's order) and chains passes: flip is fused into
+ * the first pass's reads, the dropout rectangles into the last pass's writes.               */
+typedef struct ivit_bev_pass {
+  unsigned long long src, dst; /* device addresses of plane 0; plane stride H * W floats */
+  int C;                       /* planes (0 = skip) */
+  int op;                      /* 0 copy, 1 warpAffine INTER_LINEAR / BORDER_CONSTANT 0, 2 resize + crop / pad */
+  int flip;                    /* read source columns mirrored (np.flip(axis=2) fused) */
+  int n_rect;                  /* dropout rectangles zeroed in the output, 0..5 */
+  double m[6];                 /* op 1: the INVERTED 2x3 map dst -> src, as warpAffine inverts M */
+  double scale_x, scale_y;     /* op 2: 1 / (new_w / W), 1 / (new_h / H) */
+  int new_w, new_h;            /* op 2: resized size (int(W s), int(H s)) */
+  int off_x, off_y;            /* op 2: out(y, x) = resized(y + off_y, x + off_x), zero outside */
+  int rect[5][4];              /* y0, x0, h, w */
+} ivit_bev_pass;
+int ivit_bev_augment(const void* passes, long n_passes, long H, long W, long max_planes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

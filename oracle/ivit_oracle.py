@@ -456,3 +456,209 @@ def lidar_bev_np(points_list, intensity_list, num_sweeps=SWEEPS, H=BEV_H, W=BEV_
         flat = ((i * HEIGHT_CH + hz) * H + py[ok]) * W + px[ok]
         np.maximum.at(bev.reshape(-1), flat, v[ok].astype(np.float32))  # utils.py:99-104 (order-free max)
     return bev
+
+
+# --------------------------------------------------------------------------------------
+# BEV augmentations (utils.py:394-517)
+# --------------------------------------------------------------------------------------
+# cv2 is absent from this image, so the two OpenCV resamplers the reference calls are restated
+# from OpenCV's long-standing generic scalar paths (imgwarp.cpp getRotationMatrix2D /
+# WarpAffineInvoker / remapBilinear, resize.cpp resizeGeneric HResizeLinear / VResizeLinear, as
+# in 3.x-4.10) for single-channel f32 planes: every product / sum rounds to f32 on its own (no
+# fused multiply-add; SIMD-dispatched OpenCV builds may fuse and differ by an ulp).
+# PARITY UNPINNED for that resampling arithmetic. The flow around it (random draw order,
+# crop / pad offsets, dropout rectangles, GT box and intention updates) is pinned: make_golden.py
+# runs the reference's OWN random_* / augment_bev with these functions as its cv2 stand-in.
+import random as _random  # noqa: E402
+
+_INTER_BITS, _INTER_TAB, _AB_BITS = 5, 32, 10
+
+
+def cv2_get_rotation_matrix_2d(center, angle_deg, scale):
+    """getRotationMatrix2D (f64): [[a, b, (1-a)cx - b cy], [-b, a, b cx + (1-a)cy]]; the centre is a
+    Point2f, so it is rounded to f32 first."""
+    ang = angle_deg * (math.pi / 180)
+    a, b = math.cos(ang) * scale, math.sin(ang) * scale
+    cx, cy = float(np.float32(center[0])), float(np.float32(center[1]))
+    return np.array([[a, b, (1 - a) * cx - b * cy], [-b, a, b * cx + (1 - a) * cy]], dtype=np.float64)
+
+
+def cv2_invert_affine(M):
+    """warpAffine without WARP_INVERSE_MAP inverts M in f64 (dst -> src map), in this order."""
+    m = [float(v) for v in np.asarray(M, np.float64).reshape(6)]
+    D = m[0] * m[4] - m[1] * m[3]
+    D = 1.0 / D if D != 0 else 0.0
+    a11, a22 = m[4] * D, m[0] * D
+    m[0] = a11
+    m[1] *= -D
+    m[3] *= -D
+    m[4] = a22
+    b1 = -m[0] * m[2] - m[1] * m[5]
+    b2 = -m[3] * m[2] - m[4] * m[5]
+    m[2], m[5] = b1, b2
+    return m
+
+
+def _sat_i16(v):
+    return np.clip(v, -32768, 32767)
+
+
+def cv2_warp_affine_linear(img, M, dsize, flip_src=False):
+    """cv2.warpAffine(img, M, dsize, INTER_LINEAR, BORDER_CONSTANT, 0) for one f32 plane (or a
+    [C, H, W] stack, same map per plane). Source coordinates in 1/32-pixel fixed point:
+    X = (round((m1 y + m2) 1024) + 16 + round(m0 x 1024)) >> 5 (round = half-to-even), tap
+    (X >> 5, Y >> 5), weights from the exact 32x32 bilinear table; taps outside the image read 0.
+    flip_src mirrors the source columns first (np.flip(axis=-1), fused)."""
+    src = np.asarray(img, np.float32)
+    Hs, Ws = src.shape[-2:]
+    Wd, Hd = int(dsize[0]), int(dsize[1])
+    m = cv2_invert_affine(M)
+    xs, ys = np.arange(Wd, dtype=np.float64), np.arange(Hd, dtype=np.float64)
+    adelta = np.rint(m[0] * xs * 1024.0).astype(np.int64)
+    bdelta = np.rint(m[3] * xs * 1024.0).astype(np.int64)
+    rd = (1 << _AB_BITS) // _INTER_TAB // 2
+    X0 = np.rint((m[1] * ys + m[2]) * 1024.0).astype(np.int64) + rd
+    Y0 = np.rint((m[4] * ys + m[5]) * 1024.0).astype(np.int64) + rd
+    X = (X0[:, None] + adelta[None, :]) >> (_AB_BITS - _INTER_BITS)
+    Y = (Y0[:, None] + bdelta[None, :]) >> (_AB_BITS - _INTER_BITS)
+    sx, sy = _sat_i16(X >> _INTER_BITS), _sat_i16(Y >> _INTER_BITS)
+    tx = (X & (_INTER_TAB - 1)).astype(np.float32) * np.float32(1.0 / _INTER_TAB)
+    ty = (Y & (_INTER_TAB - 1)).astype(np.float32) * np.float32(1.0 / _INTER_TAB)
+    one = np.float32(1.0)
+    w = [(one - ty) * (one - tx), (one - ty) * tx, ty * (one - tx), ty * tx]
+    flat = src.reshape(-1, Hs * Ws)
+    out = np.zeros((flat.shape[0], Hd, Wd), np.float32)
+    acc = None
+    for k, (dy, dx) in enumerate(((0, 0), (0, 1), (1, 0), (1, 1))):
+        cx, cy = sx + dx, sy + dy
+        ok = (cx >= 0) & (cx < Ws) & (cy >= 0) & (cy < Hs)
+        col = (Ws - 1 - cx) if flip_src else cx
+        idx = np.where(ok, cy * Ws + col, 0)
+        v = np.where(ok[None], flat[:, idx], np.float32(0.0))
+        term = v * w[k][None]
+        acc = term if acc is None else acc + term
+    out[:] = acc
+    return out.reshape(src.shape[:-2] + (Hd, Wd))
+
+
+def _resize_axis(n_dst, n_src, scale):
+    """resizeGeneric's per-axis source index / weights (INTER_LINEAR, f32 data)."""
+    f = ((np.arange(n_dst, dtype=np.float64) + 0.5) * scale - 0.5).astype(np.float32)
+    s = np.floor(f).astype(np.int64)
+    f = f - s.astype(np.float32)
+    lo = s < 0
+    f[lo], s[lo] = 0, 0
+    hi = s >= n_src - 1  # also xmax: HResizeLinear copies S[sx] from here on
+    f[hi], s[hi] = 0, n_src - 1
+    return s, np.float32(1.0) - f, f, hi
+
+
+def cv2_resize_linear(img, dsize, flip_src=False):
+    """cv2.resize(img, dsize, interpolation=INTER_LINEAR) for f32 planes ([.., H, W]): horizontal
+    pass h = S[sx] a0 + S[sx+1] a1 (S[sx] alone at the right clamp), then vertical
+    h[r0] b0 + h[r1] b1 with clipped rows; scale = 1 / (dst / src) in f64; same size -> copy."""
+    src = np.asarray(img, np.float32)
+    if flip_src:
+        src = src[..., ::-1]
+    Hs, Ws = src.shape[-2:]
+    Wd, Hd = int(dsize[0]), int(dsize[1])
+    if (Wd, Hd) == (Ws, Hs):
+        return src.copy()
+    sx, a0, a1, copy = _resize_axis(Wd, Ws, 1.0 / (Wd / Ws))
+    sy, b0, b1, _ = _resize_axis(Hd, Hs, 1.0 / (Hd / Hs))
+    sx1 = np.minimum(sx + 1, Ws - 1)
+    h = np.where(copy, src[..., sx], src[..., sx] * a0 + src[..., sx1] * a1)  # [.., Hs, Wd]
+    r1 = np.minimum(sy + 1, Hs - 1)
+    return (h[..., sy, :] * b0[:, None] + h[..., r1, :] * b1[:, None]).astype(np.float32)
+
+
+def resize_crop_pad(img, scale_factor, H=BEV_H, W=BEV_W, flip_src=False):
+    """random_scale_bev's per-channel body (utils.py:460-474): resize to int(H s) x int(W s), then
+    centre-crop (s > 1) or centre-pad with zeros (s <= 1) back to H x W."""
+    new_h, new_w = int(H * scale_factor), int(W * scale_factor)
+    r = cv2_resize_linear(img, (new_w, new_h), flip_src=flip_src)
+    out = np.zeros(np.asarray(img).shape[:-2] + (H, W), np.float32)
+    if scale_factor > 1.0:
+        h0, w0 = (new_h - H) // 2, (new_w - W) // 2
+        out[...] = r[..., h0:h0 + H, w0:w0 + W]
+    else:
+        h0, w0 = (H - new_h) // 2, (W - new_w) // 2
+        out[..., h0:h0 + new_h, w0:w0 + new_w] = r
+    return out
+
+
+FLIP_INTENTION = np.array([0, 2, 1, 4, 3, 5, 6, 7], np.int64)  # utils.py:406-411 (constants.py:64-67)
+
+
+def draw_augment_params(rng=_random, H=BEV_H, W=BEV_W):
+    """The random draws of augment_bev (utils.py:500-511) in the reference's order: flip (:399),
+    rotate (:422-423), scale (:451-452), dropout (:484-490)."""
+    p = {"flip": rng.random() < 0.5, "angle": None, "scale": None, "rects": []}
+    if rng.random() < 0.5:
+        p["angle"] = rng.uniform(-15.0, 15.0)
+    if rng.random() < 0.5:
+        p["scale"] = rng.uniform(0.95, 1.05)
+    if rng.random() < 0.1:
+        for _ in range(rng.randint(1, 5)):
+            ph, pw = rng.randint(20, 50), rng.randint(20, 50)
+            p["rects"].append((rng.randint(0, max(0, H - ph)), rng.randint(0, max(0, W - pw)), ph, pw))
+    return p
+
+
+def augment_gt_np(boxes, intents, p):
+    """GT updates of random_flip / rotate / scale_bev (utils.py:402-411, 440-447, 476-477)."""
+    boxes = np.array(boxes, dtype=np.float32, copy=True)
+    intents = np.array(intents, dtype=np.int64, copy=True)
+    if p["flip"]:
+        if boxes.shape[0] > 0:
+            boxes[:, 1] *= -1
+            boxes[:, 4] *= -1
+            boxes[:, 4] = np.arctan2(np.sin(boxes[:, 4]), np.cos(boxes[:, 4]))
+        if intents.shape[0] > 0:
+            intents = FLIP_INTENTION[intents]
+    if p["angle"] is not None and boxes.shape[0] > 0:
+        rad = np.radians(p["angle"])
+        cx, cy = boxes[:, 0].copy(), boxes[:, 1].copy()
+        c, s = np.cos(rad), np.sin(rad)
+        boxes[:, 0], boxes[:, 1] = cx * c - cy * s, cx * s + cy * c
+        boxes[:, 4] += rad
+        boxes[:, 4] = np.arctan2(np.sin(boxes[:, 4]), np.cos(boxes[:, 4]))
+    if p["scale"] is not None and boxes.shape[0] > 0:
+        boxes[:, :4] *= p["scale"]
+    return boxes, intents
+
+
+def augment_planes_np(x, p, H=BEV_H, W=BEV_W):
+    """The raster side of augment_bev on one [C, H, W] f32 stack with drawn params p."""
+    y = np.array(x, np.float32, copy=True)
+    if p["flip"]:
+        y = np.ascontiguousarray(y[..., ::-1])
+    if p["angle"] is not None:
+        M = cv2_get_rotation_matrix_2d((W / 2.0, H / 2.0), p["angle"], 1.0)
+        y = cv2_warp_affine_linear(y, M, (W, H))
+    if p["scale"] is not None:
+        y = resize_crop_pad(y, p["scale"], H, W)
+    for y0, x0, ph, pw in p["rects"]:
+        y[..., y0:y0 + ph, x0:x0 + pw] = 0.0
+    return y
+
+
+def augment_bev_np(lidar, map_bev, boxes, intents, rng=_random):
+    """utils.augment_bev (utils.py:500-517) restated: -> (lidar, map, boxes, intents, params)."""
+    p = draw_augment_params(rng, *np.asarray(lidar).shape[-2:])
+    H, W = np.asarray(lidar).shape[-2:]
+    b, i = augment_gt_np(boxes, intents, p)
+    return augment_planes_np(lidar, p, H, W), augment_planes_np(map_bev, p, H, W), b, i, p
+
+
+def bev_augment_inputs(seed, lidar_ch=3, map_ch=2, G=20, H=BEV_H, W=BEV_W):
+    """Seeded BEV-like planes + GT for the augmentation fixtures (regenerated on the GPU box):
+    sparse lidar intensities in [0, 255), Bernoulli(0.1) map, G boxes as in bench's synthetic GT."""
+    rng = np.random.default_rng(seed)
+    lidar = (rng.random((lidar_ch, H, W), dtype=np.float32) * np.float32(255.0))
+    lidar *= (rng.random((lidar_ch, H, W)) < 0.3)
+    mp = (rng.random((map_ch, H, W)) < 0.1).astype(np.float32)
+    boxes = np.stack([rng.uniform(-20, 60, G), rng.uniform(-72, 72, G), rng.uniform(1.5, 3.0, G),
+                      rng.uniform(3.5, 6.5, G), rng.uniform(-math.pi, math.pi, G)], 1).astype(np.float32)
+    intents = rng.integers(0, 8, G).astype(np.int64)
+    return lidar, mp, boxes, intents

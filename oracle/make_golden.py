@@ -259,6 +259,60 @@ def gen_lidar_bev():
           "NaN cells", int(np.isnan(rec["b_val"]).sum()))
 
 
+def gen_bev_augment():
+    """utils.augment_bev (utils.py:394-517): the reference's OWN flow (random draws, flip, rotate /
+    scale per channel through cv2, crop / pad, dropout, GT updates) with cv2 backed by the oracle's
+    OpenCV restatement (refshim). Per case: the python `random` seed, the drawn params, sha256 of
+    the output rasters (+ a strided sample) and the GT outputs. Cases are chosen to cover every
+    branch: none, flip only, rotate, scale up (crop), scale down (pad), rotate + scale, dropout."""
+    import hashlib
+    import random
+    import torch as _t
+    import utils as ref_utils
+    want = {"none": lambda p: not p["flip"] and p["angle"] is None and p["scale"] is None and not p["rects"],
+            "flip": lambda p: p["flip"] and p["angle"] is None and p["scale"] is None and not p["rects"],
+            "rotate": lambda p: p["angle"] is not None and p["scale"] is None,
+            "scale_up": lambda p: p["angle"] is None and p["scale"] is not None and p["scale"] > 1.0,
+            "scale_down": lambda p: p["angle"] is None and p["scale"] is not None and p["scale"] <= 1.0,
+            "rotate_scale_flip": lambda p: p["flip"] and p["angle"] is not None and p["scale"] is not None,
+            "dropout": lambda p: len(p["rects"]) >= 2,
+            "all": lambda p: p["flip"] and p["angle"] is not None and p["scale"] is not None and p["rects"]}
+    seeds = {}
+    for s in range(5000):
+        random.seed(s)
+        p = O.draw_augment_params(random)
+        for k, f in want.items():
+            if k not in seeds and f(p):
+                seeds[k] = s
+        if len(seeds) == len(want):
+            break
+    assert len(seeds) == len(want), seeds
+    rec = {"cases": np.array(list(want))}
+    for ci, (k, s) in enumerate(seeds.items()):
+        lidar, mp, boxes, intents = O.bev_augment_inputs(100 + ci)
+        random.seed(s)
+        rl, rm, rg = ref_utils.augment_bev(lidar, mp, {"boxes_xywha": _t.from_numpy(boxes.copy()),
+                                                       "intentions": _t.from_numpy(intents.copy())})
+        random.seed(s)
+        ol, om, ob, oi, p = O.augment_bev_np(lidar, mp, boxes, intents, random)
+        assert np.array_equal(rl, ol) and np.array_equal(rm, om), f"oracle != reference rasters ({k})"
+        assert np.array_equal(rg["boxes_xywha"].numpy(), ob) and np.array_equal(rg["intentions"].numpy(), oi), k
+        rects = np.zeros((5, 4), np.int64)
+        if p["rects"]:
+            rects[:len(p["rects"])] = p["rects"]
+        rec.update({f"{k}_seed": np.int64(s), f"{k}_input_seed": np.int64(100 + ci), f"{k}_flip": np.int64(p["flip"]),
+                    f"{k}_angle": np.float64(np.nan if p["angle"] is None else p["angle"]),
+                    f"{k}_scale": np.float64(np.nan if p["scale"] is None else p["scale"]),
+                    f"{k}_nrect": np.int64(len(p["rects"])), f"{k}_rects": rects,
+                    f"{k}_lidar_sha": np.array(hashlib.sha256(np.ascontiguousarray(rl).tobytes()).hexdigest()),
+                    f"{k}_map_sha": np.array(hashlib.sha256(np.ascontiguousarray(rm).tobytes()).hexdigest()),
+                    f"{k}_lidar_sample": np.ascontiguousarray(rl).reshape(-1)[::997].copy(),
+                    f"{k}_map_sample": np.ascontiguousarray(rm).reshape(-1)[::997].copy(),
+                    f"{k}_boxes": rg["boxes_xywha"].numpy(), f"{k}_intents": rg["intentions"].numpy()})
+        print("bev_augment", k, "seed", s, {kk: v for kk, v in p.items() if kk != "rects"}, "rects", len(p["rects"]))
+    np.savez_compressed(os.path.join(OUT, "bev_augment.npz"), **rec)
+
+
 def cross_check_vit():
     """HF ViTModel (stand-in) vs the oracle's timm restatement, 12 blocks, real widths."""
     cfg = model_cfg(img_size=SMALL_IMG)
@@ -290,3 +344,4 @@ if __name__ == "__main__":
     gen_model_small()
     gen_geometry()
     gen_lidar_bev()
+    gen_bev_augment()

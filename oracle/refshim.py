@@ -13,7 +13,9 @@ calls:
   published source (unpinned, README.md:115); ``nms`` follows the CPU kernel.
 * ``shapely.geometry.Polygon``: convex-polygon area/intersection in float64
   (GEOS restated for the convex rectangles ``utils.py:295-332`` builds).
-* ``cv2``: empty module (only BEV rasterisation/augmentation use it — out of scope).
+* ``cv2``: ``getRotationMatrix2D`` / ``warpAffine`` / ``resize`` (INTER_LINEAR, BORDER_CONSTANT) backed
+  by ``ivit_oracle``'s restatement of OpenCV's generic paths, so the reference's BEV augmentation
+  flow (utils.py:394-517) runs here; the resampling arithmetic itself is parity unpinned.
 """
 from __future__ import annotations
 
@@ -189,6 +191,18 @@ def install(reference_dir="/root/reference"):
     ops.nms = _nms
     tv.ops = ops
     cv2 = types.ModuleType("cv2")
+    from oracle import ivit_oracle as _O
+    cv2.INTER_LINEAR, cv2.BORDER_CONSTANT = 1, 0
+    cv2.getRotationMatrix2D = _O.cv2_get_rotation_matrix_2d
+
+    def _warp(src, M, dsize, flags=1, borderMode=0, borderValue=0):
+        assert flags == 1 and borderMode == 0 and borderValue == 0, "stand-in: INTER_LINEAR / BORDER_CONSTANT 0"
+        return _O.cv2_warp_affine_linear(src, M, dsize)
+
+    def _resize(src, dsize, interpolation=1):
+        assert interpolation == 1, "stand-in: INTER_LINEAR only"
+        return _O.cv2_resize_linear(src, dsize)
+    cv2.warpAffine, cv2.resize = _warp, _resize
     shp = types.ModuleType("shapely")
     geom = types.ModuleType("shapely.geometry")
     geom.Polygon = _Polygon

@@ -88,3 +88,143 @@ extern "C" int ivit_lidar_bev(const void* points, int points_f64, long ld, const
   IVIT_LAUNCH_CHECK();
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------
+// BEV augmentation passes (utils.py:394-517). One launch runs one pass
+// for every [C, H, W] stack of a batch (LiDAR and map stacks of all samples; blockIdx.z =
+// pass entry). Each thread owns one output pixel: it derives its source taps and weights once
+// (the same for every plane) and then streams CPB planes, so the map arithmetic is amortised
+// and the pass is a read + write of the stack (HBM-bound). Tiles are 64 x 4 pixels, so the row
+// below a tile's last row is the only extra source row it touches.
+//   op 0: copy (np.flip / dropout only), op 1: cv2.warpAffine INTER_LINEAR BORDER_CONSTANT 0
+//   (1/32-pixel fixed-point source coordinates, exact bilinear table), op 2: cv2.resize
+//   INTER_LINEAR to (new_w, new_h) then the centre crop / zero pad of random_scale_bev.
+// The f32 sums keep OpenCV's scalar order, unfused (fp contract off above); the oracle
+// (oracle/ivit_oracle.py cv2_*) restates the same arithmetic.
+namespace {
+
+struct BevPass {
+  unsigned long long src, dst;
+  int C, op, flip, n_rect;
+  double m[6];
+  double scale_x, scale_y;
+  int new_w, new_h, off_x, off_y;
+  int rect[5][4];
+};
+static_assert(sizeof(BevPass) == 192, "ivit_bev_pass layout");
+
+constexpr int kBevTileW = 64, kBevTileH = 4, kBevCPB = 8;
+
+// resizeGeneric's per-axis source index and weights (f32 data): the f64 source position is
+// rounded to f32, floored, clamped at both ends (weight 0), and from sx >= n - 1 on the
+// horizontal pass copies S[sx] instead of interpolating.
+IVIT_DEV void resize_axis(int d, int n_src, double scale, int& s0, int& s1, float& a0, float& a1, bool& copy) {
+  float f = (float)(((double)d + 0.5) * scale - 0.5);
+  int s = (int)floorf(f);
+  f = f - (float)s;
+  if (s < 0) { f = 0.f; s = 0; }
+  copy = s >= n_src - 1;
+  if (copy) { f = 0.f; s = n_src - 1; }
+  s0 = s;
+  s1 = min(s + 1, n_src - 1);
+  a0 = 1.f - f;
+  a1 = f;
+}
+
+__global__ __launch_bounds__(256) void bev_pass_kernel(const BevPass* __restrict__ passes, int H, int W) {
+  const BevPass& P = passes[blockIdx.z];
+  const int C = P.C;
+  const int c0 = blockIdx.y * kBevCPB;
+  if (c0 >= C) return;
+  const int tiles_w = (W + kBevTileW - 1) / kBevTileW;
+  const int x = (blockIdx.x % tiles_w) * kBevTileW + (threadIdx.x & (kBevTileW - 1));
+  const int y = (blockIdx.x / tiles_w) * kBevTileH + threadIdx.x / kBevTileW;
+  if (x >= W || y >= H) return;
+  const long HW = (long)H * W;
+  const float* __restrict__ src = reinterpret_cast<const float*>(P.src) + (long)c0 * HW;
+  float* __restrict__ dst = reinterpret_cast<float*>(P.dst) + (long)c0 * HW + (long)y * W + x;
+  const int cn = min(kBevCPB, C - c0);
+
+  bool zero = false;
+  for (int r = 0; r < P.n_rect; ++r)
+    zero |= y >= P.rect[r][0] && y < P.rect[r][0] + P.rect[r][2] && x >= P.rect[r][1] && x < P.rect[r][1] + P.rect[r][3];
+  const int op = P.op;
+  if (!zero && op == 2) {
+    const int ry = y + P.off_y, rx = x + P.off_x;
+    zero = ry < 0 || ry >= P.new_h || rx < 0 || rx >= P.new_w;
+  }
+  if (zero) {
+    for (int c = 0; c < cn; ++c) dst[c * HW] = 0.f;
+    return;
+  }
+  auto col = [&](int c) { return P.flip ? W - 1 - c : c; };
+  if (op == 0) {
+    const float* s = src + (long)y * W + col(x);
+#pragma unroll
+    for (int c = 0; c < kBevCPB; ++c)
+      if (c < cn) dst[c * HW] = s[c * HW];
+    return;
+  }
+  if (op == 1) {
+    const double* m = P.m;
+    const int rd = (1 << 10) / 32 / 2;
+    const int adx = (int)rint(m[0] * (double)x * 1024.0), bdx = (int)rint(m[3] * (double)x * 1024.0);
+    const int X0 = (int)rint((m[1] * (double)y + m[2]) * 1024.0) + rd;
+    const int Y0 = (int)rint((m[4] * (double)y + m[5]) * 1024.0) + rd;
+    const int X = (X0 + adx) >> 5, Y = (Y0 + bdx) >> 5;
+    const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
+    const float tx = (float)(X & 31) * (1.f / 32.f), ty = (float)(Y & 31) * (1.f / 32.f);
+    const float w[4] = {(1.f - ty) * (1.f - tx), (1.f - ty) * tx, ty * (1.f - tx), ty * tx};
+    long idx[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cx = sx + (k & 1), cy = sy + (k >> 1);
+      ok[k] = cx >= 0 && cx < W && cy >= 0 && cy < H;
+      idx[k] = ok[k] ? (long)cy * W + col(cx) : 0;
+    }
+#pragma unroll
+    for (int c = 0; c < kBevCPB; ++c) {
+      if (c < cn) {
+        const float* s = src + c * HW;
+        const float v0 = ok[0] ? s[idx[0]] : 0.f, v1 = ok[1] ? s[idx[1]] : 0.f;
+        const float v2 = ok[2] ? s[idx[2]] : 0.f, v3 = ok[3] ? s[idx[3]] : 0.f;
+        dst[c * HW] = ((v0 * w[0] + v1 * w[1]) + v2 * w[2]) + v3 * w[3];
+      }
+    }
+    return;
+  }
+  // op 2: resize (then centre crop / pad: out(y, x) = resized(y + off_y, x + off_x))
+  int sx0, sx1, sy0, sy1;
+  float a0, a1, b0, b1;
+  bool cpx, cpy;
+  resize_axis(x + P.off_x, W, P.scale_x, sx0, sx1, a0, a1, cpx);
+  resize_axis(y + P.off_y, H, P.scale_y, sy0, sy1, b0, b1, cpy);
+  const long i00 = (long)sy0 * W + col(sx0), i01 = (long)sy0 * W + col(sx1);
+  const long i10 = (long)sy1 * W + col(sx0), i11 = (long)sy1 * W + col(sx1);
+#pragma unroll
+  for (int c = 0; c < kBevCPB; ++c) {
+    if (c < cn) {
+      const float* s = src + c * HW;
+      const float h0 = cpx ? s[i00] : s[i00] * a0 + s[i01] * a1;
+      const float h1 = cpx ? s[i10] : s[i10] * a0 + s[i11] * a1;
+      dst[c * HW] = h0 * b0 + h1 * b1;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int ivit_bev_augment(const void* passes, long n_passes, long H, long W, long max_planes, void* stream) {
+  if (n_passes <= 0 || max_planes <= 0) return 0;
+  IVIT_CHECK_ARG(passes != nullptr, "ivit_bev_augment: null pass table");
+  IVIT_CHECK_ARG(n_passes < 65536, "ivit_bev_augment: too many passes (%ld)", n_passes);
+  IVIT_CHECK_ARG(H > 1 && W > 1 && H * W < (1L << 31) && H < 32768 && W < 32768,
+                 "ivit_bev_augment: bad plane size %ldx%ld", H, W);
+  const long tiles = ivit_cdiv(W, kBevTileW) * ivit_cdiv(H, kBevTileH);
+  dim3 g((unsigned)tiles, (unsigned)ivit_cdiv(max_planes, kBevCPB), (unsigned)n_passes);
+  hipLaunchKernelGGL(bev_pass_kernel, g, dim3(256), 0, ivit_stream(stream), (const BevPass*)passes, (int)H,
+                     (int)W);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}

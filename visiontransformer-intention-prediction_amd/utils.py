@@ -1,15 +1,18 @@
 """Box geometry of the reference's utils.py (anchors, axis/rotated IoU, decode, NMS, AP) and
 the LiDAR BEV voxelisation with its sweep ego transform (utils.py:27-33, 62-106; SURVEY.md §8f
-rank 1) on the MI355X kernels. Map rasterisation and augmentations (utils.py:108-225, 394-517)
-belong to the Argoverse-2 data pipeline, which is outside this build's scope."""
+rank 1) and the BEV augmentations (utils.py:394-517; §8f rank 3) on the MI355X kernels. Map
+rasterisation (utils.py:108-225) belongs to the Argoverse-2 data pipeline, outside this build."""
 from __future__ import annotations
+
+import math
+import random
 
 import numpy as np
 import torch
 
 from _lib import lib, ptr, stream, workspace
 from constants import (ANCHOR_CONFIGS_PAPER, BEV_PIXEL_OFFSET_X, BEV_PIXEL_OFFSET_Y, GRID_HEIGHT_PX, GRID_WIDTH_PX,
-                       LIDAR_HEIGHT_CHANNELS, LIDAR_SWEEPS, VOXEL_SIZE_M, Z_MAX, Z_MIN)
+                       INTENTIONS_MAP, LIDAR_HEIGHT_CHANNELS, LIDAR_SWEEPS, VOXEL_SIZE_M, Z_MAX, Z_MIN)
 
 
 def _dev(device):
@@ -244,3 +247,227 @@ def create_intentnet_lidar_bev(points_list, intensity_list, num_expected_sweeps:
     reference returns the same raster as a numpy array). transforms (optional): per-sweep 4x4
     rel_tf, fusing dataset.py:340's transform_points into the same kernel."""
     return lidar_bev_batch([(points_list, intensity_list, transforms)], num_expected_sweeps, device=device)[0]
+
+
+# ------------------------------------------------------------------ BEV augmentations (§8f rank 3)
+# The raster work runs as ivit_bev_augment passes (csrc/bev.hip): every stack of a batch in one
+# launch per pass, the flip fused into the first pass's reads and the dropout rectangles into the
+# last pass's writes (rotate + scale = 2 passes, anything else = 1). The random draws stay on the
+# host in python `random`, in the reference's order, so a seeded run makes the reference's
+# decisions; the GT updates (<= a few dozen boxes) stay host numpy as in the reference.
+_BEV_PASS = np.dtype([("src", "<u8"), ("dst", "<u8"), ("C", "<i4"), ("op", "<i4"), ("flip", "<i4"),
+                      ("n_rect", "<i4"), ("m", "<f8", (6,)), ("scale_x", "<f8"), ("scale_y", "<f8"),
+                      ("new_w", "<i4"), ("new_h", "<i4"), ("off_x", "<i4"), ("off_y", "<i4"),
+                      ("rect", "<i4", (5, 4))])
+assert _BEV_PASS.itemsize == 192  # ivit_bev_pass (include/ivit.h)
+_FLIP_INTENTION = np.arange(8, dtype=np.int64)
+for _a, _b in (("TURN_LEFT", "TURN_RIGHT"), ("LEFT_CHANGE_LANE", "RIGHT_CHANGE_LANE")):  # utils.py:406-411
+    _FLIP_INTENTION[INTENTIONS_MAP[_a]], _FLIP_INTENTION[INTENTIONS_MAP[_b]] = INTENTIONS_MAP[_b], INTENTIONS_MAP[_a]
+
+
+def _rotation_inverse(angle_deg, H, W):
+    """cv2.getRotationMatrix2D((W/2, H/2), angle, 1) (utils.py:429), inverted in f64 the way
+    warpAffine inverts a forward map (dst -> src), as the 6 doubles of ivit_bev_pass.m."""
+    ang = angle_deg * (math.pi / 180)
+    a, b = math.cos(ang), math.sin(ang)
+    cx, cy = float(np.float32(W / 2.0)), float(np.float32(H / 2.0))
+    m = [a, b, (1 - a) * cx - b * cy, -b, a, b * cx + (1 - a) * cy]
+    d = m[0] * m[4] - m[1] * m[3]
+    d = 1.0 / d if d != 0 else 0.0
+    m[0], m[4] = m[4] * d, m[0] * d
+    m[1] *= -d
+    m[3] *= -d
+    m[2], m[5] = -m[0] * m[2] - m[1] * m[5], -m[3] * m[2] - m[4] * m[5]
+    return m
+
+
+def _draw_params(flip=True, rotate=True, scale=True, dropout=True, angle_range_deg=(-15.0, 15.0),
+                 scale_range=(0.95, 1.05), dropout_prob=0.1, patch_size_range=(20, 50), num_patches_range=(1, 5),
+                 H=GRID_HEIGHT_PX, W=GRID_WIDTH_PX):
+    """One sample's draws from python `random`, in the order of utils.py:399, 422-423, 451-452, 484-490."""
+    p = {"flip": False, "angle": None, "scale": None, "rects": []}
+    if flip:
+        p["flip"] = random.random() < 0.5
+    if rotate and random.random() < 0.5:
+        p["angle"] = random.uniform(angle_range_deg[0], angle_range_deg[1])
+    if scale and random.random() < 0.5:
+        p["scale"] = random.uniform(scale_range[0], scale_range[1])
+    if dropout and random.random() < dropout_prob:
+        for _ in range(random.randint(num_patches_range[0], num_patches_range[1])):
+            ph = random.randint(patch_size_range[0], patch_size_range[1])
+            pw = random.randint(patch_size_range[0], patch_size_range[1])
+            p["rects"].append((random.randint(0, max(0, H - ph)), random.randint(0, max(0, W - pw)), ph, pw))
+    return p
+
+
+def _stages(p, H, W):
+    """The passes one stack needs for params p: [(op, fields)]; flip goes on the first, rects on the last."""
+    st = []
+    if p["angle"] is not None:
+        st.append((1, {"m": _rotation_inverse(p["angle"], H, W)}))
+    if p["scale"] is not None:
+        s = p["scale"]
+        nh, nw = int(H * s), int(W * s)  # utils.py:453
+        if (nh, nw) != (H, W):  # cv2.resize to the same size is a copy
+            if s > 1.0:  # centre crop (utils.py:465-468)
+                oy, ox = (nh - H) // 2, (nw - W) // 2
+            else:  # centre pad (utils.py:469-472)
+                oy, ox = -((H - nh) // 2), -((W - nw) // 2)
+            st.append((2, {"scale_x": 1.0 / (nw / W), "scale_y": 1.0 / (nh / H), "new_w": nw, "new_h": nh,
+                           "off_x": ox, "off_y": oy}))
+    if not st:
+        st.append((0, {}))
+    if len(p["rects"]) > 5:
+        raise ValueError("at most 5 dropout rectangles per stack")
+    return st
+
+
+def _run_bev_passes(jobs):
+    """jobs: [(src [C,H,W] cuda f32, dst like src, params)] -> ivit_bev_augment once per pass depth
+    (1 or 2) over every job; two-pass jobs go through a scratch stack."""
+    if not jobs:
+        return
+    H, W = jobs[0][0].shape[-2:]
+    levels, keep = [[], []], []
+    for src, dst, p in jobs:
+        for t in (src, dst):
+            if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous() or t.dim() != 3 \
+                    or tuple(t.shape[-2:]) != (H, W):
+                raise ValueError(f"BEV stacks must be contiguous cuda f32 [C, {H}, {W}] (got {tuple(t.shape)})")
+        if src.shape != dst.shape:
+            raise ValueError("augmentation output must match its input")
+        if src.data_ptr() == dst.data_ptr():
+            raise ValueError("augmentation passes are out of place (src and dst share storage)")
+        st = _stages(p, H, W)
+        bufs = [src] + [torch.empty_like(src) for _ in st[:-1]] + [dst]
+        keep += bufs[1:-1]
+        for i, (op, f) in enumerate(st):
+            e = np.zeros((), _BEV_PASS)
+            e["src"], e["dst"], e["C"], e["op"] = bufs[i].data_ptr(), bufs[i + 1].data_ptr(), src.shape[0], op
+            e["flip"] = int(p["flip"] and i == 0)
+            if i == len(st) - 1 and p["rects"]:
+                e["n_rect"] = len(p["rects"])
+                e["rect"][: len(p["rects"])] = p["rects"]
+            for k, v in f.items():
+                e[k] = v
+            levels[i].append(e)
+    cur = torch.cuda.current_stream()
+    for lv in levels:
+        if not lv:
+            continue
+        tab = torch.from_numpy(np.stack(lv).view(np.uint8).reshape(-1)).pin_memory().to(jobs[0][0].device,
+                                                                                           non_blocking=True)
+        keep.append(tab)
+        lib.ivit_bev_augment(ptr(tab), len(lv), H, W, max(int(e["C"]) for e in lv), stream())
+    for t in keep:  # scratch stacks and pass tables stay allocated until the launches have run
+        t.record_stream(cur)
+
+
+def _bev_in(x, device=None):
+    if isinstance(x, torch.Tensor):
+        t = x if x.is_cuda else x.to(_dev(device))
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(_dev(device))
+    return t.float().contiguous()
+
+
+def _gt_update(boxes, intents, p):
+    """GT side of utils.py:402-411 (flip), 440-447 (rotate), 476-477 (scale), in place on numpy."""
+    if p["flip"]:
+        if boxes.shape[0] > 0:
+            boxes[:, 1] *= -1
+            boxes[:, 4] *= -1
+            boxes[:, 4] = np.arctan2(np.sin(boxes[:, 4]), np.cos(boxes[:, 4]))
+        if intents is not None and intents.shape[0] > 0:
+            intents[:] = _FLIP_INTENTION[intents]
+    if p["angle"] is not None and boxes.shape[0] > 0:
+        rad = np.radians(p["angle"])
+        cos_a, sin_a = np.cos(rad), np.sin(rad)
+        cx, cy = boxes[:, 0].copy(), boxes[:, 1].copy()
+        boxes[:, 0] = cx * cos_a - cy * sin_a
+        boxes[:, 1] = cx * sin_a + cy * cos_a
+        boxes[:, 4] += rad
+        boxes[:, 4] = np.arctan2(np.sin(boxes[:, 4]), np.cos(boxes[:, 4]))
+    if p["scale"] is not None and boxes.shape[0] > 0:
+        boxes[:, :4] *= p["scale"]
+
+
+def _augment_stacks(lidar_bev, map_bev, p, device=None):
+    lb, mb = _bev_in(lidar_bev, device), _bev_in(map_bev, device)
+    lo, mo = torch.empty_like(lb), torch.empty_like(mb)
+    _run_bev_passes([(lb, lo, p), (mb, mo, p)])
+    return lo, mo
+
+
+def random_flip_bev(lidar_bev, map_bev, gt_boxes_xywha: np.ndarray, gt_intentions: np.ndarray):
+    """utils.py:394-415 on the GPU: the rasters come back as device tensors (mirrored when the draw
+    says so); the GT arrays are updated in place and returned, as in the reference."""
+    p = _draw_params(rotate=False, scale=False, dropout=False)
+    if p["flip"]:
+        lidar_bev, map_bev = _augment_stacks(lidar_bev, map_bev, p)
+        _gt_update(gt_boxes_xywha, gt_intentions, p)
+    return lidar_bev, map_bev, gt_boxes_xywha, gt_intentions
+
+
+def random_rotate_bev(lidar_bev, map_bev, gt_boxes_xywha: np.ndarray, angle_range_deg=(-15.0, 15.0)):
+    """utils.py:417-448 on the GPU: one warpAffine pass over every channel of both stacks."""
+    p = _draw_params(flip=False, scale=False, dropout=False, angle_range_deg=angle_range_deg)
+    if p["angle"] is not None:
+        lidar_bev, map_bev = _augment_stacks(lidar_bev, map_bev, p)
+        _gt_update(gt_boxes_xywha, None, p)
+    return lidar_bev, map_bev, gt_boxes_xywha
+
+
+def random_scale_bev(lidar_bev, map_bev, gt_boxes_xywha: np.ndarray, scale_range=(0.95, 1.05)):
+    """utils.py:450-478 on the GPU: one resize + centre crop / pad pass over both stacks."""
+    p = _draw_params(flip=False, rotate=False, dropout=False, scale_range=scale_range)
+    if p["scale"] is not None:
+        lidar_bev, map_bev = _augment_stacks(lidar_bev, map_bev, p)
+        _gt_update(gt_boxes_xywha, None, p)
+    return lidar_bev, map_bev, gt_boxes_xywha
+
+
+def random_bev_dropout(lidar_bev, map_bev, dropout_prob: float = 0.1, patch_size_range=(20, 50),
+                       num_patches_range=(1, 5)):
+    """utils.py:480-494 on the GPU: the drawn rectangles zeroed in a copy pass."""
+    p = _draw_params(flip=False, rotate=False, scale=False, dropout_prob=dropout_prob,
+                     patch_size_range=patch_size_range, num_patches_range=num_patches_range)
+    if p["rects"]:
+        lidar_bev, map_bev = _augment_stacks(lidar_bev, map_bev, p)
+    return lidar_bev, map_bev
+
+
+def _gt_arrays(gt_dict):
+    b, i = gt_dict["boxes_xywha"], gt_dict["intentions"]
+    b = b.detach().cpu().numpy().copy() if isinstance(b, torch.Tensor) else np.array(b, copy=True)
+    i = i.detach().cpu().numpy().copy() if isinstance(i, torch.Tensor) else np.array(i, copy=True)
+    return b, i
+
+
+def augment_bev(lidar_bev, map_bev, gt_dict: dict, device=None):
+    """utils.py:500-517 on the GPU: flip -> rotate -> scale -> dropout fused into one or two passes
+    (two when rotate and scale are both drawn). -> (lidar, map device tensors, GT dict f32 / int64)."""
+    p = _draw_params()
+    lo, mo = _augment_stacks(lidar_bev, map_bev, p, device)
+    b, i = _gt_arrays(gt_dict)
+    _gt_update(b, i, p)
+    return lo, mo, {"boxes_xywha": torch.from_numpy(b).float(), "intentions": torch.from_numpy(i).long()}
+
+
+def augment_bev_batch(lidar_bev: torch.Tensor, map_bev: torch.Tensor, gt_list, out=None):
+    """augment_bev for every sample of a device batch ([B, C, H, W] f32 each), sample 0's draws
+    first (the dataset's __getitem__ order); one launch per pass depth for all 2B stacks.
+    -> (lidar_out, map_out, gt_list_out, params)."""
+    if lidar_bev.dim() != 4 or map_bev.dim() != 4 or lidar_bev.shape[0] != map_bev.shape[0]:
+        raise ValueError("augment_bev_batch takes [B, C, H, W] lidar and map batches")
+    lo, mo = out if out is not None else (torch.empty_like(lidar_bev), torch.empty_like(map_bev))
+    jobs, gts, params = [], [], []
+    for b in range(lidar_bev.shape[0]):
+        p = _draw_params(H=lidar_bev.shape[-2], W=lidar_bev.shape[-1])
+        jobs += [(lidar_bev[b], lo[b], p), (map_bev[b], mo[b], p)]
+        bx, it = _gt_arrays(gt_list[b])
+        _gt_update(bx, it, p)
+        gts.append({"boxes_xywha": torch.from_numpy(bx).float(), "intentions": torch.from_numpy(it).long()})
+        params.append(p)
+    _run_bev_passes(jobs)
+    return lo, mo, gts, params
