@@ -4,6 +4,6 @@ timeout -k 10 300 python -u -m pytest tests/test_bev_augment.py -x -v -m gpu --t
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 180 python tools/augment_bench.py > gpurun_out/aug_bench.json 2> gpurun_out/aug_bench.err; rc=$?; echo "bench rc=$rc"; cat gpurun_out/aug_bench.json; tail -3 gpurun_out/aug_bench.err
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_aug -o aug -- python tools/augment_bench.py > gpurun_out/prof_aug.log 2>&1; rc=$?; echo "prof rc=$rc"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_aug -o aug -- python tools/augment_bench.py > gpurun_out/prof_aug.log 2>&1; rc=$?; echo "prof rc=$rc"
 find gpurun_out/prof_aug -name "*stats*" | head
 exit $rc

@@ -94,8 +94,8 @@ extern "C" int ivit_lidar_bev(const void* points, int points_f64, long ld, const
 // for every [C, H, W] stack of a batch (LiDAR and map stacks of all samples; blockIdx.z =
 // pass entry). Each thread owns one output pixel: it derives its source taps and weights once
 // (the same for every plane) and then streams CPB planes, so the map arithmetic is amortised
-// and the pass is a read + write of the stack (HBM-bound). Tiles are 64 x 4 pixels, so the row
-// below a tile's last row is the only extra source row it touches.
+// and the pass is a read + write of the stack (HBM-bound). Tiles are 64 x 4 pixels (16 x 16 for
+// the rotation, whose per-wave source footprint is sheared).
 //   op 0: copy (np.flip / dropout only), op 1: cv2.warpAffine INTER_LINEAR BORDER_CONSTANT 0
 //   (1/32-pixel fixed-point source coordinates, exact bilinear table), op 2: cv2.resize
 //   INTER_LINEAR to (new_w, new_h) then the centre crop / zero pad of random_scale_bev.
@@ -113,7 +113,7 @@ struct BevPass {
 };
 static_assert(sizeof(BevPass) == 192, "ivit_bev_pass layout");
 
-constexpr int kBevTileW = 64, kBevTileH = 4, kBevCPB = 8;
+constexpr int kBevTileW = 64, kBevTileH = 4, kBevCPB = 16;
 
 // resizeGeneric's per-axis source index and weights (f32 data): the f64 source position is
 // rounded to f32, floored, clamped at both ends (weight 0), and from sx >= n - 1 on the
@@ -131,39 +131,106 @@ IVIT_DEV void resize_axis(int d, int n_src, double scale, int& s0, int& s1, floa
   a1 = f;
 }
 
+using gcfloat = const __attribute__((address_space(1))) float;
+using gfloat = __attribute__((address_space(1))) float;
+
+// One pixel's source taps (plane offsets), weights and flags: MODE 0 copies tap 0; MODE 1 sums
+// ((v0 w0 + v1 w1) + v2 w2) + v3 w3 with taps outside the image reading 0 (ok); MODE 2 is the
+// separable resize, h_r = cpx ? v_r0 : v_r0 w0 + v_r1 w1 (rows r = taps 0-1 / 2-3), out =
+// h_0 w2 + h_1 w3; MODE 3 writes zeros.
+struct Taps {
+  unsigned i[4];  // unsigned 32-bit offsets: the loads take the uniform base in SGPRs (saddr)
+  bool ok[4];
+  float w[4];
+  bool cpx;
+};
+
+// N planes of one pixel: every load is issued before the first store, so a thread keeps 4N
+// loads in flight (the planes are independent; src and dst never alias).
+template <int MODE, int N>
+IVIT_DEV void bev_planes(gcfloat* __restrict__ s, gfloat* __restrict__ d, unsigned HW, unsigned o, const Taps& t) {
+  if constexpr (MODE == 3) {
+#pragma unroll
+    for (unsigned c = 0; c < N; ++c) d[c * HW + o] = 0.f;
+  } else if constexpr (MODE == 0) {
+    float v[N];
+#pragma unroll
+    for (unsigned c = 0; c < N; ++c) v[c] = s[c * HW + t.i[0]];
+#pragma unroll
+    for (unsigned c = 0; c < N; ++c) d[c * HW + o] = v[c];
+  } else {
+    float v[N][4];
+#pragma unroll
+    for (unsigned c = 0; c < N; ++c)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[c][k] = s[c * HW + t.i[k]];
+#pragma unroll
+    for (unsigned c = 0; c < N; ++c) {
+      float r;
+      if constexpr (MODE == 1) {
+        const float v0 = t.ok[0] ? v[c][0] : 0.f, v1 = t.ok[1] ? v[c][1] : 0.f;
+        const float v2 = t.ok[2] ? v[c][2] : 0.f, v3 = t.ok[3] ? v[c][3] : 0.f;
+        r = ((v0 * t.w[0] + v1 * t.w[1]) + v2 * t.w[2]) + v3 * t.w[3];
+      } else {
+        const float h0 = t.cpx ? v[c][0] : v[c][0] * t.w[0] + v[c][1] * t.w[1];
+        const float h1 = t.cpx ? v[c][2] : v[c][2] * t.w[0] + v[c][3] * t.w[1];
+        r = h0 * t.w[2] + h1 * t.w[3];
+      }
+      d[c * HW + o] = r;
+    }
+  }
+}
+
+template <int MODE>
+IVIT_DEV void bev_run(gcfloat* s, gfloat* d, unsigned HW, unsigned o, int cn, const Taps& t) {
+  if (cn == kBevCPB) {
+    bev_planes<MODE, kBevCPB>(s, d, HW, o, t);
+  } else {
+    for (int c = 0; c < cn; ++c) bev_planes<MODE, 1>(s + (long)c * HW, d + (long)c * HW, HW, o, t);
+  }
+}
+
 __global__ __launch_bounds__(256) void bev_pass_kernel(const BevPass* __restrict__ passes, int H, int W) {
-  const BevPass& P = passes[blockIdx.z];
-  const int C = P.C;
+  const BevPass& P = passes[blockIdx.z];  // uniform: scalar loads, all read before the first store
   const int c0 = blockIdx.y * kBevCPB;
-  if (c0 >= C) return;
-  const int tiles_w = (W + kBevTileW - 1) / kBevTileW;
-  const int x = (blockIdx.x % tiles_w) * kBevTileW + (threadIdx.x & (kBevTileW - 1));
-  const int y = (blockIdx.x / tiles_w) * kBevTileH + threadIdx.x / kBevTileW;
+  if (c0 >= P.C) return;
+  const int op = P.op;
+  // XCD-aware tile order: gridDim.x is a multiple of 8 and workgroups go round-robin over the 8
+  // XCDs, so XCD k runs the contiguous tile range [k * per, (k + 1) * per): neighbouring tiles,
+  // which share source cache lines and the rows below, hit one L2.
+  const int per = gridDim.x >> 3;
+  const int tile = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  int x, y;
+  if (op == 1) {  // rotation: 16 x 16 tiles (a wave = 16 x 4 pixels), so one gather instruction's
+                  // sheared source footprint spans ~8 rows instead of the ~17 of a 64-pixel row
+    const int tw = (W + 15) / 16;
+    x = (tile % tw) * 16 + (threadIdx.x & 15);
+    y = (tile / tw) * 16 + (threadIdx.x >> 4);
+  } else {  // 64 x 4 tiles: 256-B row segments per wave
+    const int tw = (W + kBevTileW - 1) / kBevTileW;
+    x = (tile % tw) * kBevTileW + (threadIdx.x & (kBevTileW - 1));
+    y = (tile / tw) * kBevTileH + threadIdx.x / kBevTileW;
+  }
   if (x >= W || y >= H) return;
-  const long HW = (long)H * W;
-  const float* __restrict__ src = reinterpret_cast<const float*>(P.src) + (long)c0 * HW;
-  float* __restrict__ dst = reinterpret_cast<float*>(P.dst) + (long)c0 * HW + (long)y * W + x;
-  const int cn = min(kBevCPB, C - c0);
+  const unsigned HW = H * W, o = y * W + x;  // 32-bit plane offsets (launcher: kBevCPB * H * W < 2^31)
+  gcfloat* src = reinterpret_cast<gcfloat*>(P.src) + (long)c0 * HW;  // uniform bases: saddr loads / stores
+  gfloat* dst = reinterpret_cast<gfloat*>(P.dst) + (long)c0 * HW;
+  const int cn = min(kBevCPB, P.C - c0);
 
   bool zero = false;
   for (int r = 0; r < P.n_rect; ++r)
     zero |= y >= P.rect[r][0] && y < P.rect[r][0] + P.rect[r][2] && x >= P.rect[r][1] && x < P.rect[r][1] + P.rect[r][3];
-  const int op = P.op;
   if (!zero && op == 2) {
     const int ry = y + P.off_y, rx = x + P.off_x;
     zero = ry < 0 || ry >= P.new_h || rx < 0 || rx >= P.new_w;
   }
-  if (zero) {
-    for (int c = 0; c < cn; ++c) dst[c * HW] = 0.f;
-    return;
-  }
-  auto col = [&](int c) { return P.flip ? W - 1 - c : c; };
+  if (zero) return bev_run<3>(src, dst, HW, o, cn, Taps{});
+  const bool flip = P.flip;
+  auto col = [&](int c) { return flip ? W - 1 - c : c; };
+  Taps t{};
   if (op == 0) {
-    const float* s = src + (long)y * W + col(x);
-#pragma unroll
-    for (int c = 0; c < kBevCPB; ++c)
-      if (c < cn) dst[c * HW] = s[c * HW];
-    return;
+    t.i[0] = (unsigned)(y * W + col(x));
+    return bev_run<0>(src, dst, HW, o, cn, t);
   }
   if (op == 1) {
     const double* m = P.m;
@@ -174,43 +241,28 @@ __global__ __launch_bounds__(256) void bev_pass_kernel(const BevPass* __restrict
     const int X = (X0 + adx) >> 5, Y = (Y0 + bdx) >> 5;
     const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
     const float tx = (float)(X & 31) * (1.f / 32.f), ty = (float)(Y & 31) * (1.f / 32.f);
-    const float w[4] = {(1.f - ty) * (1.f - tx), (1.f - ty) * tx, ty * (1.f - tx), ty * tx};
-    long idx[4];
-    bool ok[4];
+    t.w[0] = (1.f - ty) * (1.f - tx);
+    t.w[1] = (1.f - ty) * tx;
+    t.w[2] = ty * (1.f - tx);
+    t.w[3] = ty * tx;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int cx = sx + (k & 1), cy = sy + (k >> 1);
-      ok[k] = cx >= 0 && cx < W && cy >= 0 && cy < H;
-      idx[k] = ok[k] ? (long)cy * W + col(cx) : 0;
+      t.ok[k] = cx >= 0 && cx < W && cy >= 0 && cy < H;
+      t.i[k] = t.ok[k] ? (unsigned)(cy * W + col(cx)) : 0u;  // an in-bounds address; the value is replaced by 0
     }
-#pragma unroll
-    for (int c = 0; c < kBevCPB; ++c) {
-      if (c < cn) {
-        const float* s = src + c * HW;
-        const float v0 = ok[0] ? s[idx[0]] : 0.f, v1 = ok[1] ? s[idx[1]] : 0.f;
-        const float v2 = ok[2] ? s[idx[2]] : 0.f, v3 = ok[3] ? s[idx[3]] : 0.f;
-        dst[c * HW] = ((v0 * w[0] + v1 * w[1]) + v2 * w[2]) + v3 * w[3];
-      }
-    }
-    return;
+    return bev_run<1>(src, dst, HW, o, cn, t);
   }
   // op 2: resize (then centre crop / pad: out(y, x) = resized(y + off_y, x + off_x))
   int sx0, sx1, sy0, sy1;
-  float a0, a1, b0, b1;
-  bool cpx, cpy;
-  resize_axis(x + P.off_x, W, P.scale_x, sx0, sx1, a0, a1, cpx);
-  resize_axis(y + P.off_y, H, P.scale_y, sy0, sy1, b0, b1, cpy);
-  const long i00 = (long)sy0 * W + col(sx0), i01 = (long)sy0 * W + col(sx1);
-  const long i10 = (long)sy1 * W + col(sx0), i11 = (long)sy1 * W + col(sx1);
-#pragma unroll
-  for (int c = 0; c < kBevCPB; ++c) {
-    if (c < cn) {
-      const float* s = src + c * HW;
-      const float h0 = cpx ? s[i00] : s[i00] * a0 + s[i01] * a1;
-      const float h1 = cpx ? s[i10] : s[i10] * a0 + s[i11] * a1;
-      dst[c * HW] = h0 * b0 + h1 * b1;
-    }
-  }
+  bool cpy;
+  resize_axis(x + P.off_x, W, P.scale_x, sx0, sx1, t.w[0], t.w[1], t.cpx);
+  resize_axis(y + P.off_y, H, P.scale_y, sy0, sy1, t.w[2], t.w[3], cpy);
+  t.i[0] = (unsigned)(sy0 * W + col(sx0));
+  t.i[1] = (unsigned)(sy0 * W + col(sx1));
+  t.i[2] = (unsigned)(sy1 * W + col(sx0));
+  t.i[3] = (unsigned)(sy1 * W + col(sx1));
+  bev_run<2>(src, dst, HW, o, cn, t);
 }
 
 }  // namespace
@@ -219,9 +271,10 @@ extern "C" int ivit_bev_augment(const void* passes, long n_passes, long H, long 
   if (n_passes <= 0 || max_planes <= 0) return 0;
   IVIT_CHECK_ARG(passes != nullptr, "ivit_bev_augment: null pass table");
   IVIT_CHECK_ARG(n_passes < 65536, "ivit_bev_augment: too many passes (%ld)", n_passes);
-  IVIT_CHECK_ARG(H > 1 && W > 1 && H * W < (1L << 31) && H < 32768 && W < 32768,
+  IVIT_CHECK_ARG(H > 1 && W > 1 && kBevCPB * H * W < (1L << 31) && H < 32768 && W < 32768,
                  "ivit_bev_augment: bad plane size %ldx%ld", H, W);
-  const long tiles = ivit_cdiv(W, kBevTileW) * ivit_cdiv(H, kBevTileH);
+  long tiles = std::max(ivit_cdiv(W, kBevTileW) * ivit_cdiv(H, kBevTileH), ivit_cdiv(W, 16) * ivit_cdiv(H, 16));
+  tiles = ivit_cdiv(tiles, 8) * 8;  // the kernel's XCD tile order needs a multiple of 8
   dim3 g((unsigned)tiles, (unsigned)ivit_cdiv(max_planes, kBevCPB), (unsigned)n_passes);
   hipLaunchKernelGGL(bev_pass_kernel, g, dim3(256), 0, ivit_stream(stream), (const BevPass*)passes, (int)H,
                      (int)W);
