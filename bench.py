@@ -123,6 +123,9 @@ def main():
     ap.add_argument("--grid", type=str, default="400x720")
     ap.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--augment", action="store_true",
+                    help="train mode: run the training-time augment_bev (dataset.py:352-353) on the batch "
+                         "inside every timed step (ivit_bev_augment passes)")
     ap.add_argument("--bucket-mb", type=float, default=64)
     ap.add_argument("--ddp", choices=["buckets", "torch"], default="buckets",
                     help="gradient exchange: ddp.GradBuckets (default) or torch DistributedDataParallel")
@@ -164,8 +167,18 @@ def main():
         if trainer.buckets is None and world > 1 and args.ddp == "buckets":
             raise RuntimeError("gradient buckets missing for world > 1")
 
-        def step():
-            return trainer.step(batch)
+        if args.augment:
+            import random
+            random.seed(1234 + rank)
+            aug_out = (torch.empty_like(batch["lidar_bev"]), torch.empty_like(batch["map_bev"]))
+
+            def step():
+                lo, mo, gts, _ = utils.augment_bev_batch(batch["lidar_bev"], batch["map_bev"], batch["gt_list"],
+                                                         out=aug_out)
+                return trainer.step({"lidar_bev": lo, "map_bev": mo, "gt_list": gts})
+        else:
+            def step():
+                return trainer.step(batch)
     else:
         kept = []
 
@@ -209,10 +222,12 @@ def main():
     achieved = afl / (attn_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if cd == torch.bfloat16 else 157.3
     # PMC traffic was collected on the default train configuration only
-    default_cfg = train and (H, W) == (400, 720) and B == 8 and cd == torch.bfloat16
+    default_cfg = train and (H, W) == (400, 720) and B == 8 and cd == torch.bfloat16 and not args.augment
     traffic, traffic_src = pmc_traffic(ROOF_KERNEL) if default_cfg else (None, None)
     if train:
         workload = f"IntentNetViT train step (fwd+loss+bwd+AdamW), {args.dtype}, {H}x{W}, batch {B}/GPU"
+        if args.augment:
+            workload = "augment_bev (GPU) + " + workload
         metric = "BEV samples/sec (fwd+bwd) IntentNetViT at 1/2/4/8 MI355X; attn MFMA util %"
     else:
         workload = (f"IntentNetViT eval_vit.py inference (fwd + sigmoid/threshold 0.1 + decode + NMS 0.2 + argmax), "

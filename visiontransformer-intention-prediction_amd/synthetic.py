@@ -41,23 +41,34 @@ def synthetic_batch(batch: int, grid=(GRID_HEIGHT_PX, GRID_WIDTH_PX), gen: torch
 class SyntheticBEVLoader:
     """Iterable of ``num_batches`` synthetic batches (a stand-in for the reference DataLoader).
     ``resident=True`` draws one batch and yields it every time (inputs stay in HBM: the
-    benchmark's primary placement); otherwise each batch is drawn fresh on the host."""
+    benchmark's primary placement); otherwise each batch is drawn fresh on the host.
+    ``augment=True`` applies the training-time augment_bev of dataset.py:352-353 to every
+    yielded batch on the GPU (utils.augment_bev_batch; python `random` draws, reference order)."""
 
     def __init__(self, batch: int, num_batches: int, grid=(GRID_HEIGHT_PX, GRID_WIDTH_PX), rank: int = 0,
-                 device=None, resident: bool = True, n_boxes: int = 20):
+                 device=None, resident: bool = True, n_boxes: int = 20, augment: bool = False):
         self.batch, self.num_batches, self.grid = batch, num_batches, tuple(grid)
         self.device, self.resident, self.n_boxes = device, resident, n_boxes
+        self.augment, self._aug_out = augment, None
         self.gen = torch.Generator().manual_seed(1234 + rank)
         self._fixed = None
 
     def __len__(self):
         return self.num_batches
 
+    def _augmented(self, b):
+        import utils
+        if self._aug_out is None:
+            self._aug_out = (torch.empty_like(b["lidar_bev"]), torch.empty_like(b["map_bev"]))
+        lo, mo, gts, _ = utils.augment_bev_batch(b["lidar_bev"], b["map_bev"], b["gt_list"], out=self._aug_out)
+        return {"lidar_bev": lo, "map_bev": mo, "gt_list": gts}
+
     def __iter__(self):
         for _ in range(self.num_batches):
             if self.resident:
                 if self._fixed is None:
                     self._fixed = synthetic_batch(self.batch, self.grid, self.gen, self.n_boxes, self.device)
-                yield self._fixed
+                b = self._fixed
             else:
-                yield synthetic_batch(self.batch, self.grid, self.gen, self.n_boxes, self.device)
+                b = synthetic_batch(self.batch, self.grid, self.gen, self.n_boxes, self.device)
+            yield self._augmented(b) if self.augment else b

@@ -81,6 +81,8 @@ def parse_args(argv=None):
     ap.add_argument("--save-dir", type=str, default=MODEL_SAVE_DIR_VIT)
     ap.add_argument("--no-save", action="store_true")
     ap.add_argument("--fresh-batches", action="store_true", help="draw a new synthetic batch every step")
+    ap.add_argument("--augment", action="store_true",
+                    help="training-time augment_bev on every batch (dataset.py:352-353), on the GPU")
     return ap.parse_args(argv)
 
 
@@ -107,7 +109,7 @@ def main(argv=None):
 
     if args.synthetic:
         loader = SyntheticBEVLoader(args.batch, args.batches_per_epoch, (H, W), rank=rank, device=device,
-                                    resident=not args.fresh_batches)
+                                    resident=not args.fresh_batches, augment=args.augment)
     else:
         if not Path(TRAIN_DATA_DIR).is_dir():
             log(f"ERROR: Training data directory not found: {TRAIN_DATA_DIR} (use --synthetic)")
