@@ -244,6 +244,18 @@ typedef struct ivit_bev_pass {
 } ivit_bev_pass;
 int ivit_bev_augment(const void* passes, long n_passes, long H, long W, long max_planes, void* stream);
 
+/* ---- Strided convolutions of the CNN variant (model_cnn.py:7-12, 14-33, 86-100; SURVEY.md
+ * §8f rank 4) as im2col + the dense GEMMs above. X: NHWC [B, H, W, C] (f32 or bf16); cols:
+ * [B*Ho*Wo, ldc] row (b, oy, ox), column (ky*k + kx)*C + c = X[b, oy*s - pad + ky,
+ * ox*s - pad + kx, c] (0 outside the map and in columns k*k*C .. ldc-1), i.e. the
+ * [Cout][k][k][Cin] packed weight viewed [Cout, k*k*C] is the GEMM operand; Ho, Wo follow
+ * nn.Conv2d (floor((H + 2 pad - k) / s) + 1). col2im is the adjoint as a gather: dX (f32, NHWC)
+ * = sum over (ky, kx) ascending of the dcols entries whose window covers the pixel.       */
+int ivit_im2col(int x_dtype, const void* X, long B, long H, long W, long C, long k, long stride, long pad, long Ho,
+                long Wo, void* cols, long ldc, int cols_dtype, void* stream);
+int ivit_col2im(const float* dcols, long ldc, long B, long H, long W, long C, long k, long stride, long pad, long Ho,
+                long Wo, float* dX, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

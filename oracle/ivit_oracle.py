@@ -662,3 +662,42 @@ def bev_augment_inputs(seed, lidar_ch=3, map_ch=2, G=20, H=BEV_H, W=BEV_W):
                       rng.uniform(3.5, 6.5, G), rng.uniform(-math.pi, math.pi, G)], 1).astype(np.float32)
     intents = rng.integers(0, 8, G).astype(np.int64)
     return lidar, mp, boxes, intents
+
+
+# --------------------------------------------------------------------------------------
+# IntentNetCNN (model_cnn.py) — torch fp32 restatement
+# --------------------------------------------------------------------------------------
+CNN_STAGES = (("lidar", ((160, 2), (192, 1), (224, 2))), ("map", ((32, 2), (64, 1), (96, 2))))  # model_cnn.py:39-73
+
+
+def _cnn_bn(sd, p, x, training):
+    rm, rv = sd[p + "running_mean"], sd[p + "running_var"]
+    return F.batch_norm(x, rm, rv, sd[p + "weight"], sd[p + "bias"], training, 0.1, 1e-5)
+
+
+def cnn_block(sd, p, x, stride, k, training):
+    """model_cnn.py:14-33: conv k x k (pad (k-1)//2, stride) -> BN -> ReLU -> conv k x k -> BN,
+    + identity (conv1x1 stride + BN when p + 'downsample.0.weight' exists) -> ReLU."""
+    pad = (k - 1) // 2
+    out = F.relu(_cnn_bn(sd, p + "bn1.", F.conv2d(x, sd[p + "conv1.weight"], None, stride, pad), training))
+    out = _cnn_bn(sd, p + "bn2.", F.conv2d(out, sd[p + "conv2.weight"], None, 1, pad), training)
+    if p + "downsample.0.weight" in sd:
+        x = _cnn_bn(sd, p + "downsample.1.", F.conv2d(x, sd[p + "downsample.0.weight"], None, stride), training)
+    return F.relu(out + x)
+
+
+def cnn_forward(sd, lidar, map_bev, training=False, ks=5, fusion_ks=3, blocks=2, fusion_layers=2):
+    """IntentNetCNN.forward (model_cnn.py:110-150). BN running stats in sd update in place in
+    training mode, as nn.BatchNorm2d's do."""
+    def stage(name, x, stride, k, n):
+        for i in range(n):
+            x = cnn_block(sd, f"backbone.{name}.{i}.", x, stride if i == 0 else 1, k, training)
+        return x
+    feats = []
+    for stream_name, stages in CNN_STAGES:
+        x = lidar if stream_name == "lidar" else map_bev
+        for si, (_, stride) in enumerate(stages):
+            x = stage(f"{stream_name}_stage{si + 1}", x, stride, ks, blocks)
+        feats.append(x)
+    f = stage("fusion_block", torch.cat(feats, 1), 2, fusion_ks, fusion_layers)
+    return heads_forward(sd, f)

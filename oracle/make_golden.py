@@ -313,6 +313,54 @@ def gen_bev_augment():
     np.savez_compressed(os.path.join(OUT, "bev_augment.npz"), **rec)
 
 
+def gen_cnn_small():
+    """The reference's OWN IntentNetCNN (model_cnn.py) at a 32x48 grid with its default channels,
+    filled by the seeded filler in its state_dict order: eval outputs, train outputs + loss
+    (downsampling off) + gradient samples + BN running stats; the oracle restatement agrees."""
+    import loss as ref_loss
+    import model_cnn as ref_cnn
+    import utils as ref_utils
+    from oracle.weights import fill_state_dict
+    img = SMALL_IMG
+    m = ref_cnn.IntentNetCNN()
+    keys = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    sd = fill_state_dict(keys, seed=0)
+    m.load_state_dict(sd, strict=True)
+    lidar, mp, _ = O.synthetic_batch(2, img, seed=1234)
+    gts = small_gt()
+    anchors = ref_utils.generate_anchors(img[0], img[1], 8)
+    rec = {"keys": np.array([k for k, _ in keys]), "w_checksum": state_checksum(sd)}
+    for i, g in enumerate(gts):
+        rec[f"gt{i}_boxes"] = g["boxes_xywha"].numpy()
+        rec[f"gt{i}_ints"] = g["intentions"].numpy()
+    m.eval()
+    with torch.no_grad():
+        c, b, it = m(lidar, mp)
+        oc, ob, oi = O.cnn_forward({k: v.clone() for k, v in sd.items()}, lidar, mp, training=False)
+    assert max(float((x - y).abs().max()) for x, y in ((c, oc), (b, ob), (it, oi))) < 1e-4
+    rec.update(eval_cls=c.numpy(), eval_box=b.numpy(), eval_int=it.numpy())
+    m.train()
+    c, b, it = m(lidar, mp)
+    d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False)(c, b, it, anchors, gts)
+    d["loss"].backward()
+    rec.update(train_cls=c.detach().numpy(), train_box=b.detach().numpy(), train_int=it.detach().numpy(),
+               train_loss=np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]),
+                                    float(d["intent_loss"]), float(d["num_pos_anchors"])]))
+    grads = {k: p.grad for k, p in m.named_parameters() if p.grad is not None}
+    names = sorted(grads)
+    samples, strides = zip(*[_sample(grads[k]) for k in names])
+    rec.update(grad_names=np.array(names), grad_abssum=np.array([float(grads[k].double().abs().sum()) for k in names]),
+               grad_samples=np.stack(samples), grad_strides=np.array(strides))
+    bn = {k: v for k, v in m.state_dict().items() if "running_" in k}
+    rec.update(bn_names=np.array(sorted(bn)), bn_values=np.concatenate([bn[k].numpy() for k in sorted(bn)]),
+               bn_sizes=np.array([bn[k].numel() for k in sorted(bn)]))
+    osd = {k: v.clone() for k, v in sd.items()}
+    c2, _, _ = O.cnn_forward(osd, lidar, mp, training=True)
+    assert float((c2 - c.detach()).abs().max()) < 1e-4
+    np.savez_compressed(os.path.join(OUT, "cnn_small.npz"), **rec)
+    print("cnn_small: params", sum(int(np.prod(s)) for _, s in keys), "loss", rec["train_loss"])
+
+
 def cross_check_vit():
     """HF ViTModel (stand-in) vs the oracle's timm restatement, 12 blocks, real widths."""
     cfg = model_cfg(img_size=SMALL_IMG)
@@ -345,3 +393,4 @@ if __name__ == "__main__":
     gen_geometry()
     gen_lidar_bev()
     gen_bev_augment()
+    gen_cnn_small()

@@ -88,9 +88,14 @@ def make_state_dict(cfg, seed=0):
     Scales keep activations O(1) through 12 pre-norm blocks so fp32 parity is
     meaningful (no saturation, no vanishing signal).
     """
+    return fill_state_dict(param_shapes(cfg), seed)
+
+
+def fill_state_dict(shapes, seed=0):
+    """The filler over any ordered (key, shape) list (also the CNN variant's state dict)."""
     g = torch.Generator().manual_seed(seed)
     sd = OrderedDict()
-    for key, shape in param_shapes(cfg):
+    for key, shape in shapes:
         if key.endswith("num_batches_tracked"):
             sd[key] = torch.zeros((), dtype=torch.long)
             continue
