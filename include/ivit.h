@@ -70,7 +70,7 @@ int ivit_patch_embed_wgrad_cols(const void* dtok, const void* cols, long B, long
                                 long work_bytes, void* stream);
 
 /* ---- k x k stride-1 "same" convolution on NHWC maps (BasicBlock conv3x3/conv1x1,
- *      model_vit.py:12-17; DetectionHead/IntentionHead conv, heads.py:16,37).
+ *      model_vit.py:12-17; DetectionHead/IntentionHead conv, heads.py:16,37; k = 5: model_cnn.py:7-9).
  *      Weights packed [Cout][k][k][Cin] (see ivit_pack_conv_weight).                           */
 int ivit_conv_fwd(int dtype, const void* X, long B, long H, long W, long Cin, const void* Wp, const float* bias,
                   long Cout, long ks, void* Y, long ldy, int y_dtype, void* stream);
@@ -249,7 +249,7 @@ int ivit_bev_augment(const void* passes, long n_passes, long H, long W, long max
  * [B*Ho*Wo, ldc] row (b, oy, ox), column (ky*k + kx)*C + c = X[b, oy*s - pad + ky,
  * ox*s - pad + kx, c] (0 outside the map and in columns k*k*C .. ldc-1), i.e. the
  * [Cout][k][k][Cin] packed weight viewed [Cout, k*k*C] is the GEMM operand; Ho, Wo follow
- * nn.Conv2d (floor((H + 2 pad - k) / s) + 1). col2im is the adjoint as a gather: dX (f32, NHWC)
+ * nn.Conv2d (floor((H + 2 pad - k) / s) + 1). col2im (C <= 512) is the adjoint as a gather: dX (f32, NHWC)
  * = sum over (ky, kx) ascending of the dcols entries whose window covers the pixel.       */
 int ivit_im2col(int x_dtype, const void* X, long B, long H, long W, long C, long k, long stride, long pad, long Ho,
                 long Wo, void* cols, long ldc, int cols_dtype, void* stream);

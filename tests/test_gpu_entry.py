@@ -65,3 +65,15 @@ def test_postprocess_empty_after_threshold():
     out = utils.postprocess_batch(cls, torch.zeros(1, NA, 6, device="cuda"), torch.zeros(1, NA, 8, device="cuda"),
                                   anchors)
     assert out[0]["pred_scores"].numel() == 0 and out[0]["pred_boxes_xywha"].shape == (0, 5)
+
+
+def test_train_cnn_synthetic_augmented_epoch_and_checkpoint(tmp_path):
+    """train_cnn.py flow (IntentNetCNN, stride 8) with the GPU augment_bev on every batch."""
+    import train_cnn
+    rc = train_cnn.main(["--synthetic", "--epochs", "1", "--batches-per-epoch", "2", "--batch", "2", "--grid", "32x48",
+                         "--dtype", "bf16", "--augment", "--save-dir", str(tmp_path)])
+    assert rc == 0
+    ck = tmp_path / "cnn_model.pth"
+    assert ck.is_file()
+    d = torch.load(str(ck), map_location="cpu", weights_only=False)
+    assert "backbone.lidar_stage1.0.conv1.weight" in d["model_state_dict"]

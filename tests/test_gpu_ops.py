@@ -209,13 +209,13 @@ def test_attention_large_grid_bf16():
         assert _rel(d[:, i], g[:, i]) < 3e-2, ("qkv"[i], _rel(d[:, i], g[:, i]))
 
 
-@pytest.mark.parametrize("k", [1, 3])
+@pytest.mark.parametrize("k,Cin", [(1, 48), (3, 48), (5, 48), (5, 64)])  # 5: model_cnn.py stride-1 convs
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
-def test_conv_nhwc(k, cd):
+def test_conv_nhwc(k, Cin, cd):
     import ops
     from _lib import BF16, F32
     cdt = BF16 if cd == torch.bfloat16 else F32
-    B, H, W, Cin, Cout = 2, 7, 9, 48, 40
+    B, H, W, Cout = 2, 7, 9, 40
     x = torch.randn(B, Cin, H, W)
     w = torch.randn(Cout, Cin, k, k) / math.sqrt(Cin * k * k)
     bias = torch.randn(Cout) * 0.1

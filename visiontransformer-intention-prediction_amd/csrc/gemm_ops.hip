@@ -429,7 +429,7 @@ static int conv_fwd_t(const void* X, long B, long H, long W, long Cin, const voi
 
 extern "C" int ivit_conv_fwd(int dtype, const void* X, long B, long H, long W, long Cin, const void* Wp,
                              const float* bias, long Cout, long ks, void* Y, long ldy, int y_dtype, void* stream) {
-  IVIT_CHECK_ARG(Cin % 8 == 0 && (ks == 1 || ks == 3), "ivit_conv_fwd: Cin %% 8 and ks in {1,3}");
+  IVIT_CHECK_ARG(Cin % 8 == 0 && (ks == 1 || ks == 3 || ks == 5), "ivit_conv_fwd: Cin %% 8 and ks in {1,3,5}");
   hipStream_t st = ivit_stream(stream);
   int rc;
   if (dtype == IVIT_BF16)

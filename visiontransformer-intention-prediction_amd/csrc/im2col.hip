@@ -14,36 +14,45 @@
 
 namespace {
 
+// One wave per (output pixel, tap): the tap's source pixel is a contiguous run of C channels and
+// so is its destination, so lanes stride over channels (coalesced, f32 -> bf16 in flight); the
+// pixel / tap decomposition is done once per wave in 32-bit arithmetic. The last tap's wave also
+// zeroes the pad columns K .. ldc-1.
 template <typename TI, typename TO>
 __global__ __launch_bounds__(256) void im2col_kernel(const TI* __restrict__ X, int B, int H, int W, int C, int k,
-                                                     int s, int p, int Ho, int Wo, TO* __restrict__ cols, long ldc) {
-  const long K = (long)k * k * C, total = (long)B * Ho * Wo * ldc;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const long row = i / ldc, col = i - row * ldc;
-    float v = 0.f;
-    if (col < K) {
-      const int c = (int)(col % C), kk = (int)(col / C), kx = kk % k, ky = kk / k;
-      const int ox = (int)(row % Wo);
-      const long t = row / Wo;
-      const int oy = (int)(t % Ho), b = (int)(t / Ho);
-      const int y = oy * s - p + ky, x = ox * s - p + kx;
-      if (y >= 0 && y < H && x >= 0 && x < W) v = to_f32(X[(((long)b * H + y) * W + x) * C + c]);
+                                                     int s, int p, int Ho, int Wo, TO* __restrict__ cols, long ldc,
+                                                     int pairs) {
+  const int lane = threadIdx.x & 63;
+  const int taps = k * k;
+  for (int pr = blockIdx.x * 4 + (threadIdx.x >> 6); pr < pairs; pr += gridDim.x * 4) {
+    const int row = pr / taps, tap = pr - (pr / taps) * taps;
+    const int ox = row % Wo, t = row / Wo, oy = t % Ho, b = t / Ho;
+    const int ky = tap / k, kx = tap - (tap / k) * k;
+    const int y = oy * s - p + ky, x = ox * s - p + kx;
+    TO* dst = cols + (long)row * ldc + (long)tap * C;
+    if (y >= 0 && y < H && x >= 0 && x < W) {
+      const TI* src = X + (((long)b * H + y) * W + x) * C;
+      for (int c = lane; c < C; c += 64) dst[c] = from_f32<TO>(to_f32(src[c]));
+    } else {
+      for (int c = lane; c < C; c += 64) dst[c] = from_f32<TO>(0.f);
     }
-    cols[i] = from_f32<TO>(v);
+    if (tap == taps - 1)
+      for (long c = (long)taps * C + lane; c < ldc; c += 64) cols[(long)row * ldc + c] = from_f32<TO>(0.f);
   }
 }
 
+// One wave per input pixel: lanes hold up to 8 x 64 channel sums (C <= 512) and the wave walks
+// the taps whose output pixel exists (ky then kx ascending: the summation order is fixed).
 __global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcols, long ldc, int B, int H, int W,
                                                      int C, int k, int s, int p, int Ho, int Wo,
                                                      float* __restrict__ dX) {
-  const long total = (long)B * H * W * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int x = (int)(t % W);
-    t /= W;
-    const int y = (int)(t % H), b = (int)(t / H);
-    float acc = 0.f;
+  const int lane = threadIdx.x & 63;
+  const int npix = B * H * W;
+  for (int px = blockIdx.x * 4 + (threadIdx.x >> 6); px < npix; px += gridDim.x * 4) {
+    const int x = px % W, t = px / W, y = t % H, b = t / H;
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
     for (int ky = 0; ky < k; ++ky) {
       const int ny = y + p - ky;
       if (ny < 0 || ny % s) continue;
@@ -54,14 +63,22 @@ __global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ d
         if (nx < 0 || nx % s) continue;
         const int ox = nx / s;
         if (ox >= Wo) continue;
-        acc += dcols[(((long)b * Ho + oy) * Wo + ox) * ldc + ((long)ky * k + kx) * C + c];
+        const float* src = dcols + (((long)b * Ho + oy) * Wo + ox) * ldc + (long)(ky * k + kx) * C;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = lane + 64 * j;
+          if (c < C) acc[j] += src[c];
+        }
       }
     }
-    dX[i] = acc;
+    float* dst = dX + (long)px * C;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = lane + 64 * j;
+      if (c < C) dst[c] = acc[j];
+    }
   }
 }
-
-int grid_for(long n) { return (int)std::min<long>((n + 255) / 256, 256L * 8 * 16); }
 
 }  // namespace
 
@@ -72,12 +89,13 @@ extern "C" int ivit_im2col(int x_dtype, const void* X, long B, long H, long W, l
                  "ivit_im2col: output size %ldx%ld does not match the conv geometry", Ho, Wo);
   IVIT_CHECK_ARG(ldc >= k * k * C, "ivit_im2col: ldc %ld < k*k*C", ldc);
   IVIT_CHECK_ARG(B * H * W * C < (1L << 40) && H < (1 << 30) && W < (1 << 30), "ivit_im2col: too large");
-  const long n = B * Ho * Wo * ldc;
-  const int g = grid_for(n);
+  IVIT_CHECK_ARG(B * Ho * Wo * k * k < (1L << 31) && B * H * W < (1L << 31), "ivit_im2col: too many pixel-taps");
+  const long pairs = B * Ho * Wo * k * k;
+  const int g = (int)std::min<long>((pairs + 3) / 4, 256L * 8 * 16);
   hipStream_t st = ivit_stream(stream);
 #define IVIT_I2C(TI, TO)                                                                                       \
   hipLaunchKernelGGL((im2col_kernel<TI, TO>), dim3(g), dim3(256), 0, st, (const TI*)X, (int)B, (int)H, (int)W, \
-                     (int)C, (int)k, (int)stride, (int)pad, (int)Ho, (int)Wo, (TO*)cols, ldc)
+                     (int)C, (int)k, (int)stride, (int)pad, (int)Ho, (int)Wo, (TO*)cols, ldc, (int)pairs)
   if (x_dtype == IVIT_F32 && cols_dtype == IVIT_BF16) IVIT_I2C(float, bf16);
   else if (x_dtype == IVIT_F32 && cols_dtype == IVIT_F32) IVIT_I2C(float, float);
   else if (x_dtype == IVIT_BF16 && cols_dtype == IVIT_BF16) IVIT_I2C(bf16, bf16);
@@ -93,8 +111,9 @@ extern "C" int ivit_col2im(const float* dcols, long ldc, long B, long H, long W,
   IVIT_CHECK_ARG(Ho == (H + 2 * pad - k) / stride + 1 && Wo == (W + 2 * pad - k) / stride + 1,
                  "ivit_col2im: output size does not match the conv geometry");
   IVIT_CHECK_ARG(ldc >= k * k * C, "ivit_col2im: ldc %ld < k*k*C", ldc);
-  const long n = B * H * W * C;
-  hipLaunchKernelGGL(col2im_kernel, dim3(grid_for(n)), dim3(256), 0, ivit_stream(stream), dcols, ldc, (int)B,
+  IVIT_CHECK_ARG(C <= 512 && B * H * W < (1L << 31), "ivit_col2im: C <= 512 channels");
+  const long npix = B * H * W;
+  hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)std::min<long>((npix + 3) / 4, 256L * 8 * 16)), dim3(256), 0, ivit_stream(stream), dcols, ldc, (int)B,
                      (int)H, (int)W, (int)C, (int)k, (int)stride, (int)pad, (int)Ho, (int)Wo, dX);
   IVIT_LAUNCH_CHECK();
   return 0;

@@ -2,9 +2,10 @@
 kernels. Same classes, constructor kwargs, attribute and state-dict names as the reference
 (model_cnn.py:7-150), so its checkpoints load and train_cnn.py / eval_cnn.py-style callers work.
 
-Every convolution (stride-2 5x5 / 3x3 / 1x1, stride-1 5x5) runs as ``ivit_im2col`` + the dense
-MFMA GEMMs (``ivit_linear_fwd`` / ``_dgrad`` / ``_wgrad``) on NHWC maps, backward through
-``ivit_col2im``; BatchNorm (+ ReLU, + residual) through the ``ivit_bn_*`` kernels; both heads as
+Stride-1 'same' convolutions (the 5x5 convs of every block after the first, the fusion 3x3s)
+run on the implicit-GEMM conv kernels (``ivit_conv_fwd`` / ``_dgrad`` / ``_wgrad``); the strided
+ones (stride-2 5x5 / 3x3 / 1x1, and any channel count not % 8, e.g. the 290-plane input) as
+``ivit_im2col`` + the dense MFMA GEMMs (``ivit_linear_*``), backward through ``ivit_col2im``; BatchNorm (+ ReLU, + residual) through the ``ivit_bn_*`` kernels; both heads as
 one GEMM over the fused feature map. Activations stay NHWC from the input permute to the heads.
 """
 from __future__ import annotations
@@ -94,8 +95,36 @@ class _BNFn(torch.autograd.Function):
                 None if dr is None else dr.view(shp))
 
 
+class _ConvSameFn(torch.autograd.Function):
+    """NHWC stride-1 'same' conv (k in {1, 3, 5}, Cin / Cout % 8): the implicit-GEMM kernels
+    (ivit_conv_fwd / _dgrad / _wgrad) read the taps straight from the map, no im2col copy."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cdt):
+        B, H, W, C = x.shape
+        Cout, _, k, _ = w.shape
+        xh = ops.cast(x.reshape(-1, C).contiguous(), tdtype(cdt))
+        wp = ops.pack_conv(w, cdt)
+        y = ops.conv_fwd(xh, B, H, W, wp, b, cdt, torch.float32)
+        ctx.save_for_backward(xh, wp)
+        ctx.meta = (B, H, W, C, Cout, k, cdt, b is not None)
+        return y.view(B, H, W, Cout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xh, wp = ctx.saved_tensors
+        B, H, W, C, Cout, k, cdt, has_b = ctx.meta
+        d2 = ops.cast(dy.reshape(-1, Cout).contiguous(), tdtype(cdt))
+        dx = ops.conv_dgrad(d2, B, H, W, wp, cdt, torch.float32).view(B, H, W, C) if ctx.needs_input_grad[0] else None
+        gp, db = ops.conv_wgrad(d2, xh, B, H, W, C, Cout, k, cdt, want_bias=has_b)
+        return dx, ops.unpack_conv_grad(gp, Cout, C, k), db, None
+
+
 def _conv(m: Conv2d, x, cdt):
-    return _ConvColsFn.apply(x, m.weight, m.bias, m.stride[0], m.padding[0], cdt)
+    k, s, p = m.kernel_size[0], m.stride[0], m.padding[0]
+    if s == 1 and p == k // 2 and k in (1, 3, 5) and x.shape[-1] % 8 == 0 and m.out_channels % 8 == 0:
+        return _ConvSameFn.apply(x, m.weight, m.bias, cdt)
+    return _ConvColsFn.apply(x, m.weight, m.bias, s, p, cdt)
 
 
 def _bn(m: BatchNorm2d, x, relu=False, resid=None):

@@ -69,6 +69,20 @@ def backbone_cfg(img_size=(GRID_HEIGHT_PX, GRID_WIDTH_PX)):
     }
 
 
+MODEL_SAVE_DIR_CNN = "./trained_models_cnn"
+FEATURE_MAP_STRIDE_CNN = 8  # train_cnn.py:42
+
+
+def cnn_backbone_cfg():
+    """train_cnn.py:32-40 (CNN_BACKBONE_CFG)."""
+    from model_cnn import BasicBlock as CNNBlock
+    return {'block': CNNBlock, 'lidar_input_channels': LIDAR_TOTAL_CHANNELS, 'map_input_channels': MAP_CHANNELS,
+            'lidar_s1_planes': 160, 'lidar_s2_planes': 192, 'lidar_s3_planes': 224,
+            'map_s1_planes': 32, 'map_s2_planes': 64, 'map_s3_planes': 96,
+            'fusion_block_planes': 512, 'fusion_block_layers': 2, 'num_blocks_per_stage': 2,
+            'res_block2_kernel_size': 5, 'fusion_block_kernel_size': 3}
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--synthetic", action="store_true", help="seeded synthetic BEV batches instead of TRAIN_DATA_DIR")
@@ -78,7 +92,7 @@ def parse_args(argv=None):
     ap.add_argument("--grid", type=str, default=f"{GRID_HEIGHT_PX}x{GRID_WIDTH_PX}")
     ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--bucket-mb", type=float, default=64.0)
-    ap.add_argument("--save-dir", type=str, default=MODEL_SAVE_DIR_VIT)
+    ap.add_argument("--save-dir", type=str, default=None)
     ap.add_argument("--no-save", action="store_true")
     ap.add_argument("--fresh-batches", action="store_true", help="draw a new synthetic batch every step")
     ap.add_argument("--augment", action="store_true",
@@ -86,23 +100,30 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def main(argv=None):
+def main(argv=None, variant="vit"):
+    """variant "vit" (train_vit.py) or "cnn" (train_cnn.py: IntentNetCNN, stride 8)."""
     args = parse_args(argv)
+    tag = "ViT" if variant == "vit" else "CNN"
+    if args.save_dir is None:
+        args.save_dir = MODEL_SAVE_DIR_VIT if variant == "vit" else MODEL_SAVE_DIR_CNN
     rank, local, world, device = init_distributed()
     if device.type != "cuda":
         raise RuntimeError("train_vit.py runs on the MI355X kernels: no ROCm GPU visible")
     H, W = (int(v) for v in args.grid.lower().split("x"))
-    cfg = backbone_cfg((H, W))
-    stride = int(cfg['vit_model_name_lidar'].split('_patch')[-1].split('_')[0]) * cfg.get('fusion_block_stride', 1)
+    if variant == "vit":
+        cfg = backbone_cfg((H, W))
+        stride = int(cfg['vit_model_name_lidar'].split('_patch')[-1].split('_')[0]) * cfg.get('fusion_block_stride', 1)
+    else:
+        cfg, stride = cnn_backbone_cfg(), FEATURE_MAP_STRIDE_CNN
     log = print if rank == 0 else (lambda *a, **k: None)
 
-    log("--- ViT Training Configuration ---")
+    log(f"--- {tag} Training Configuration ---")
     log(f"Device: {device} x {world} rank(s)")
     log(f"Training data: {'synthetic' if args.synthetic else TRAIN_DATA_DIR}")
-    log(f"BEV Image Size for ViT: {(H, W)}")
+    log(f"BEV Image Size for {tag}: {(H, W)}")
     log(f"Using Rotated IoU: {USE_ROTATED_IOU}")
     log(f"Batch Size: {args.batch}/GPU (global {args.batch * world}), Num Epochs: {args.epochs}, LR: {LEARNING_RATE}")
-    log(f"Feature Map Stride (ViT): {stride}")
+    log(f"Feature Map Stride ({tag}): {stride}")
     log(f"Apply Intention Downsampling: {APPLY_INTENTION_DOWNSAMPLING}")
     log(f"Compute dtype: {args.dtype}")
     log("---------------------------------")
@@ -120,7 +141,11 @@ def main(argv=None):
         log("Warning: Both USE_INTENTION_WEIGHTS and APPLY_INTENTION_DOWNSAMPLING are True. "
             "Downsampling will be applied; explicit weights will be ignored by the loss function.")
 
-    model = IntentNetViT(backbone_cfg=cfg).to(device)
+    if variant == "vit":
+        model = IntentNetViT(backbone_cfg=cfg).to(device)
+    else:
+        from model_cnn import IntentNetCNN
+        model = IntentNetCNN(backbone_cfg=cfg).to(device)
     model.set_compute_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     loss_fn = DetectionIntentionLoss(use_rotated_iou=USE_ROTATED_IOU, intention_class_weights=None,
                                      apply_intention_downsampling=APPLY_INTENTION_DOWNSAMPLING,
@@ -132,7 +157,7 @@ def main(argv=None):
     log(f"Anchors generated (stride {stride}), shape: {tuple(anchors.shape)}")
     trainer = Trainer(model, loss_fn, optimizer, anchors, world=world, bucket_mb=args.bucket_mb, check_nan=True)
 
-    log("\n--- Starting ViT Training ---")
+    log(f"\n--- Starting {tag} Training ---")
     for epoch in range(args.epochs):
         model.train()
         acc = torch.zeros(4, dtype=torch.float64, device=device)
@@ -155,15 +180,15 @@ def main(argv=None):
             scheduler.step(avg[0])
         else:
             log(f"Epoch {epoch + 1} Warning: No batches processed successfully.")
-    log("\n--- ViT Training Finished ---")
+    log(f"\n--- {tag} Training Finished ---")
 
     if rank == 0 and not args.no_save:
         save_dir = Path(args.save_dir)
         save_dir.mkdir(parents=True, exist_ok=True)
-        path = save_dir / "vit_model.pth"
+        path = save_dir / f"{variant}_model.pth"
         torch.save({'epoch': args.epochs, 'model_state_dict': model.state_dict(),
                     'optimizer_state_dict': optimizer.state_dict(), 'backbone_cfg': cfg}, path)
-        log(f"Saved final TRAINED ViT model to {path}")
+        log(f"Saved final TRAINED {tag} model to {path}")
     if world > 1:
         torch.distributed.destroy_process_group()
     return 0
