@@ -75,5 +75,10 @@ def test_train_cnn_synthetic_augmented_epoch_and_checkpoint(tmp_path):
     assert rc == 0
     ck = tmp_path / "cnn_model.pth"
     assert ck.is_file()
-    d = torch.load(str(ck), map_location="cpu", weights_only=False)
+    import eval_cnn
+    import eval_vit
+    d = eval_vit.load_checkpoint(str(ck), torch.device("cuda"))
     assert "backbone.lidar_stage1.0.conv1.weight" in d["model_state_dict"]
+    rc = eval_cnn.main_eval_cnn(["--synthetic", "--checkpoint", str(ck), "--batch", "2", "--batches", "1",
+                                 "--grid", "32x48"])
+    assert rc == 0

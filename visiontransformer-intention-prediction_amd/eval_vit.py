@@ -39,8 +39,12 @@ INFERENCE_BATCH_SIZE = 8
 NUM_WORKERS_EVAL = 0
 
 
+MODEL_SAVE_PATH_CNN = "./trained_models_cnn/cnn_model.pth"  # eval_cnn.py:19
+
+
 def load_checkpoint(path, device):
-    torch.serialization.add_safe_globals([model_vit.BasicBlock])
+    import model_cnn
+    torch.serialization.add_safe_globals([model_vit.BasicBlock, model_cnn.BasicBlock])
     return torch.load(path, map_location=device, weights_only=True)
 
 
@@ -62,7 +66,7 @@ def default_cfg(cfg: dict, grid):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--synthetic", action="store_true")
-    ap.add_argument("--checkpoint", type=str, default=MODEL_SAVE_PATH_VIT)
+    ap.add_argument("--checkpoint", type=str, default=None)
     ap.add_argument("--batch", type=int, default=INFERENCE_BATCH_SIZE)
     ap.add_argument("--batches", type=int, default=4, help="synthetic batches")
     ap.add_argument("--grid", type=str, default=f"{GRID_HEIGHT_PX}x{GRID_WIDTH_PX}")
@@ -87,40 +91,50 @@ def run_inference(model, loader, anchors, conf=CONFIDENCE_THRESHOLD, nms=NMS_IOU
     return results
 
 
-def main_eval_vit(argv=None):
+def main_eval_vit(argv=None, variant="vit"):
+    """variant "vit" (eval_vit.py) or "cnn" (eval_cnn.py: IntentNetCNN, stride 8)."""
     args = parse_args(argv)
+    tag = "ViT" if variant == "vit" else "CNN"
+    if args.checkpoint is None:
+        args.checkpoint = MODEL_SAVE_PATH_VIT if variant == "vit" else MODEL_SAVE_PATH_CNN
     if not torch.cuda.is_available():
         raise RuntimeError("eval_vit.py runs on the MI355X kernels: no ROCm GPU visible")
     device = torch.device("cuda")
     H, W = (int(v) for v in args.grid.lower().split("x"))
-    print("--- ViT Model Evaluation ---")
+    print(f"--- {tag} Model Evaluation ---")
     print(f"Torch version: {torch.__version__}, device: {torch.cuda.get_device_name(0)}")
     print(f"Evaluation using Rotated IoU for mAP/matching: {args.rotated}")
 
     ckpt = None
     if Path(args.checkpoint).is_file():
-        print(f"\nLoading TRAINED ViT Model from: {args.checkpoint}")
+        print(f"\nLoading TRAINED {tag} Model from: {args.checkpoint}")
         ckpt = load_checkpoint(args.checkpoint, device)
         cfg = ckpt.get('backbone_cfg')
         if not cfg:
-            print("ERROR: 'backbone_cfg' not found in ViT checkpoint.")
+            print(f"ERROR: 'backbone_cfg' not found in {tag} checkpoint.")
             return 1
     elif args.synthetic:
         print(f"No checkpoint at {args.checkpoint}: random-init weights (synthetic run)")
-        from train_vit import backbone_cfg
-        cfg = backbone_cfg((H, W))
+        from train_vit import backbone_cfg, cnn_backbone_cfg
+        cfg = backbone_cfg((H, W)) if variant == "vit" else cnn_backbone_cfg()
     else:
-        print(f"ERROR: ViT Model checkpoint not found at {args.checkpoint}")
+        print(f"ERROR: {tag} Model checkpoint not found at {args.checkpoint}")
         return 1
-    cfg = default_cfg(dict(cfg), (H, W))
-    model = IntentNetViT(backbone_cfg=cfg).to(device)
+    if variant == "vit":
+        cfg = default_cfg(dict(cfg), (H, W))
+        model = IntentNetViT(backbone_cfg=cfg).to(device)
+        img_size = tuple(cfg['img_size'])
+    else:
+        from model_cnn import IntentNetCNN
+        model = IntentNetCNN(backbone_cfg=dict(cfg)).to(device)
+        img_size = (H, W)
     if ckpt is not None:
         model.load_state_dict(ckpt['model_state_dict'])
     model.set_compute_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     model.eval()
 
     if args.synthetic:
-        loader = SyntheticBEVLoader(args.batch, args.batches, tuple(cfg['img_size']), rank=0, device=device,
+        loader = SyntheticBEVLoader(args.batch, args.batches, img_size, rank=0, device=device,
                                     resident=False)
     else:
         if not Path(VAL_DATA_DIR).is_dir():
@@ -128,11 +142,14 @@ def main_eval_vit(argv=None):
             return 1
         raise SystemExit("The Argoverse-2 dataset loader is outside this build's scope; use --synthetic")
 
-    stride = int(cfg.get('vit_model_name_lidar', 'vit_small_patch8_224').split('_patch')[-1].split('_')[0]) \
-        * cfg.get('fusion_block_stride', 1)
-    Hc, Wc = cfg['img_size']
+    if variant == "vit":
+        stride = int(cfg.get('vit_model_name_lidar', 'vit_small_patch8_224').split('_patch')[-1].split('_')[0]) \
+            * cfg.get('fusion_block_stride', 1)
+    else:
+        stride = 8  # eval_cnn.py: FEATURE_MAP_STRIDE_CNN
+    Hc, Wc = img_size
     anchors = generate_anchors(Hc, Wc, stride, ANCHOR_CONFIGS_PAPER, device=device)
-    print(f"Anchors for ViT evaluation generated (stride {stride}), shape: {tuple(anchors.shape)}")
+    print(f"Anchors for {tag} evaluation generated (stride {stride}), shape: {tuple(anchors.shape)}")
 
     t0 = time.perf_counter()
     results = run_inference(model, loader, anchors)
@@ -140,27 +157,27 @@ def main_eval_vit(argv=None):
     dt = time.perf_counter() - t0
     print(f"Collected results for {len(results)} samples ({len(results) / dt:.2f} samples/s incl. host transfer)")
 
-    print("\n--- ViT Detection Results (mAP) ---")
+    print(f"\n--- {tag} Detection Results (mAP) ---")
     maps = detection_map(results, DETECTION_IOU_THRESHOLDS, args.rotated)
     for t, v in maps.items():
-        print(f"ViT mAP @ IoU={t:.1f}: {v:.4f}")
+        print(f"{tag} mAP @ IoU={t:.1f}: {v:.4f}")
 
     mp, mg = intention_matches(results, IOU_THRESHOLD_FOR_INTENTION_MATCH, args.rotated)
     if mp:
         from sklearn.metrics import accuracy_score, f1_score
         labels = list(range(NUM_INTENTION_CLASSES))
-        print(f"\n--- ViT Intention Prediction Results (on TP detections @ IoU>={IOU_THRESHOLD_FOR_INTENTION_MATCH}) ---")
-        print(f"ViT Overall Accuracy: {accuracy_score(mg, mp):.4f}")
-        print(f"ViT F1 (Macro):   {f1_score(mg, mp, labels=labels, average='macro', zero_division=0):.4f}")
-        print(f"ViT F1 (Weighted): {f1_score(mg, mp, labels=labels, average='weighted', zero_division=0):.4f}")
+        print(f"\n--- {tag} Intention Prediction Results (on TP detections @ IoU>={IOU_THRESHOLD_FOR_INTENTION_MATCH}) ---")
+        print(f"{tag} Overall Accuracy: {accuracy_score(mg, mp):.4f}")
+        print(f"{tag} F1 (Macro):   {f1_score(mg, mp, labels=labels, average='macro', zero_division=0):.4f}")
+        print(f"{tag} F1 (Weighted): {f1_score(mg, mp, labels=labels, average='weighted', zero_division=0):.4f}")
         per = f1_score(mg, mp, labels=labels, average=None, zero_division=0)
-        print("ViT F1 (Per Class):")
+        print(f"{tag} F1 (Per Class):")
         for i in labels:
             print(f"  {INTENTIONS_MAP_REV.get(i, f'Class_{i}'):<20}: {per[i]:.4f}")
     else:
-        print(f"\nNo True Positive detections found for ViT model at IoU >= {IOU_THRESHOLD_FOR_INTENTION_MATCH} "
+        print(f"\nNo True Positive detections found for {tag} model at IoU >= {IOU_THRESHOLD_FOR_INTENTION_MATCH} "
               "to evaluate intention.")
-    print("\n--- Evaluation Script for ViT Finished ---")
+    print(f"\n--- Evaluation Script for {tag} Finished ---")
     return 0
 
 
