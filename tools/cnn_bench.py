@@ -28,13 +28,7 @@ m = IntentNetCNN().to(dev).set_compute_dtype(torch.bfloat16).train()
 
 
 def conv_flops():
-    fwd, first = 0.0, 0.0
-    hooks = []
-    from layers import Conv2d
-
-    def walk(mod, h, w, c_in, prefix=""):
-        return h, w
-    # analytic: walk the stages with their geometry
+    """Analytic conv + head FLOPs per sample: (fwd, fwd + bwd without the input layers' dgrads)."""
     tot = 0.0
     inputs = 0.0
     bb = m.backbone

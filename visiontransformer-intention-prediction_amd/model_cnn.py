@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 import ops
 from _lib import BF16, F32, dt, lib, ptr, stream, tdtype
-from constants import LIDAR_TOTAL_CHANNELS, MAP_CHANNELS, NUM_ANCHORS_PER_LOC, NUM_INTENTION_CLASSES
+from constants import LIDAR_TOTAL_CHANNELS, MAP_CHANNELS, NUM_INTENTION_CLASSES
 from heads import DetectionHead, IntentionHead
 from layers import BatchNorm2d, Conv2d, ReLU
 
