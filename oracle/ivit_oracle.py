@@ -31,12 +31,17 @@ DOMINANT = (0, 6, 7)  # iteration order of the reference's set({0, 7, 6}) for sm
 # --------------------------------------------------------------------------------------
 # ViT stream (timm VisionTransformer.forward_features semantics, model_vit.py:64,71,119)
 # --------------------------------------------------------------------------------------
-def vit_forward_features(sd, prefix, x, num_heads, depth, drop_path_scales=None, eps=1e-6):
+def vit_forward_features(sd, prefix, x, num_heads, depth, drop_path_scales=None, eps=1e-6, attn="explicit",
+                         checkpoint=False):
     """timm ``forward_features``: PatchEmbed conv k=s=patch → cat CLS → +pos_embed →
     ``depth`` pre-norm blocks (LN eps 1e-6, MHSA, exact-erf GELU MLP) → final LN.
 
     ``drop_path_scales``: optional list (per block) of (attn_scale[B], mlp_scale[B])
     standing in for timm DropPath's per-sample Bernoulli/keep_prob factors.
+    ``attn``: "explicit" materialises softmax(q kᵀ · d^-0.5) (the golden-pinned form);
+    "sdpa" calls ``F.scaled_dot_product_attention`` as timm's fused path does (timm
+    ``Attention.fused_attn``), used by the CPU baseline and by large-grid checks.
+    ``checkpoint``: recompute each block in backward (memory only; same arithmetic).
     """
     w = sd[prefix + "patch_embed.proj.weight"]
     p = w.shape[-1]
@@ -45,34 +50,46 @@ def vit_forward_features(sd, prefix, x, num_heads, depth, drop_path_scales=None,
     t = t.flatten(2).transpose(1, 2)
     cls = sd[prefix + "cls_token"].expand(B, -1, -1)
     t = torch.cat([cls, t], dim=1) + sd[prefix + "pos_embed"]
-    N = t.shape[1]
-    hd = D // num_heads
     for i in range(depth):
-        b = f"{prefix}blocks.{i}."
-        h = F.layer_norm(t, (D,), sd[b + "norm1.weight"], sd[b + "norm1.bias"], eps)
-        qkv = F.linear(h, sd[b + "attn.qkv.weight"], sd[b + "attn.qkv.bias"])
-        q, k, v = qkv.reshape(B, N, 3, num_heads, hd).permute(2, 0, 3, 1, 4).unbind(0)
-        s = (q @ k.transpose(-2, -1)) * (hd ** -0.5)
-        a = torch.softmax(s, dim=-1) @ v
-        a = a.transpose(1, 2).reshape(B, N, D)
-        a = F.linear(a, sd[b + "attn.proj.weight"], sd[b + "attn.proj.bias"])
-        if drop_path_scales is not None:
-            a = a * drop_path_scales[i][0].view(B, 1, 1)
-        t = t + a
-        h = F.layer_norm(t, (D,), sd[b + "norm2.weight"], sd[b + "norm2.bias"], eps)
-        h = F.gelu(F.linear(h, sd[b + "mlp.fc1.weight"], sd[b + "mlp.fc1.bias"]))
-        h = F.linear(h, sd[b + "mlp.fc2.weight"], sd[b + "mlp.fc2.bias"])
-        if drop_path_scales is not None:
-            h = h * drop_path_scales[i][1].view(B, 1, 1)
-        t = t + h
+        sc = None if drop_path_scales is None else drop_path_scales[i]
+        if checkpoint and torch.is_grad_enabled():
+            from torch.utils.checkpoint import checkpoint as _ckpt
+            t = _ckpt(_vit_block, sd, f"{prefix}blocks.{i}.", t, num_heads, sc, eps, attn, use_reentrant=False)
+        else:
+            t = _vit_block(sd, f"{prefix}blocks.{i}.", t, num_heads, sc, eps, attn)
     return F.layer_norm(t, (D,), sd[prefix + "norm.weight"], sd[prefix + "norm.bias"], eps)
 
 
-def _stream(sd, name, x, num_heads, depth, dps):
+def _vit_block(sd, b, t, num_heads, scales, eps, attn):
+    """timm Block: x + dp(attn(LN1 x)); x + dp(mlp(LN2 x)); qkv rows [q heads; k; v]."""
+    B, N, D = t.shape
+    hd = D // num_heads
+    h = F.layer_norm(t, (D,), sd[b + "norm1.weight"], sd[b + "norm1.bias"], eps)
+    qkv = F.linear(h, sd[b + "attn.qkv.weight"], sd[b + "attn.qkv.bias"])
+    q, k, v = qkv.reshape(B, N, 3, num_heads, hd).permute(2, 0, 3, 1, 4).unbind(0)
+    if attn == "sdpa":
+        a = F.scaled_dot_product_attention(q, k, v)
+    else:
+        s = (q @ k.transpose(-2, -1)) * (hd ** -0.5)
+        a = torch.softmax(s, dim=-1) @ v
+    a = a.transpose(1, 2).reshape(B, N, D)
+    a = F.linear(a, sd[b + "attn.proj.weight"], sd[b + "attn.proj.bias"])
+    if scales is not None:
+        a = a * scales[0].view(B, 1, 1).to(a)
+    t = t + a
+    h = F.layer_norm(t, (D,), sd[b + "norm2.weight"], sd[b + "norm2.bias"], eps)
+    h = F.gelu(F.linear(h, sd[b + "mlp.fc1.weight"], sd[b + "mlp.fc1.bias"]))
+    h = F.linear(h, sd[b + "mlp.fc2.weight"], sd[b + "mlp.fc2.bias"])
+    if scales is not None:
+        h = h * scales[1].view(B, 1, 1).to(h)
+    return t + h
+
+
+def _stream(sd, name, x, num_heads, depth, dps, attn="explicit", checkpoint=False):
     """model_vit.py:116-122 (_process_stream): drop CLS, adapter LN(eps 1e-5)→Linear→GELU,
     tokens → (B, C, Hf, Wf) with token n = gy*Wf + gx."""
     pre = f"backbone.vit_{name}."
-    tok = vit_forward_features(sd, pre, x, num_heads, depth, dps)[:, 1:]
+    tok = vit_forward_features(sd, pre, x, num_heads, depth, dps, attn=attn, checkpoint=checkpoint)[:, 1:]
     a = f"backbone.adapter_{name}."
     D = tok.shape[-1]
     y = F.layer_norm(tok, (D,), sd[a + "0.weight"], sd[a + "0.bias"], 1e-5)
@@ -112,7 +129,8 @@ def heads_forward(sd, feat, num_anchors=5, num_classes=8):
     return d[..., 0].reshape(B, -1, 1), d[..., 1:].reshape(B, -1, 6), it.reshape(B, -1, num_classes)
 
 
-def intentnet_forward(sd, lidar, map_bev, cfg, training=False, drop_path_scales=None):
+def intentnet_forward(sd, lidar, map_bev, cfg, training=False, drop_path_scales=None, attn="explicit",
+                      checkpoint=False):
     """IntentNetViT.forward (model_vit.py:179-185) → (cls (B,A·HW,1), box (B,A·HW,6), intent)."""
     from oracle.weights import VIT_ARCH
     al, am = VIT_ARCH[cfg["vit_lidar"]], VIT_ARCH[cfg["vit_map"]]
@@ -121,8 +139,8 @@ def intentnet_forward(sd, lidar, map_bev, cfg, training=False, drop_path_scales=
     dl = dm = None
     if drop_path_scales is not None:
         dl, dm = drop_path_scales
-    fl = _stream(sd, "lidar", lidar, al["num_heads"], depth_l, dl)
-    fm = _stream(sd, "map", map_bev, am["num_heads"], depth_m, dm)
+    fl = _stream(sd, "lidar", lidar, al["num_heads"], depth_l, dl, attn, checkpoint)
+    fm = _stream(sd, "map", map_bev, am["num_heads"], depth_m, dm, attn, checkpoint)
     feat = fusion_forward(sd, torch.cat([fl, fm], dim=1), cfg["layers"], training)
     return heads_forward(sd, feat, cfg["num_anchors"], cfg["num_classes"])
 

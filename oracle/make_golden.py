@@ -188,6 +188,97 @@ def gen_geometry():
     print("geometry: loss", rec["loss_full"], "ds", rec["loss_full_ds"], "nms keeps", keeps)
 
 
+def _loss_vec(d):
+    return np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]),
+                     float(d["num_pos_anchors"])])
+
+
+def gen_loss_options():
+    """The reference's OWN DetectionIntentionLoss (loss.py) on its non-default option paths:
+    * ``intention_class_weights`` with downsampling off (loss.py:40-45), full 400x720 anchors;
+    * ``use_rotated_iou=True`` (loss.py:81, utils.py:335-392 with the convex-clip Polygon
+      stand-in: GEOS absent) on an 80x120 grid (750 anchors, boxes inside its footprint);
+    * the NaN / Inf guard (loss.py:190-198): a NaN class logit, an +Inf class logit on a
+      negative anchor, an Inf intention logit on a positive anchor.
+    Records the loss dicts and, where a gradient flows, d loss / d logits (full arrays)."""
+    import loss as ref_loss
+    import utils as ref_utils
+    rec = {}
+    # --- class weights, full grid ---
+    anchors = ref_utils.generate_anchors(400, 720, 8)
+    NA = anchors.shape[0]
+    g = torch.Generator().manual_seed(31)
+    cls = torch.randn((2, NA, 1), generator=g)
+    box = 0.5 * torch.randn((2, NA, 6), generator=g)
+    it = torch.randn((2, NA, 8), generator=g)
+    _, _, gts = O.synthetic_batch(2, seed=2025, G=20)
+    cw = torch.tensor([0.3, 1.7, 2.5, 0.9, 1.2, 3.1, 0.5, 0.6], dtype=torch.float32)
+    for i, gg in enumerate(gts):
+        rec[f"cw_gt{i}_boxes"] = gg["boxes_xywha"].numpy()
+        rec[f"cw_gt{i}_ints"] = gg["intentions"].numpy()
+    ts = [t.clone().requires_grad_(True) for t in (cls, box, it)]
+    d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False, intention_class_weights=cw)(
+        *ts, anchors, gts)
+    d["loss"].backward()
+    rec.update(cw_seed=np.array([31]), cw_weights=cw.numpy(), cw_loss=_loss_vec(d),
+               cw_gcls=ts[0].grad.numpy(), cw_gbox=ts[1].grad.numpy(), cw_gint=ts[2].grad.numpy())
+    # weights given but downsampling on: the reference ignores the weights (loss.py:41-42)
+    torch.manual_seed(3)
+    d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=True, intention_class_weights=cw)(
+        cls, box, it, anchors, gts)
+    rec["cw_ds_loss_nods_terms"] = _loss_vec(d)[:3]  # cls / box terms do not depend on the draws
+    # --- rotated IoU, 80x120 grid ---
+    H, W = 80, 120
+    anchors = ref_utils.generate_anchors(H, W, 8)
+    NA = anchors.shape[0]
+    g = torch.Generator().manual_seed(41)
+    cls = torch.randn((2, NA, 1), generator=g)
+    box = 0.5 * torch.randn((2, NA, 6), generator=g)
+    it = torch.randn((2, NA, 8), generator=g)
+    ax, ay = anchors[:, 0], anchors[:, 1]
+    lo_x, hi_x, lo_y, hi_y = float(ax.min()), float(ax.max()), float(ay.min()), float(ay.max())
+    gts = []
+    for b, G in enumerate((8, 5)):
+        u = torch.rand((G, 5), generator=g)
+        boxes = torch.stack([lo_x + (hi_x - lo_x) * u[:, 0], lo_y + (hi_y - lo_y) * u[:, 1], 1.5 + 1.5 * u[:, 2],
+                             3.5 + 3.0 * u[:, 3], -math.pi + 2 * math.pi * u[:, 4]], 1).float()
+        if b == 0:  # two GTs exactly on anchors at yaw 0 / pi/2 (rotated IoU 1.0 on the matching anchor)
+            boxes[0] = anchors[37].clone()
+            boxes[1] = anchors[301].clone()
+        gts.append({"boxes_xywha": boxes, "intentions": torch.randint(0, 8, (G,), generator=g)})
+        rec[f"rot_gt{b}_boxes"] = boxes.numpy()
+        rec[f"rot_gt{b}_ints"] = gts[-1]["intentions"].numpy()
+    ts = [t.clone().requires_grad_(True) for t in (cls, box, it)]
+    d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False, use_rotated_iou=True)(
+        *ts, anchors, gts)
+    d["loss"].backward()
+    rec.update(rot_grid=np.array([H, W]), rot_anchors=anchors.numpy(), rot_cls=cls.numpy(), rot_box=box.numpy(),
+               rot_int=it.numpy(), rot_loss=_loss_vec(d), rot_gcls=ts[0].grad.numpy(),
+               rot_gbox=ts[1].grad.numpy(), rot_gint=ts[2].grad.numpy())
+    # axis-aligned on the same inputs, to show the option changes the result
+    d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False)(cls, box, it, anchors, gts)
+    rec["rot_axis_loss"] = _loss_vec(d)
+    # --- NaN / Inf guard (same 80x120 inputs) ---
+    iou = ref_utils.compute_axis_aligned_iou(anchors, gts[0]["boxes_xywha"])
+    pos_a = int(iou.max(dim=0)[1][0])  # force-matched positive of sample 0
+    neg_a = int(torch.nonzero(iou.max(dim=1)[0] < 0.45)[0])
+    cases = {"nan_cls": ("cls", 0, pos_a, 0, float("nan")), "inf_cls_neg": ("cls", 0, neg_a, 0, float("inf")),
+             "inf_int_pos": ("int", 0, pos_a, 3, float("inf"))}
+    for name, (which, b, a, k, v) in cases.items():
+        c2, b2, i2 = cls.clone(), box.clone(), it.clone()
+        (c2 if which == "cls" else i2)[b, a, k] = v
+        ts = [t.requires_grad_(True) for t in (c2, b2, i2)]
+        d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False)(*ts, anchors, gts)
+        leaf = d["loss"].grad_fn is None and d["loss"].requires_grad
+        d["loss"].backward()
+        rec[f"guard_{name}"] = np.array([b, a, k, v], np.float64)
+        rec[f"guard_{name}_loss"] = _loss_vec(d)
+        rec[f"guard_{name}_leaf"] = np.array([int(leaf), int(all(t.grad is None for t in ts))])
+    np.savez_compressed(os.path.join(OUT, "loss_options.npz"), **rec)
+    print("loss_options: cw", rec["cw_loss"], "rot", rec["rot_loss"], "axis", rec["rot_axis_loss"],
+          "guard", {k: rec[f"guard_{k}_loss"].tolist() + rec[f"guard_{k}_leaf"].tolist() for k in cases})
+
+
 def _sparse(bev):
     flat = bev.reshape(-1)
     nz = np.flatnonzero(flat != 0)  # NaN != 0: NaN cells are kept

@@ -44,17 +44,19 @@ class Toy(nn.Module):
         return o[:, :1], o[:, 1:7], o[:, 7:]
 
 
-def _data(rank, step, nan=False):
+def _data(rank, step, nan=False, inf_loss=False):
     g = torch.Generator().manual_seed(100 * step + rank)
     x = torch.randn(6, 8, generator=g)
     m = torch.randn(6, 4, generator=g)
     if nan:
         x[0, 0] = float("nan")
-    return {"lidar_bev": x, "map_bev": m, "gt_list": [None] * 6}
+    return {"lidar_bev": x, "map_bev": m, "gt_list": ["inf" if inf_loss else None] * 6}
 
 
 def _loss(c, b, i, anchors, gts):
     loss = c.square().mean() + 0.5 * b.abs().mean() + i.sin().sum() * 0.1
+    if gts is not None and gts[0] == "inf":
+        loss = loss + float("inf")
     z = loss.detach()
     return {"loss": loss, "cls_loss": z, "box_loss": z, "intent_loss": z, "num_pos_anchors": torch.tensor(0)}
 
@@ -110,17 +112,63 @@ def _trainer_worker(rank, world, port):
     model = Toy()
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
     tr = Trainer(model, _loss, opt, anchors=None, world=world, bucket_mb=0.001, check_nan=True)
-    # step 0 normal, step 1 NaN on rank 1 only → skipped on every rank, step 2 normal
+    # step 0 normal, step 1 NaN on rank 1 only → skipped on every rank, step 2 normal,
+    # step 3 non-finite loss on rank 0 only → no update on any rank (loss.py:190-198)
     outs = []
     for step in range(3):
         outs.append(tr.step(_data(rank, step, nan=(step == 1 and rank == 1))))
     assert outs[0] is not None and outs[1] is None and outs[2] is not None
     assert tr.skipped == 1
+    before = [p.detach().clone() for p in model.parameters()]
+    st_before = {k: v.clone() if torch.is_tensor(v) else v for k, v in opt.state_dict()["state"][0].items()}
+    d = tr.step(_data(rank, 3, inf_loss=(rank == 0)))
+    assert d is not None and tr.nonfinite == 1
+    assert all(torch.equal(a, p.detach()) for a, p in zip(before, model.parameters()))
+    st_after = opt.state_dict()["state"][0]
+    assert all(torch.equal(torch.as_tensor(st_before[k]), torch.as_tensor(st_after[k])) for k in st_before)
     flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
     other = flat.clone()
     dist.broadcast(other, 0)
     assert torch.equal(flat, other)
     dist.destroy_process_group()
+
+
+def _broadcast_sched_worker(rank, world, port):
+    """Replicas built from different seeds are made identical by Trainer (broadcast from rank
+    0), and ReduceLROnPlateau stepped on the global epoch mean (train_vit.py) keeps the LR,
+    and so the replicas, identical although each rank sees different data and losses."""
+    _init(rank, world, port)
+    from ddp import all_reduce_sum
+    from trainer import Trainer
+    torch.manual_seed(rank)
+    model = Toy()
+    model.n.weight.data.add_(rank)  # parameters AND ...
+    model.register_buffer("stat", torch.full((3,), float(rank)))  # ... buffers differ per rank
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=1e-4)
+    sched = torch.optim.lr_scheduler.ReduceLROnPlateau(opt, mode="min", factor=0.1, patience=0)
+    tr = Trainer(model, _loss, opt, anchors=None, world=world, bucket_mb=0.001, check_nan=True)
+    assert float(model.stat.sum()) == 0.0
+    for epoch in range(4):
+        acc, n = 0.0, 0
+        for step in range(2):
+            d = tr.step(_data(rank, 10 * epoch + step))
+            acc += float(d["loss"]) * (1 + 5 * rank)  # rank-dependent epoch losses
+            n += 1
+        tot = all_reduce_sum([acc, n], torch.device("cpu"))
+        sched.step(tot[0] / tot[1])
+    lrs = torch.tensor([opt.param_groups[0]["lr"]], dtype=torch.float64)
+    other = lrs.clone()
+    dist.broadcast(other, 0)
+    assert torch.equal(lrs, other)
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    other = flat.clone()
+    dist.broadcast(other, 0)
+    assert torch.equal(flat, other)
+    dist.destroy_process_group()
+
+
+def test_broadcast_and_global_plateau_schedule():
+    mp.spawn(_broadcast_sched_worker, args=(2, _port()), nprocs=2, join=True)
 
 
 def _any_rank_worker(rank, world, port):

@@ -134,3 +134,76 @@ def test_rotated_iou():
     got = O.rotated_iou_numpy(z["rot_b1"], z["rot_b2"])
     np.testing.assert_allclose(got, z["rot_iou"], atol=1e-6)
     assert np.all(got[3] == 0)
+
+
+def _opt_logits(seed, NA):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn((2, NA, 1), generator=g), 0.5 * torch.randn((2, NA, 6), generator=g),
+            torch.randn((2, NA, 8), generator=g))
+
+
+def _opt_gts(z, pre, n=2):
+    return [{"boxes_xywha": torch.from_numpy(z[f"{pre}_gt{i}_boxes"]),
+             "intentions": torch.from_numpy(z[f"{pre}_gt{i}_ints"])} for i in range(n)]
+
+
+def _rot_iou(a, b):
+    return torch.from_numpy(O.rotated_iou_numpy(a.detach().float().numpy(), b.detach().float().numpy()))
+
+
+def _vec(d):
+    return np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]),
+                     float(d["num_pos_anchors"])])
+
+
+def test_loss_class_weights_vs_golden():
+    """loss.py:40-45: intention_class_weights with downsampling off (full 400x720 anchors)."""
+    z = golden("loss_options.npz")
+    anchors = O.generate_anchors(400, 720, 8)
+    ts = [t.requires_grad_(True) for t in _opt_logits(int(z["cw_seed"][0]), anchors.shape[0])]
+    d = O.detection_loss(*ts, anchors, _opt_gts(z, "cw"), downsampling=False,
+                         class_weights=torch.from_numpy(z["cw_weights"]))
+    np.testing.assert_allclose(_vec(d), z["cw_loss"], rtol=1e-5)
+    d["loss"].backward()
+    for t, k in zip(ts, ("cw_gcls", "cw_gbox", "cw_gint")):
+        np.testing.assert_allclose(t.grad.numpy(), z[k], rtol=1e-4, atol=1e-6 * np.abs(z[k]).max())
+
+
+def test_loss_rotated_iou_vs_golden():
+    """loss.py:81 use_rotated_iou=True (80x120 grid, GEOS restated as f64 convex clipping)."""
+    z = golden("loss_options.npz")
+    anchors = torch.from_numpy(z["rot_anchors"])
+    assert np.array_equal(O.generate_anchors(80, 120, 8).numpy(), z["rot_anchors"])
+    ts = [torch.from_numpy(z[k]).clone().requires_grad_(True) for k in ("rot_cls", "rot_box", "rot_int")]
+    d = O.detection_loss(*ts, anchors, _opt_gts(z, "rot"), downsampling=False, iou_fn=_rot_iou)
+    np.testing.assert_allclose(_vec(d), z["rot_loss"], rtol=1e-5)
+    assert not np.allclose(z["rot_loss"], z["rot_axis_loss"])
+    d["loss"].backward()
+    for t, k in zip(ts, ("rot_gcls", "rot_gbox", "rot_gint")):
+        np.testing.assert_allclose(t.grad.numpy(), z[k], rtol=1e-4, atol=1e-6 * np.abs(z[k]).max())
+
+
+@pytest.mark.parametrize("case", ["nan_cls", "inf_cls_neg", "inf_int_pos"])
+def test_loss_guard_vs_golden(case):
+    """loss.py:190-198: a non-finite total returns zeros and a disconnected leaf (no gradient)."""
+    z = golden("loss_options.npz")
+    anchors = torch.from_numpy(z["rot_anchors"])
+    b, a, k, v = z[f"guard_{case}"]
+    ts = [torch.from_numpy(z[n]).clone() for n in ("rot_cls", "rot_box", "rot_int")]
+    ts[0 if case.endswith(("cls", "cls_neg")) else 2][int(b), int(a), int(k)] = v
+    ts = [t.requires_grad_(True) for t in ts]
+    d = O.detection_loss(*ts, anchors, _opt_gts(z, "rot"), downsampling=False)
+    np.testing.assert_array_equal(_vec(d), z[f"guard_{case}_loss"])
+    d["loss"].backward()
+    assert all(t.grad is None for t in ts) and bool(z[f"guard_{case}_leaf"][1])
+
+
+def test_forward_sdpa_variant_matches_golden(small):
+    """The oracle's timm-fused-path variant (F.scaled_dot_product_attention, used by the CPU
+    baseline and the large-grid checks) against the same reference goldens."""
+    z, cfg, sd, lidar, mp = small
+    sd = {k: v.clone() for k, v in sd.items()}
+    with torch.no_grad():
+        c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=False, attn="sdpa")
+    for got, key in ((c, "eval_cls"), (b, "eval_box"), (i, "eval_int")):
+        np.testing.assert_allclose(got.numpy(), z[key], rtol=1e-4, atol=1e-4)

@@ -204,7 +204,15 @@ __global__ __launch_bounds__(LB) void loss_bwd_kernel(const float* __restrict__ 
                                                       float* dcls, float* dbox, float* dint) {
   const long i = (long)blockIdx.x * LB + threadIdx.x;
   if (i >= total) return;
-  const float go = (grad_loss ? grad_loss[0] : 1.f) * stats[ST_FINITE];
+  if (stats[ST_FINITE] == 0.f) {
+    // loss.py:190-198 returns a disconnected zero leaf: no gradient reaches the logits. Write
+    // exact zeros (a non-finite per-anchor gradient times 0 would be NaN).
+    dcls[i] = 0.f;
+    for (int k = 0; k < 6; ++k) dbox[i * 6 + k] = 0.f;
+    for (int k = 0; k < K; ++k) dint[i * K + k] = 0.f;
+    return;
+  }
+  const float go = grad_loss ? grad_loss[0] : 1.f;
   const float cden = stats[ST_CDEN], iden = stats[ST_IDEN];
   const int code = tgt[i];
   const int t = (code & 3) - 1, it = (code >> 2) - 1;

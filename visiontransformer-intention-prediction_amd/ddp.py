@@ -181,6 +181,25 @@ class GradBuckets:
         self._hooks = []
 
 
+@torch.no_grad()
+def broadcast_state(module, src: int = 0, group=None):
+    """Copy rank ``src``'s parameters and buffers (BN running stats included) to every rank,
+    as DistributedDataParallel does at construction; a no-op without a process group."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return
+    for t in list(module.parameters()) + list(module.buffers()):
+        dist.broadcast(t.data, src, group=group)
+
+
+def all_reduce_sum(values, device, group=None):
+    """Sum a list of floats over ranks (f64); returns the list unchanged without a group."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return [float(v) for v in values]
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    dist.all_reduce(t, group=group)
+    return t.tolist()
+
+
 def any_rank(flag: bool, device, group=None) -> bool:
     """Collective OR of a per-rank condition (the train loop's NaN skip must be taken by every
     rank together, or the next bucketed all-reduce would pair different steps)."""

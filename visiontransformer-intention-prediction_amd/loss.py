@@ -59,6 +59,7 @@ class DetectionIntentionLoss(nn.Module):
             w = torch.as_tensor(intention_class_weights, dtype=torch.float32)
         self.register_buffer("final_intention_class_weights", w)
         self.keep_generator = None
+        self.last_finite = None
 
     def _cfg(self, device):
         dom = 0
@@ -88,5 +89,8 @@ class DetectionIntentionLoss(nn.Module):
         box = box_preds.float().reshape(B, NA, 6)
         it = intention_logits.float().reshape(B, NA, -1)
         loss, stats = ops.DetLossFn.apply(cls, box, it, anchors, gt, ng, gi, keep, self._cfg(dev))
+        # 1.0 / 0.0 on device: 0 means the guard of loss.py:190-198 fired (loss and terms are 0,
+        # and the backward writes exact zero gradients); trainer.Trainer skips the update on it
+        self.last_finite = stats[9].detach()
         return {"loss": loss, "cls_loss": stats[6].detach(), "box_loss": stats[7].detach(),
                 "intent_loss": stats[8].detach(), "num_pos_anchors": stats[3].detach().round().long()}

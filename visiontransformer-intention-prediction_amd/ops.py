@@ -594,7 +594,8 @@ class NeckFn(torch.autograd.Function):
 
 class DetLossFn(torch.autograd.Function):
     """DetectionIntentionLoss on device (loss.py:58-206). Returns the 16-float stats vector;
-    element 5 is the loss (0 with no gradient when non-finite, loss.py:190-198)."""
+    element 5 is the loss (0 with no gradient when non-finite, loss.py:190-198); element 9 is
+    the finite flag (1.0 / 0.0) the Trainer reads to skip backward + optimizer step."""
 
     @staticmethod
     def forward(ctx, cls, box, intent, anchors, gt, ngt, gint, keep, cfg):

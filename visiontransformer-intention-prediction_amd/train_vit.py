@@ -26,7 +26,7 @@ import torch
 
 from constants import (ANCHOR_CONFIGS_PAPER, DOMINANT_CLASSES_FOR_DOWNSAMPLING, GRID_HEIGHT_PX, GRID_WIDTH_PX,
                        INTENTION_DOWNSAMPLE_RATIO, LIDAR_TOTAL_CHANNELS, MAP_CHANNELS)
-from ddp import init_distributed
+from ddp import all_reduce_sum, init_distributed
 from loss import DetectionIntentionLoss
 from model_vit import BasicBlock, IntentNetViT
 from optim import FusedAdamW
@@ -172,11 +172,15 @@ def main(argv=None, variant="vit"):
             n_ok += 1
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        # global epoch mean over ranks: every rank steps ReduceLROnPlateau on the same value, so
+        # the LR (and with it the all-reduced update) stays identical across replicas
+        tot = all_reduce_sum(acc.tolist() + [n_ok], device)
+        acc, n_ok = torch.tensor(tot[:4], dtype=torch.float64), int(round(tot[4]))
         if n_ok > 0:
             avg = (acc / n_ok).tolist()
             log(f"Epoch {epoch + 1} Summary: Avg Loss: {avg[0]:.4f} (Cls: {avg[1]:.4f}, Box: {avg[2]:.4f}, "
                 f"Intent: {avg[3]:.4f}) LR: {optimizer.param_groups[0]['lr']:.1e}  "
-                f"[{n_ok * args.batch * world / dt:.1f} samples/s]")
+                f"[{n_ok * args.batch / dt:.1f} samples/s]")
             scheduler.step(avg[0])
         else:
             log(f"Epoch {epoch + 1} Warning: No batches processed successfully.")

@@ -1,17 +1,27 @@
 """One IntentNetViT training step — the loop body of train_vit.py:151-187 — shared by
 train_vit.py and bench.py.
 
-zero_grad → forward → (NaN skip) → DetectionIntentionLoss → (NaN skip) → backward (gradient
-buckets all-reduce while it runs when world > 1) → FusedAdamW. The NaN skips are taken
-collectively across ranks (ddp.any_rank) so every rank stays on the same step; they cost one
-host sync each, as the reference's ``torch.isnan(...)`` checks do, and the benchmark turns
-them off (``check_nan=False``) — nothing else in the step is skipped.
+zero_grad → forward → (NaN skip) → DetectionIntentionLoss → (non-finite-loss no-op) → backward
+(gradient buckets all-reduce while it runs when world > 1) → FusedAdamW.
+
+* NaN in the model outputs skips the batch (train_vit.py:160-162): ``step`` returns None.
+* A non-finite total loss comes back from the loss as a zero (loss.py:190-198 returns a
+  disconnected zero leaf): the reference's ``loss.backward()`` then produces no gradient and
+  ``optimizer.step()`` updates nothing (AdamW skips parameters whose ``.grad`` is None, step
+  counters included). Here backward and the optimizer step are skipped outright, so the
+  weights, the Adam moments and the step counters stay bit-identical; the zero loss dict is
+  returned, and the caller accumulates it as the reference's loop does.
+
+Both checks are taken collectively across ranks (ddp.any_rank) so every rank stays on the same
+step; under DDP one rank's non-finite loss therefore skips the update on every rank (the
+replicas stay identical). They cost one host sync each, as the reference's ``torch.isnan``
+checks do; the benchmark turns them off (``check_nan=False``) — nothing else is skipped.
 """
 from __future__ import annotations
 
 import torch
 
-from ddp import GradBuckets, any_rank
+from ddp import GradBuckets, any_rank, broadcast_state
 
 
 class Trainer:
@@ -20,8 +30,12 @@ class Trainer:
         self.model, self.loss_fn, self.optimizer, self.anchors = model, loss_fn, optimizer, anchors
         self.world = world
         self.check_nan = check_nan
+        if world > 1:
+            # identical replicas from the first step, whatever each rank's RNG did
+            broadcast_state(model)
         self.buckets = GradBuckets(model.parameters(), bucket_mb) if world > 1 else None
         self.skipped = 0
+        self.nonfinite = 0
 
     def zero_grad(self):
         if self.buckets is not None:
@@ -29,8 +43,14 @@ class Trainer:
         else:
             self.optimizer.zero_grad(set_to_none=True)
 
+    def _loss_finite(self, d):
+        fin = getattr(self.loss_fn, "last_finite", None)
+        if fin is None:
+            return bool(torch.isfinite(d["loss"]).all())
+        return bool(fin) and not bool(torch.isnan(d["loss"]))
+
     def step(self, batch: dict):
-        """Returns the loss dict, or None when the batch was skipped (NaN outputs or loss)."""
+        """Returns the loss dict, or None when the batch was skipped (NaN in the outputs)."""
         lidar, mp, gts = batch["lidar_bev"], batch["map_bev"], batch["gt_list"]
         self.zero_grad()
         cls, box, intent = self.model(lidar, mp)
@@ -41,9 +61,9 @@ class Trainer:
                 self.skipped += 1
                 return None
         d = self.loss_fn(cls, box, intent, self.anchors, gts)
-        if self.check_nan and any_rank(bool(torch.isnan(d["loss"])), dev):
-            self.skipped += 1
-            return None
+        if self.check_nan and any_rank(not self._loss_finite(d), dev):
+            self.nonfinite += 1
+            return d
         d["loss"].backward()
         if self.buckets is not None:
             self.buckets.finish()

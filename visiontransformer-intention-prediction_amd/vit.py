@@ -54,15 +54,26 @@ class Block(nn.Module):
         self.norm2 = LayerNorm(dim, eps=1e-6)
         self.mlp = Mlp(dim, int(dim * mlp_ratio))
         self.drop_path_rate = drop_path
+        # injection hook (parity tests): (attn_scale[B], mlp_scale[B]) used instead of the drawn
+        # masks while training; the same per-sample factors oracle.vit_forward_features takes
+        self.drop_path_scales = None
+        self.last_scales = (None, None)
 
     def _scales(self, B, device):
-        """timm DropPath: per-sample Bernoulli(1-p) / (1-p), independent per branch."""
+        """timm DropPath: per-sample Bernoulli(1-p) / (1-p), independent per branch (identity
+        in eval mode or at p = 0)."""
         p = self.drop_path_rate
         if not self.training or p <= 0.0:
+            self.last_scales = (None, None)
             return None, None
-        keep = 1.0 - p
-        s = torch.empty((2, B), device=device).bernoulli_(keep).div_(keep)
-        return s[0].contiguous(), s[1].contiguous()
+        if self.drop_path_scales is not None:
+            s = torch.stack([torch.as_tensor(v, dtype=torch.float32).reshape(B) for v in self.drop_path_scales])
+            s = s.to(device)
+        else:
+            keep = 1.0 - p
+            s = torch.empty((2, B), device=device).bernoulli_(keep).div_(keep)
+        self.last_scales = (s[0].contiguous(), s[1].contiguous())
+        return self.last_scales
 
     def forward_flat(self, x, B, N, cdt):
         s1, s2 = self._scales(B, x.device)
@@ -93,6 +104,12 @@ class VisionTransformer(nn.Module):
         self.head = nn.Identity()
         nn.init.normal_(self.cls_token, std=1e-6)
         self.compute_dtype = torch.float32
+
+    def set_drop_path_scales(self, scales):
+        """Inject per-block DropPath factors: a list (one per block) of (attn_scale[B],
+        mlp_scale[B]), or None to draw them again (timm semantics)."""
+        for i, blk in enumerate(self.blocks):
+            blk.drop_path_scales = None if scales is None else scales[i]
 
     def _cdt(self):
         return BF16 if self.compute_dtype == torch.bfloat16 else F32
