@@ -226,15 +226,34 @@ def test_drop_path_injected_vs_oracle():
     m(lidar.to(DEV), mp.to(DEV))
     p11 = m.backbone.vit_map.blocks[11].drop_path_rate
     vals = set(torch.cat(m.backbone.vit_map.blocks[11].last_scales).cpu().tolist())
-    assert vals <= {0.0, pytest.approx(1.0 / (1.0 - p11))}
+    assert all(v == 0.0 or abs(v - 1.0 / (1.0 - p11)) < 1e-6 for v in vals), vals
 
 
-def _bf16_vs_oracle(H, W, B, seed, dp, attn, checkpoint, tol):
-    """bf16 HIP train step vs the f32 oracle on the same inputs / weights / DropPath factors:
-    outputs, loss terms and per-parameter gradient norms. The oracle (plain PyTorch f32,
-    pinned to the reference goldens on the CPU) is evaluated on the GPU with torch's own
-    kernels (hipBLASLt GEMMs, torch SDPA) — independent of this build's kernels — because the
-    full-grid f32 step does not fit a CPU test budget."""
+def _oracle_step(cfg, lidar, mp, gts, keep, sc, attn, checkpoint, autocast):
+    """The oracle's train step (forward, loss, backward) on the GPU with torch's own kernels:
+    f32, or under torch.autocast(bf16) — the reference's mixed-precision form (timm's fused
+    SDPA + bf16 linears / convs, f32 LayerNorm / softmax stats / loss)."""
+    sd = {k: (v.clone().to(DEV).requires_grad_(True) if v.is_floating_point() and "running" not in k
+              else v.clone().to(DEV)) for k, v in make_state_dict(cfg, seed=0).items()}
+    scd = None if sc is None else tuple([(a.to(DEV), b_.to(DEV)) for a, b_ in s] for s in sc)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        rc, rb, ri = O.intentnet_forward(sd, lidar.to(DEV), mp.to(DEV), cfg, training=True, drop_path_scales=scd,
+                                         attn=attn, checkpoint=checkpoint)
+    rc, rb, ri = rc.float(), rb.float(), ri.float()
+    anchors = O.generate_anchors(*cfg["img_size"])
+    rd = O.detection_loss(rc.cpu(), rb.cpu(), ri.cpu(), anchors, gts, downsampling=True, keep=keep)
+    rd["loss"].backward()
+    return (rc.detach(), rb.detach(), ri.detach()), rd, {k: v.grad for k, v in sd.items() if v.grad is not None}
+
+
+def _bf16_vs_oracle(H, W, B, seed, dp, attn, checkpoint, slack):
+    """bf16 HIP train step vs the f32 oracle on the same inputs / weights / DropPath factors
+    (outputs, loss terms, every parameter gradient), judged against the error the reference's
+    own bf16 mixed precision (the oracle under torch.autocast, torch's kernels) makes vs the
+    same f32 oracle: ours must stay within ``slack`` x that error (+ a small floor). The oracle
+    (plain PyTorch, pinned to the reference goldens on the CPU) runs on the GPU with torch's
+    kernels — independent of this build's — because the full-grid f32 step does not fit a CPU
+    test budget. Returns (errors, autocast errors, per-parameter (ours, autocast) grad errors)."""
     import loss as L
     import utils
     torch.backends.cuda.matmul.allow_tf32 = False
@@ -250,45 +269,51 @@ def _bf16_vs_oracle(H, W, B, seed, dp, attn, checkpoint, tol):
     c, b, i = m(lidar.to(DEV), mp.to(DEV))
     d = L.DetectionIntentionLoss()(c, b, i, anchors, gts, intent_keep=keep)
     d["loss"].backward()
-    sd = {k: (v.clone().to(DEV).requires_grad_(True) if v.is_floating_point() and "running" not in k
-              else v.clone().to(DEV)) for k, v in make_state_dict(cfg, seed=0).items()}
-    scd = None if sc is None else tuple([(a.to(DEV), b_.to(DEV)) for a, b_ in s] for s in sc)
-    rc, rb, ri = O.intentnet_forward(sd, lidar.to(DEV), mp.to(DEV), cfg, training=True, drop_path_scales=scd,
-                                     attn=attn, checkpoint=checkpoint)
-    rd = O.detection_loss(rc.cpu(), rb.cpu(), ri.cpu(), anchors.cpu(), gts, downsampling=True, keep=keep)
-    rd["loss"].backward()
-    errs = {"cls": _rel(c.detach(), rc.detach()), "box": _rel(b.detach(), rb.detach()),
-            "int": _rel(i.detach(), ri.detach())}
-    for k in ("loss", "cls_loss", "box_loss", "intent_loss"):
-        errs[k] = abs(float(d[k]) - float(rd[k])) / max(abs(float(rd[k])), 1e-12)
-    assert int(d["num_pos_anchors"]) == int(rd["num_pos_anchors"])
-    gn = []
-    for k, p in m.named_parameters():
-        r = sd[k].grad
-        gn.append((float((p.grad.double() - r.double()).norm() / (r.double().norm() + 1e-30)), k))
-    gn.sort(reverse=True)
-    print(f"bf16 vs f32 oracle {H}x{W} B={B}:", errs, "worst grad rel-L2:", gn[:4])
-    assert errs["cls"] < tol["out"] and errs["box"] < tol["out"] and errs["int"] < tol["out"], errs
-    assert all(errs[k] < tol["loss"] for k in ("loss", "cls_loss", "box_loss", "intent_loss")), errs
-    assert gn[0][0] < tol["grad"], gn[:6]
-    return errs, gn
+    ours = ((c.detach(), b.detach(), i.detach()), d, {k: p.grad for k, p in m.named_parameters()})
+    del m
+    ref = _oracle_step(cfg, lidar, mp, gts, keep, sc, attn, checkpoint, autocast=False)
+    amp = _oracle_step(cfg, lidar, mp, gts, keep, sc, "sdpa", checkpoint, autocast=True)
+
+    def errs(run):
+        e = {k: _rel(x, y) for k, x, y in zip(("cls", "box", "int"), run[0], ref[0])}
+        for k in ("loss", "cls_loss", "box_loss", "intent_loss"):
+            e[k] = abs(float(run[1][k]) - float(ref[1][k])) / max(abs(float(ref[1][k])), 1e-12)
+        return e
+
+    e_ours, e_amp = errs(ours), errs(amp)
+    assert int(d["num_pos_anchors"]) == int(ref[1]["num_pos_anchors"])
+    gn = {}
+    for k, r in ref[2].items():
+        rn = r.double().norm() + 1e-30
+        gn[k] = (float((ours[2][k].double() - r.double()).norm() / rn), float((amp[2][k].double() - r.double()).norm() / rn))
+    worst = sorted(((o / (a + 1e-3), o, a, k) for k, (o, a) in gn.items()), reverse=True)
+    print(f"bf16 vs f32 oracle {H}x{W} B={B}: ours", e_ours, "\n  torch autocast bf16", e_amp,
+          "\n  worst grad rel-L2 (ratio, ours, autocast, name):", worst[:5],
+          "\n  max grad rel-L2 ours", max(o for o, _ in gn.values()), "autocast", max(a for _, a in gn.values()))
+    for k in e_ours:
+        assert e_ours[k] <= slack * e_amp[k] + 2e-3, (k, e_ours, e_amp)
+    for k, (o, a) in gn.items():
+        assert o <= slack * a + 1e-2, (k, o, a)
+    return e_ours, e_amp, gn
 
 
-# bf16 tolerances, measured (profiles/r02_bf16_parity.txt) with ~2x headroom: bf16 operands
-# (8-bit mantissa) through 12 blocks + patch embed over K = 18560
-BF16_TOL = {"out": 6e-2, "loss": 2e-2, "grad": 8e-2}
+# ours may be at most 1.5x the error of torch's own bf16 autocast path vs the f32 oracle
+# (+ 2e-3 on outputs / losses, + 1e-2 on gradient rel-L2): bf16 noise, not a kernel defect.
+# Measured (profiles/r02_bf16_parity.txt): ours is below autocast on every output / loss term
+# and on nearly every gradient (400x720: outputs 2.0e-2 vs 2.7e-2, worst grad 0.17 vs 0.20).
+BF16_SLACK = 1.5
 
 
 def test_full_grid_bf16_train_step_vs_oracle():
     """BASELINE config 2 shape (400x720, real channels / depth / width), B=2, bf16, DropPath 0.1
     injected: outputs, loss and every parameter gradient vs the f32 oracle."""
-    _bf16_vs_oracle(400, 720, 2, 1234, 0.1, "explicit", False, BF16_TOL)
+    _bf16_vs_oracle(400, 720, 2, 1234, 0.1, "explicit", False, BF16_SLACK)
 
 
 def test_large_grid_bf16_train_step_vs_oracle():
     """BASELINE config 5 shape (800x1440, N = 18001 tokens, 90000 anchors), B=1, bf16: vs the
     f32 oracle (SDPA attention, per-block checkpointing for memory)."""
-    _bf16_vs_oracle(800, 1440, 1, 1234, 0.1, "sdpa", True, BF16_TOL)
+    _bf16_vs_oracle(800, 1440, 1, 1234, 0.1, "sdpa", True, BF16_SLACK)
 
 
 def test_full_grid_bf16_fused_adamw_step():
