@@ -77,8 +77,23 @@ def pmc_traffic(kernel_prefix):
     return None, None
 
 
-def cpu_baseline(seconds_budget=25.0):
-    """The CPU oracle's train step (B=1, full grid, f32) on this host's cores."""
+def cpu_model_name():
+    """lscpu's "Model name" (the first /proc/cpuinfo model name line)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(steps=3):
+    """The reference's CPU path restated by the oracle (timm semantics with the fused
+    F.scaled_dot_product_attention, as timm's Attention.fused_attn runs it): f32 train step
+    (forward, loss, backward, torch AdamW), B=1, full grid, on this host's cores; median of
+    ``steps`` timed steps after one warm-up."""
     sys.path.insert(0, HERE)
     from oracle import ivit_oracle as O
     from oracle.weights import make_state_dict, model_cfg
@@ -92,24 +107,23 @@ def cpu_baseline(seconds_budget=25.0):
 
     def step():
         opt.zero_grad()
-        c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=True)
+        c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=True, attn="sdpa")
         d = O.detection_loss(c, b, i, anchors, gts, downsampling=True)
         d["loss"].backward()
         opt.step()
 
-    t0 = time.time()
     step()  # warm-up
-    warm = time.time() - t0
-    n = max(1, min(3, int(seconds_budget / max(warm, 1e-3))))
     ts = []
-    for _ in range(n):
+    for _ in range(steps):
         t0 = time.time()
         step()
         ts.append(time.time() - t0)
     med = sorted(ts)[len(ts) // 2]
     return {"value": 1.0 / med, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle f32 train step (fwd+loss+bwd+AdamW), B=1, 400x720, median of {n} after 1 warm-up",
-            "step_s": med}
+            "cpu": cpu_model_name(),
+            "sample": f"oracle f32 train step (fwd with SDPA attention + loss + bwd + AdamW), B=1, 400x720, "
+                      f"median of {steps} after 1 warm-up",
+            "step_s": med, "steps_s": [round(t, 3) for t in ts]}
 
 
 def main():

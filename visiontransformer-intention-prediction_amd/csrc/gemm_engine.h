@@ -1003,176 +1003,14 @@ __global__ __launch_bounds__(256, 1) void gemm_bf16_big_kernel(LA la_, LB lb_, E
     }
 }
 
-// ----------------------------------------------------------------------------- persistent bf16 kernel
-// For the short-K token GEMMs (M = 36 008, K = 384 … 1536: 6–24 K tiles per output tile) the
-// per-tile prologue (first K tile's HBM latency) and epilogue (64 KiB of stores per tile) are as
-// long as the main loop. Here a fixed grid of two workgroups per CU walks the output tiles, and
-// the LDS-DMA pipeline runs straight across tile seams: the next tile's first K tile is in
-// flight while this tile's epilogue transposes and stores. The epilogue therefore gets its own
-// small LDS region (8-row chunks, 8.5 KiB per workgroup) instead of the staging buffers.
-// Tiles are visited XCD-contiguously: at step j the 64 workgroups of one XCD own 64 consecutive
-// tile ids (tm-major), so the A row panels and the weight panel they share stay in that L2.
-template <class EPI>
-IVIT_DEV void epilogue_tile8(float* ep, f32x16 (&acc)[2][2], const EPI& epi, int z, int split, int mbase, int nbase,
-                             int M, int N, int lane) {
-  const int h = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {  // rows 8q .. 8q+7 of the 32-row block: registers 4q .. 4q+3, both halves
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) ep[(e + 4 * h) * EP_LD + 32 * j + (lane & 31)] = acc[i][j][4 * q + e];
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      const int row = lane >> 3, c0 = (lane & 7) * 8;
-      float v[8];
-      const float4 a = *(const float4*)(ep + row * EP_LD + c0);
-      const float4 b = *(const float4*)(ep + row * EP_LD + c0 + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      // local row L = e + 4h of chunk q holds accumulator row (L & 3) + 8q + 4(L >> 2) = 8q + L
-      const int m = mbase + 32 * i + 8 * q + row;
-      const int n = nbase + c0;
-      if (m < M && n < N) epi.apply8(z, split, m, n, v, min(8, N - n));
-    }
-  }
-}
-
-template <class LA, class LB, class EPI, bool A_KC, bool B_KC>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_persist_kernel(LA la_, LB lb_, EPI epi_, int M, int N, int K,
-                                                                   int tilesM, int tilesN) {
-  constexpr int PA = 4, PB = 4;          // 1-KiB pieces per wave per K tile (128 rows x 64 k each operand)
-  constexpr int SA = 128 * 128, STAGE = SA + 16384;
-  constexpr int EPB = 4 * 8 * EP_LD * 4;  // epilogue region: 4 waves x 8 rows x EP_LD floats
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + EPB];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 1, wn = wv & 1;
-  const LA la = la_.bind(0);
-  const LB lb = lb_.bind(0);
-  const EPI epi = epi_.bind(0);
-  const int G = gridDim.x, slot = xcd_remap(blockIdx.x, G);
-  const int ntiles = tilesM * tilesN;
-  if (slot >= ntiles) return;
-  const int nk = (K + GBK16 - 1) / GBK16;
-  const int total = ((ntiles - 1 - slot) / G + 1) * nk;  // (tile, K tile) steps of this workgroup
-  const bool fastA = la.fast_ok(A_KC), fastB = lb.fast_ok(B_KC);
-
-  // issue side: the (tile, K tile) whose pieces go out next, with its per-lane source state
-  int ij = 0, ik = 0, im0 = 0, in0 = 0;
-  typename LA::Pre preA[PA];
-  typename LB::Pre preB[PB];
-  auto set_tile = [&](int j) {
-    const int t = j * G + slot, tm = t / tilesN;
-    im0 = tm * GBM;
-    in0 = (t - tm * tilesN) * GBN;
-#pragma unroll
-    for (int i = 0; i < PA; ++i) preA[i] = la.pre(A_KC, wv * PA + i, lane, im0);
-#pragma unroll
-    for (int i = 0; i < PB; ++i) preB[i] = lb.pre(B_KC, wv * PB + i, lane, in0);
-  };
-  auto issue = [&](int stage) {
-    const int k0 = ik * GBK16;
-    const bool full = k0 + GBK16 <= K;
-    glds_operand<PA>(la, 0, A_KC, smem + stage * STAGE, wv, lane, im0, k0, K, fastA && full, preA);
-    glds_operand<PB>(lb, 0, B_KC, smem + stage * STAGE + SA, wv, lane, in0, k0, K, fastB && full, preB);
-    if (++ik == nk) {
-      ik = 0;
-      if ((++ij) * G + slot < ntiles) set_tile(ij);
-    }
-  };
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  set_tile(0);
-  issue(0);
-  int cj = 0, kt = 0;  // compute side
-  float* ep = (float*)(smem + 2 * STAGE) + wv * (8 * EP_LD);
-  for (int g = 0; g < total; ++g) {
-    const int cur = g & 1;
-    if (g + 1 < total) {
-      issue(cur ^ 1);
-      // this step's pieces (and any epilogue stores issued before the next step's pieces) landed
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    const char* ia = smem + cur * STAGE;
-    const char* ib = ia + SA;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      bf16x8 fa[2], fb[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int rb0 = wm * 64 + 32 * i;
-        fa[i] = A_KC ? frag_kc(ia, rb0 + (lane & 31), 2 * t + (lane >> 5)) : frag_mn(ia, 16 * t, rb0, lane);
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int cb0 = wn * 64 + 32 * j;
-        fb[j] = B_KC ? frag_kc(ib, cb0 + (lane & 31), 2 * t + (lane >> 5)) : frag_mn(ib, 16 * t, cb0, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done with stage `cur` before it is refilled
-    if (++kt == nk) {
-      kt = 0;
-      const int t = cj * G + slot, tm = t / tilesN;
-      epilogue_tile8(ep, acc, epi, 0, 0, tm * GBM + wm * 64, (t - tm * tilesN) * GBN + wn * 64, M, N, lane);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-      ++cj;
-    }
-  }
-}
-
-// IVIT_GEMM_PERSIST=1 enables the persistent token-GEMM kernel (2 = for every eligible shape).
-// Off by default: 10-18 % faster in isolation (tools/gemm_bench.py: qkv 68 -> 56 us, fc1+GELU
-// 126 -> 107 us), but with the two ViT streams running concurrently its fixed two-workgroups-per-CU
-// grid keeps the other stream's kernels off the CUs: 62.1 -> 63.1 ms per step (tools/gpu_ab.sh).
-inline int gemm_persist_mode() {
-  const char* v = getenv("IVIT_GEMM_PERSIST");
-  return v ? atoi(v) : 0;
-}
-inline int gemm_slots() {
-  static const int s = [] {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0) != hipSuccess || cus <= 0) cus = 256;
-    return 2 * cus;
-  }();
-  return s;
-}
-
 // ----------------------------------------------------------------------------- launcher
-// IVIT_GEMM_WIDE=1 puts large-M K-contiguous bf16 GEMMs on 256x128 tiles. Off by default:
-// measured on MI355X it wins on square shapes (4096^3: 882 -> 960 TF/s) but loses 2-8 % on the
-// M = 36 008, K <= 1536 token GEMMs of this model (one workgroup per CU hides less of the
-// short-K prologue/epilogue than two).
 // 256-row tiles (gemm_bf16_big_kernel) for single-split GEMMs: IVIT_GEMM_BIG=1 where they pay
-// (M >= 2048, K >= 1024, N % 256 == 0), 2 for every shape with N >= 256 (tests), 0 off.
+// (M >= 2048, K >= 1024, N % 256 == 0), 2 for every shape with N >= 256 (tests), 0 off (default:
+// this model's shapes give too few 256x256 tiles at one workgroup per CU). Read per launch so a
+// test can switch it (tests/test_gpu_ops.py covers both paths).
 inline int gemm_big_mode() {
   const char* v = getenv("IVIT_GEMM_BIG");
   return v ? atoi(v) : 0;
-}
-inline bool gemm_wide_tiles() {
-  const char* v = getenv("IVIT_GEMM_WIDE");
-  return v && v[0] == '1';
 }
 
 // dtype_bf16: which kernel. batch: number of z. splits: split-K factor (kchunk multiple
@@ -1193,16 +1031,6 @@ int launch_gemm(bool bf16_path, const LA& la, const LB& lb, const EPI& epi, int 
   if (bf16_path) {
     if constexpr (LA::kGlds && LB::kGlds) {
       if constexpr (!BiasOnes<EPI>::v) {
-        const int pm = gemm_persist_mode();
-        const long tiles = (long)tilesM * tilesN;
-        if (pm && batch == 1 && splits == 1 && (pm == 2 || tiles > gemm_slots())) {
-          const int G = (int)(tiles < gemm_slots() ? tiles : gemm_slots());
-          hipLaunchKernelGGL((gemm_bf16_persist_kernel<LA, LB, EPI, A_KC, B_KC>), dim3(G), dim3(256), 0, st, la, lb, epi,
-                             M, N, K, tilesM, tilesN);
-          return 0;
-        }
-      }
-      if constexpr (!BiasOnes<EPI>::v) {
         // 256x256 tiles where they pay (measured, tools/gemm_bench.py): long K and N a multiple of
         // 256 (the fusion convolutions; 4096^3 160 -> 140 us). Short-K token GEMMs and N = 384
         // lose on the one-workgroup-per-CU quantisation (fc2 fwd 61 -> 71 us at BN = 128).
@@ -1218,14 +1046,6 @@ int launch_gemm(bool bf16_path, const LA& la, const LB& lb, const EPI& epi, int 
             hipLaunchKernelGGL((gemm_bf16_big_kernel<LA, LB, EPI, A_KC, B_KC, 128>), dim3(tM * tN, batch), dim3(256),
                                0, st, la, lb, epi, M, N, K, tM, tN);
           }
-          return 0;
-        }
-      }
-      if constexpr (A_KC && !BiasOnes<EPI>::v) {
-        if (gemm_wide_tiles() && M >= 4096 && splits == 1) {  // 256x128 tiles, 8 waves
-          const int tM = ivit_cdiv(M, 256);
-          hipLaunchKernelGGL((gemm_bf16_glds_kernel<LA, LB, EPI, A_KC, B_KC, 4>), dim3(tM * tilesN, batch), dim3(512),
-                             0, st, la, lb, epi, M, N, K, tM, tilesN, 1, kchunk);
           return 0;
         }
       }

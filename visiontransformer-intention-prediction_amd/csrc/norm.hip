@@ -24,11 +24,6 @@ constexpr int LN_MAXV = 8;  // D <= 512
 // 4 rows per half-wave in flight (a 256-thread block covers 32 rows). D % 128 == 0, D <= 512;
 // all row strides multiples of 4 and base pointers 16-B aligned (checked on the host).
 static inline bool al16h(const void* p) { return ((uintptr_t)p & 15) == 0; }
-// IVIT_LN_SCALAR=1 selects the one-wave-per-row kernels (A/B and numerics comparisons)
-static inline bool ln_scalar() {
-  const char* v = getenv("IVIT_LN_SCALAR");
-  return v && v[0] == '1';
-}
 IVIT_DEV long rowmap32(int r, int rpb, int rstride, int roff) {
   return rpb ? (long)(r / rpb) * rstride + roff + r % rpb : (long)r;
 }
@@ -403,7 +398,7 @@ extern "C" int ivit_layernorm_fwd(const float* X, long ldx, long rpb, long rstri
   IVIT_CHECK_ARG(D % 64 == 0 && D <= 64 * LN_MAXV, "ivit_layernorm_fwd: D must be a multiple of 64, <= 512");
   if (M <= 0) return 0;
   hipStream_t st = ivit_stream(stream);
-  const bool vec = !ln_scalar() && D % 128 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16h(X) && al16h(Y) && al16h(gamma) &&
+  const bool vec = D % 128 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && al16h(X) && al16h(Y) && al16h(gamma) &&
                    al16h(beta) && M < (1L << 30) && rstride < (1L << 30) && roff < (1L << 30) && rpb < (1L << 30);
   if (vec) {
     const dim3 grid(ivit_cdiv(M, 8 * LNV_ROWS));
@@ -441,7 +436,7 @@ extern "C" int ivit_layernorm_bwd(const float* X, long ldx, long rpb, long rstri
   hipStream_t st = ivit_stream(stream);
   const int nb = ivit_cdiv(M, 4 * LNB_ROWS);  // = cdiv(M, 8 * LNV_ROWS): both kernels cover 32 rows per block
   const int rps = (int)(rows_per_scale > 0 ? rows_per_scale : 1);
-  const bool vec = !ln_scalar() && D % 128 == 0 && ldx % 4 == 0 && lddy % 4 == 0 && lddx % 4 == 0 && al16h(X) && al16h(dY) &&
+  const bool vec = D % 128 == 0 && ldx % 4 == 0 && lddy % 4 == 0 && lddx % 4 == 0 && al16h(X) && al16h(dY) &&
                    al16h(dX) && al16h(gamma) && (!dres || al16h(dres)) && (!dXs || al16h(dXs)) && M < (1L << 30) &&
                    rstride < (1L << 30) && roff < (1L << 30) && rpb < (1L << 30);
   if (vec) {
