@@ -643,12 +643,7 @@ long ld_scores(long N) { return (N + 7) / 8 * 8; }
 }  // namespace
 
 extern "C" long ivit_attn_workspace(int dtype, long B, long N, long H, long Dh, int backward) {
-  if (dtype == IVIT_BF16) {
-    if (!backward) return 0;
-    const long two = 2 * B * H * ((N + AK - 1) / AK * AK) * 4;  // two-kernel form (dev A/B)
-    const long f = attn_bwd_fused_ws(B, N, H);
-    return f > two ? f : two;
-  }
+  if (dtype == IVIT_BF16) return backward ? 2 * B * H * ((N + AK - 1) / AK * AK) * 4 : 0;
   const long one = B * H * N * ld_scores(N) * 4;
   return backward ? 2 * one : one;
 }
@@ -695,11 +690,6 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
   if (B * N * H == 0) return 0;
   const long D = H * Dh, ldq = 3 * D;
   if (dtype == IVIT_BF16) {
-    if (!bwd_old()) {
-      attn_bwd_fused(false, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, B, N, H, (bf16*)dqkv, work, st);
-      IVIT_LAUNCH_CHECK();
-      return 0;
-    }
     dim3 g(ivit_cdiv(N, AQ), B * H);
     const long Npad = (N + AK - 1) / AK * AK;
     float* lse2p = (float*)work;
@@ -782,11 +772,6 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   IVIT_CHECK_ARG(work_bytes >= ivit_attn_workspace(IVIT_BF16, B, N, H, Dh, 1), "ivit_attn_bwd_q2: workspace too small");
   if (B * N * H == 0) return 0;
   hipStream_t st = ivit_stream(stream);
-  if (!bwd_old()) {
-    attn_bwd_fused(true, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, B, N, H, (bf16*)dqkv, work, st);
-    IVIT_LAUNCH_CHECK();
-    return 0;
-  }
   const float scale = 1.0f / sqrtf((float)Dh);
   dim3 g(ivit_cdiv(N, AQ), B * H);
   const long Npad = (N + AK - 1) / AK * AK;

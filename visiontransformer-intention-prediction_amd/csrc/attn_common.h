@@ -1,5 +1,5 @@
-// Shared helpers of the attention kernels (attention.hip: forward + f32 path; attn_bwd.hip: the
-// fused bf16 backward). gfx950 only.
+// Helpers of the attention kernels (attention.hip: flash forward, the dQ and dK/dV backward
+// kernels and the f32 parity path). gfx950 only.
 #pragma once
 #include "gemm_engine.h"
 
@@ -129,11 +129,3 @@ IVIT_DEV void retire_loads(bf16x8 (&a)[4], bf16x8 (&b)[4]) {
 }
 
 }  // namespace
-
-namespace ivit {
-// fused bf16 backward (attn_bwd.hip): workspace bytes and launcher (rows + main + dQ reduce)
-long attn_bwd_fused_ws(long B, long N, long H);
-bool bwd_old();  // TEMPORARY dev A/B switch (IVIT_ATTN_BWD_OLD=1: two-kernel form)
-int attn_bwd_fused(bool q2, const bf16* qkv, const bf16* out, const bf16* dout, const float* lse, long B, long N,
-                   long H, bf16* dqkv, void* work, hipStream_t st);
-}  // namespace ivit
