@@ -42,18 +42,28 @@ def step_flops(B, H, W, depth=12, D=384, C_l=290, C_m=9, planes=512, A=5, K=8, a
     return B * (3 * fwd - patch), B * (3 * vit), B * fwd
 
 
-# the kernel the bf16 ViT blocks launch: v6 on the prescaled Q (ivit_attn_fwd_q2), v5 with IVIT_ATTN_Q2=0
-ROOF_KERNEL = ("attn_fwd_bf16_v6_kernel<4" if os.environ.get("IVIT_ATTN_Q2", "1") == "1" else "attn_fwd_bf16_v5_kernel<4")
-ROOF_ENTRY = "ivit_attn_fwd_q2" if ROOF_KERNEL.startswith("attn_fwd_bf16_v6") else "ivit_attn_fwd"
+# The dominant kernels of the bf16 step (profiles/r02_*_bench_kernel_stats.csv): the attention
+# backward pair of ivit_attn_bwd_q2 (attn_bwd_dq_v2 + attn_bwd_dkv_v2, ~30 % of GPU time), then the
+# attention forward (ivit_attn_fwd_q2, ~11 %). The roofline object reports whichever of the two has
+# the larger measured time per step (HIP events on the launching stream, inside the timed loop).
+ATTN = {
+    "attn_bwd": {"kernels": ["attn_bwd_dq_v2_kernel", "attn_bwd_dkv_v2_kernel"], "entry": "ivit_attn_bwd_q2",
+                 "flops_note": "8*B*H*N^2*64 (dQ, dK, dV, dP products; the S recompute is not counted)"},
+    "attn_fwd": {"kernels": ["attn_fwd_bf16_v6_kernel"], "entry": "ivit_attn_fwd_q2",
+                 "flops_note": "4*B*H*N^2*64 (QK^T, PV)"},
+}
 
 
-def attn_fwd_flops(B, N, H, Dh=64):
-    return 4.0 * B * H * N * N * Dh
+def attn_flops(name, B, N, H, Dh=64):
+    return (8.0 if name == "attn_bwd" else 4.0) * B * H * N * N * Dh
 
 
-def attn_fwd_bytes(B, N, H, Dh=64):
-    """Algorithmic HBM bytes of one attention-forward launch: qkv read once (bf16), out (bf16) + lse (f32) written."""
-    return B * N * 3 * H * Dh * 2 + B * N * H * Dh * 2 + B * H * N * 4
+def attn_bytes(name, B, N, H, Dh=64):
+    """Algorithmic HBM bytes per launch: forward reads qkv, writes out + lse; backward reads qkv, out,
+    dO, lse and writes dqkv (bf16), plus the padded f32 row constants written and read once."""
+    if name == "attn_fwd":
+        return B * N * 3 * H * Dh * 2 + B * N * H * Dh * 2 + B * H * N * 4
+    return B * N * 3 * H * Dh * 2 * 2 + 2 * B * N * H * Dh * 2 + B * H * N * 4 + 2 * 2 * B * H * N * 4
 
 
 def pmc_traffic(kernel_prefix):
@@ -71,10 +81,17 @@ def pmc_traffic(kernel_prefix):
             kern = json.load(fh)["kernels"]
     except (OSError, ValueError, KeyError):
         return None, None
-    for name, v in kern.items():
-        if name.startswith(kernel_prefix) and v.get("hbm_bytes_avg") is not None:
-            return float(v["hbm_bytes_avg"]), os.path.relpath(files[-1], HERE)
-    return None, None
+    prefixes = [kernel_prefix] if isinstance(kernel_prefix, str) else list(kernel_prefix)
+    tot, found = 0.0, 0
+    for pre in prefixes:
+        for name, v in kern.items():
+            if name.startswith(pre) and v.get("hbm_bytes_avg") is not None:
+                tot += float(v["hbm_bytes_avg"])
+                found += 1
+                break
+    if found != len(prefixes):
+        return None, None
+    return tot, os.path.relpath(files[-1], HERE)
 
 
 def cpu_model_name():
@@ -206,7 +223,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ops.KernelTimer.enabled = {"attn_fwd"}
+    ops.KernelTimer.enabled = set(ATTN)
     ops.KernelTimer.records = {}
     if world > 1:
         dist.barrier()
@@ -218,7 +235,8 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    attn_ms = ops.KernelTimer.mean_ms("attn_fwd")
+    attn_ms = {k: ops.KernelTimer.mean_ms(k) for k in ATTN}
+    attn_n = {k: ops.KernelTimer.count(k) for k in ATTN}
     ops.KernelTimer.enabled = set()
     if world > 1:
         t = torch.tensor([el], device=dev)
@@ -232,12 +250,20 @@ def main():
     if not train:
         fl_step = fl_fwd
     N = (H // 8) * (W // 8) + 1
-    afl = attn_fwd_flops(B, N, 6)
-    achieved = afl / (attn_ms * 1e-3) / 1e12
     peak = PEAK_BF16_TFLOPS if cd == torch.bfloat16 else 157.3
+    # dominant attention kernel(s): larger measured time per step
+    per_step = {k: (attn_ms[k] * attn_n[k] / args.steps if attn_n[k] else 0.0) for k in ATTN}
+    roof = max(per_step, key=per_step.get) if any(per_step.values()) else "attn_fwd"
+    afl = attn_flops(roof, B, N, 6)
+    achieved = afl / (attn_ms[roof] * 1e-3) / 1e12 if attn_n[roof] else float("nan")
     # PMC traffic was collected on the default train configuration only
     default_cfg = train and (H, W) == (400, 720) and B == 8 and cd == torch.bfloat16 and not args.augment
-    traffic, traffic_src = pmc_traffic(ROOF_KERNEL) if default_cfg else (None, None)
+    traffic, traffic_src = pmc_traffic(ATTN[roof]["kernels"]) if default_cfg else (None, None)
+    # attention MFMA utilisation (BASELINE metric "attn MFMA util %"): attention fwd + bwd algorithmic
+    # flops per step / their measured kernel time per step; ViT attention + MLP block flops per step /
+    # the whole step's wall time (a lower bound for the blocks' own utilisation)
+    at_ms = sum(per_step.values())
+    at_fl = sum(attn_flops(k, B, N, 6) * attn_n[k] / args.steps for k in ATTN)
     if train:
         workload = f"IntentNetViT train step (fwd+loss+bwd+AdamW), {args.dtype}, {H}x{W}, batch {B}/GPU"
         if args.augment:
@@ -255,14 +281,23 @@ def main():
                                      "random-init weights)",
         "config": {"workload": workload, "global_batch": gb, "per_gpu_batch": B, "grid": [H, W],
                    "tokens_per_stream": N, "parallelism": f"dp{world}"},
-        "roofline": {"kernel": ROOF_KERNEL + f"> ({ROOF_ENTRY})", "bound": "mfma",
+        "roofline": {"kernel": " + ".join(ATTN[roof]["kernels"]) + f" ({ATTN[roof]['entry']})", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "per_launch": f"4*B*H*N^2*64 = {afl:.4g} flop (B={B}, H=6, N={N}); {attn_ms:.4f} ms avg over "
-                                   f"{len(ops.KernelTimer.records.get('attn_fwd', []))} launches (HIP events)",
+                     "per_launch": f"{ATTN[roof]['flops_note']} = {afl:.4g} flop (B={B}, H=6, N={N}); "
+                                   f"{attn_ms[roof]:.4f} ms avg over {attn_n[roof]} launches (HIP events on the "
+                                   f"launching stream; the other ViT stream runs concurrently)",
                      "traffic_note": (f"HBM bytes per launch from {traffic_src} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
-                                      f"gfx950-corrected); algorithmic bytes {attn_fwd_bytes(B, N, 6):.4g}")
-                     if traffic is not None else "no PMC summary for this configuration"},
+                                      f"gfx950-corrected, summed over the kernels); algorithmic bytes "
+                                      f"{attn_bytes(roof, B, N, 6):.4g}")
+                     if traffic is not None else "no PMC summary for this configuration",
+                     "per_step_ms": {k: round(v, 3) for k, v in per_step.items()}},
+        "attn_mfma_util": {
+            "attention_fwd_bwd": round(at_fl / (at_ms * 1e-3) / 1e12 / peak, 4) if at_ms else None,
+            "vit_blocks_lower_bound": round((fl_vit if train else fl_vit / 3) / (el / args.steps) / 1e12 / peak, 4),
+            "note": "attention_fwd_bwd: 12*B*H*N^2*64 flops per block pass (fwd 4 + bwd 8, no recompute) per step / "
+                    "the measured attention kernel time per step; vit_blocks_lower_bound: ViT attention + MLP "
+                    "block fwd+bwd flops per step / the whole step's wall time; peak = dense bf16 MFMA"},
         "step_mfma": {"achieved": round(fl_step * world / el * args.steps / 1e12 / world, 2), "unit": "TFLOP/s/GPU",
                       "frac": round(fl_step / (el / args.steps) / 1e12 / peak, 4),
                       "flops_per_step_per_gpu": fl_step},

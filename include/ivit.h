@@ -244,6 +244,19 @@ typedef struct ivit_bev_pass {
 } ivit_bev_pass;
 int ivit_bev_augment(const void* passes, long n_passes, long H, long W, long max_planes, void* stream);
 
+/* HD-map rasterisation (utils.py:108-182 rasterize_map_ego_centric):
+ * cv2.polylines / cv2.fillPoly (LINE_8, 1 px, shift 0, colour 1) into zero-filled f32 planes.
+ * seg [n_seg, 5] int32 (x0, y0, x1, y1, plane bitmask): open-polyline segments AND polygon
+ * edges (fillPoly draws every edge with cv::Line); seg_base [n_seg] int64 element offset of the
+ * segment's [planes, H, W] image. edges [*, 4] int64 (y0, y1, x_top << 16, dx << 16 truncated)
+ * of the non-horizontal polygon edges; polys [n_polys, 3] int32 (first edge, edge count <=
+ * max_edges <= 256, plane bitmask), poly_base [n_polys] int64; rows [n_rows, 2] int32
+ * (polygon, scanline y) fill work items (polygons with >= 2 edges, y0_min <= y < min(y1_max, H)).
+ * Replaces utils.py:148-182's per-lane cv2 calls. */
+int ivit_map_raster(const int* seg, long n_seg, const long* seg_base, const long* edges, const int* polys,
+                    long n_polys, const long* poly_base, const int* rows, long n_rows, long max_edges, long H, long W,
+                    float* out, void* stream);
+
 /* ---- Strided convolutions of the CNN variant (model_cnn.py:7-12, 14-33, 86-100; SURVEY.md
  * §8f rank 4) as im2col + the dense GEMMs above. X: NHWC [B, H, W, C] (f32 or bf16); cols:
  * [B*Ho*Wo, ldc] row (b, oy, ox), column (ky*k + kx)*C + c = X[b, oy*s - pad + ky,

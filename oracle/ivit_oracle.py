@@ -719,3 +719,218 @@ def cnn_forward(sd, lidar, map_bev, training=False, ks=5, fusion_ks=3, blocks=2,
         feats.append(x)
     f = stage("fusion_block", torch.cat(feats, 1), 2, fusion_ks, fusion_layers)
     return heads_forward(sd, f)
+
+
+# --------------------------------------------------------------------------------------
+# HD-map rasterisation: utils.py:35-60 (ego transform, world → pixel)
+# and utils.py:108-182 (rasterize_map_ego_centric), with OpenCV's integer fillPoly / polylines
+# (LINE_8, thickness 1, shift 0) restated from OpenCV 4.x imgproc/drawing.cpp. cv2 is absent
+# here: PARITY UNPINNED at the OpenCV level (the flow is pinned by tests/golden/map_raster.npz).
+# --------------------------------------------------------------------------------------
+CV_XY_SHIFT = 16
+MAP_CH = 9
+
+
+def cv_line8_pixels(p0, p1):
+    """cv::LineIterator(connectivity 8, leftToRight) pixels of the segment p0 → p1 (x, y ints);
+    both endpoints inside the image (the callers pre-filter points)."""
+    (x0, y0), (x1, y1) = p0, p1
+    dx, dy = x1 - x0, y1 - y0
+    if dx < 0:  # leftToRight: iterate from the left endpoint
+        dx, dy = -dx, -dy
+        x0, y0, x1, y1 = x1, y1, x0, y0
+    sy = 1
+    if dy < 0:
+        dy, sy = -dy, -1
+    vert = dy > dx
+    major, minor = (dy, dx) if vert else (dx, dy)
+    err = major - 2 * minor
+    out = []
+    x, y = x0, y0
+    for _ in range(major + 1):
+        out.append((x, y))
+        step = err < 0
+        err += -2 * minor + (2 * major if step else 0)
+        if vert:
+            y += sy
+            x += 1 if step else 0
+        else:
+            x += 1
+            y += sy if step else 0
+    return out
+
+
+def _trunc_div(a, b):
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def cv_fill_poly(img, pts):
+    """cv2.fillPoly(img, [pts], 1) for one polygon of integer (x, y) vertices, LINE_8, shift 0:
+    CollectPolyEdges (every edge also drawn by Line) + FillEdgeCollection scanlines (edge x in
+    16.16 fixed point, x += dx per scanline, spans [x_l >> 16, x_r >> 16] between sorted pairs,
+    an edge active on y0 <= y < y1, horizontal edges skipped, fewer than 2 edges: no fill)."""
+    H, W = img.shape
+    pts = [(int(x), int(y)) for x, y in pts]
+    n = len(pts)
+    edges = []
+    for i in range(n):
+        (xa, ya), (xb, yb) = pts[i - 1], pts[i]
+        for x, y in cv_line8_pixels((xa, ya), (xb, yb)):
+            if 0 <= x < W and 0 <= y < H:
+                img[y, x] = 1
+        if ya == yb:
+            continue
+        Xa, Xb = xa << CV_XY_SHIFT, xb << CV_XY_SHIFT
+        if ya < yb:
+            e = (ya, yb, Xa)
+        else:
+            e = (yb, ya, Xb)
+        edges.append((e[0], e[1], e[2], _trunc_div(Xb - Xa, yb - ya)))
+    if len(edges) < 2:
+        return img
+    y_min = min(e[0] for e in edges)
+    y_max = min(max(e[1] for e in edges), H)
+    for y in range(max(y_min, 0), y_max):
+        xs = sorted(x0 + (y - ya) * dx for ya, yb, x0, dx in edges if ya <= y < yb)
+        for k in range(0, len(xs) - 1, 2):
+            x1, x2 = xs[k] >> CV_XY_SHIFT, xs[k + 1] >> CV_XY_SHIFT
+            if x1 < W and x2 >= 0:
+                img[y, max(x1, 0):min(x2, W - 1) + 1] = 1
+    return img
+
+
+def cv_polyline(img, pts):
+    """cv2.polylines(img, [pts], isClosed=False, 1, thickness=1): Line per consecutive pair."""
+    H, W = img.shape
+    pts = [(int(x), int(y)) for x, y in pts]
+    for i in range(1, len(pts)):
+        for x, y in cv_line8_pixels(pts[i - 1], pts[i]):
+            if 0 <= x < W and 0 <= y < H:
+                img[y, x] = 1
+    return img
+
+
+def ego_yaw_from_quat(qx, qy, qz, qw):
+    """scipy Rotation.from_quat([qx, qy, qz, qw]).as_euler('xyz')[2] (utils.py:123)."""
+    from scipy.spatial.transform import Rotation
+    return float(Rotation.from_quat([qx, qy, qz, qw]).as_euler('xyz')[2])
+
+
+def world_to_pixel_np(world_xy, ego_xy, ego_yaw, H=BEV_H, W=BEV_W, voxel=0.2):
+    """utils.py:35-60: T = [R(-yaw) | -R(-yaw) t] (f64), pixel = round(offset ± ego / voxel)."""
+    c, s = np.cos(-ego_yaw), np.sin(-ego_yaw)
+    Rm = np.array([[c, -s], [s, c]])
+    T = np.eye(3)
+    T[:2, :2] = Rm
+    T[:2, 2] = -Rm @ np.asarray(ego_xy, np.float64)
+    homo = np.hstack([world_xy, np.ones((world_xy.shape[0], 1))])
+    ego = (T @ homo.T).T[:, :2]
+    px = W / 2.0 + ego[:, 1] / voxel
+    py = H * 3.0 / 4.0 - ego[:, 0] / voxel
+    return np.round(np.vstack([px, py]).T).astype(int)
+
+
+def map_pixels_np(points, ego_xy, ego_yaw, H=BEV_H, W=BEV_W):
+    """to_bev_pixel_local (utils.py:131-145): drop malformed points, transform, keep in-bounds."""
+    if not points:
+        return np.empty((0, 2), dtype=int)
+    valid = [p for p in points if isinstance(p, dict) and 'x' in p and 'y' in p]
+    if not valid:
+        return np.empty((0, 2), dtype=int)
+    xy = np.array([[p['x'], p['y']] for p in valid])
+    pix = world_to_pixel_np(xy, ego_xy, ego_yaw, H, W)
+    m = (pix[:, 0] >= 0) & (pix[:, 0] < W) & (pix[:, 1] >= 0) & (pix[:, 1] < H)
+    return pix[m]
+
+
+MARK_CHANNELS = {"DASHED_WHITE": 6, "SOLID_WHITE": 7, "SOLID_YELLOW": 8}
+
+
+def rasterize_map_np(map_data, ego_pose, H=BEV_H, W=BEV_W):
+    """rasterize_map_ego_centric (utils.py:108-182) on a parsed map dict and an ego pose mapping
+    with tx_m, ty_m, qx, qy, qz, qw → (9, H, W) float32 {0, 1}."""
+    out = np.zeros((MAP_CH, H, W), np.uint8)
+    yaw = ego_yaw_from_quat(ego_pose['qx'], ego_pose['qy'], ego_pose['qz'], ego_pose['qw'])
+    exy = (ego_pose['tx_m'], ego_pose['ty_m'])
+    for _, lane in map_data.get("lane_segments", {}).items():
+        lpx = map_pixels_np(lane.get("left_lane_boundary", []), exy, yaw, H, W)
+        rpx = map_pixels_np(lane.get("right_lane_boundary", []), exy, yaw, H, W)
+        if len(lpx) > 1 and len(rpx) > 1:
+            poly = np.vstack([lpx, np.flipud(rpx)])
+            if poly.shape[0] >= 3:
+                cv_fill_poly(out[0], poly)
+                if lane.get("is_intersection", False):
+                    cv_fill_poly(out[4], poly)
+                if lane.get("lane_type") == "BUS":
+                    cv_fill_poly(out[5], poly)
+        if len(lpx) > 1:
+            cv_polyline(out[1], lpx)
+        if len(rpx) > 1:
+            cv_polyline(out[2], rpx)
+        lm, rm = lane.get("left_lane_mark_type", ""), lane.get("right_lane_mark_type", "")
+        if lm in MARK_CHANNELS and len(lpx) > 1:
+            cv_polyline(out[MARK_CHANNELS[lm]], lpx)
+        if rm in MARK_CHANNELS and len(rpx) > 1:
+            cv_polyline(out[MARK_CHANNELS[rm]], rpx)
+    for _, cw in map_data.get("pedestrian_crossings", {}).items():
+        poly = cw.get('polygon', [])
+        if poly:
+            px = map_pixels_np(poly, exy, yaw, H, W)
+            if len(px) >= 3:
+                cv_fill_poly(out[3], px)
+    return out.astype(np.float32)
+
+
+def synthetic_map(seed, n_lanes=40, n_cross=6, center=(100.0, -50.0), spread=70.0):
+    """A seeded Argoverse-2-style map dict: lanes with left / right boundaries of 2-12 points
+    (some leaving the grid, some malformed), intersections, bus lanes, the three mark types and
+    others, crosswalk polygons; plus degenerate cases (1-point / empty boundaries, collinear and
+    horizontal polygons)."""
+    rng = np.random.default_rng(seed)
+    cx, cy = center
+    lanes = {}
+    marks = ["DASHED_WHITE", "SOLID_WHITE", "SOLID_YELLOW", "DOUBLE_SOLID_YELLOW", "NONE", ""]
+    for i in range(n_lanes):
+        n = int(rng.integers(2, 13))
+        x0, y0 = cx + rng.uniform(-spread, spread), cy + rng.uniform(-spread, spread)
+        ang = rng.uniform(-np.pi, np.pi)
+        L = rng.uniform(5, 60)
+        t = np.linspace(0, L, n)
+        bend = rng.normal(0, 0.02)
+        xs = x0 + t * np.cos(ang + bend * t)
+        ys = y0 + t * np.sin(ang + bend * t)
+        w = rng.uniform(2.5, 4.5)
+        nx, ny = -np.sin(ang), np.cos(ang)
+        left = [{"x": float(a + nx * w / 2), "y": float(b + ny * w / 2), "z": 0.0} for a, b in zip(xs, ys)]
+        right = [{"x": float(a - nx * w / 2), "y": float(b - ny * w / 2), "z": 0.0} for a, b in zip(xs, ys)]
+        if i % 13 == 5:
+            left = left[:1]  # a 1-point boundary: no polygon, no polyline
+        if i % 17 == 3:
+            right = [{"y": 1.0}] + right  # a malformed point is dropped
+        lanes[str(1000 + i)] = {"left_lane_boundary": left, "right_lane_boundary": right,
+                                "is_intersection": bool(rng.random() < 0.25),
+                                "lane_type": "BUS" if rng.random() < 0.15 else "VEHICLE",
+                                "left_lane_mark_type": marks[int(rng.integers(len(marks)))],
+                                "right_lane_mark_type": marks[int(rng.integers(len(marks)))]}
+    # a horizontal-edge polygon (axis-aligned in the ego frame is not guaranteed; a sliver) and an empty lane
+    lanes["9001"] = {"left_lane_boundary": [], "right_lane_boundary": []}
+    crosses = {}
+    for i in range(n_cross):
+        x0, y0 = cx + rng.uniform(-spread / 2, spread / 2), cy + rng.uniform(-spread / 2, spread / 2)
+        a = rng.uniform(-np.pi, np.pi)
+        Lw, Ww = rng.uniform(4, 15), rng.uniform(2, 5)
+        pts = [(0, 0), (Lw, 0), (Lw, Ww), (0, Ww)]
+        c, s = np.cos(a), np.sin(a)
+        crosses[str(2000 + i)] = {"polygon": [{"x": float(x0 + c * u - s * v), "y": float(y0 + s * u + c * v), "z": 0.0}
+                                              for u, v in pts]}
+    crosses["2999"] = {"polygon": []}
+    return {"lane_segments": lanes, "pedestrian_crossings": crosses}
+
+
+def synthetic_pose(seed, center=(100.0, -50.0)):
+    from scipy.spatial.transform import Rotation
+    rng = np.random.default_rng(seed)
+    q = Rotation.from_euler("xyz", [rng.normal(0, 0.01), rng.normal(0, 0.01), rng.uniform(-np.pi, np.pi)]).as_quat()
+    return {"tx_m": center[0] + rng.normal(0, 5), "ty_m": center[1] + rng.normal(0, 5), "tz_m": 0.0,
+            "qx": q[0], "qy": q[1], "qz": q[2], "qw": q[3]}

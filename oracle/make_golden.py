@@ -404,6 +404,43 @@ def gen_bev_augment():
     np.savez_compressed(os.path.join(OUT, "bev_augment.npz"), **rec)
 
 
+def gen_map_raster():
+    """utils.rasterize_map_ego_centric (utils.py:108-182): the reference's OWN flow (JSON load,
+    ego yaw from the quaternion, world -> pixel, point filtering, lane polygons / boundaries /
+    mark types / intersections / bus lanes / crosswalks into the 9 channels) with cv2.fillPoly /
+    polylines backed by the oracle's OpenCV restatement (parity unpinned at the OpenCV level).
+    Cases: 4 seeded maps + poses, an empty map, a missing file and an invalid quaternion."""
+    import json as _json
+    import tempfile
+    import pandas as pd
+    import utils as ref_utils
+    rec = {}
+    cases = []
+    for sd in range(4):
+        cases.append((f"seed{sd}", O.synthetic_map(10 + sd, n_lanes=30 + 10 * sd), O.synthetic_pose(20 + sd)))
+    cases.append(("empty", {}, O.synthetic_pose(7)))
+    cases.append(("badquat", O.synthetic_map(3), dict(O.synthetic_pose(3), qx=0.0, qy=0.0, qz=0.0, qw=0.0)))
+    with tempfile.TemporaryDirectory() as td:
+        for name, m, pose in cases + [("missing", None, O.synthetic_pose(5))]:
+            path = os.path.join(td, f"{name}.json")
+            if m is not None:
+                with open(path, "w") as fh:
+                    _json.dump(m, fh)
+            ser = pd.Series(pose)
+            ref = ref_utils.rasterize_map_ego_centric(path, ser)
+            mine = (O.rasterize_map_np(m, pose) if m is not None and name != "badquat"
+                    else np.zeros((9, 400, 720), np.float32))
+            assert ref.dtype == np.float32 and np.array_equal(ref, mine), f"oracle != reference map raster ({name})"
+            nz = np.flatnonzero(ref.reshape(-1))
+            rec[f"{name}_json"] = np.array(_json.dumps(m) if m is not None else "")
+            rec[f"{name}_pose"] = np.array([pose[k] for k in ("tx_m", "ty_m", "qx", "qy", "qz", "qw")])
+            rec[f"{name}_idx"] = nz.astype(np.int64)
+            rec[f"{name}_per_channel"] = ref.reshape(9, -1).sum(1)
+    rec["cases"] = np.array([c[0] for c in cases] + ["missing"])
+    np.savez_compressed(os.path.join(OUT, "map_raster.npz"), **rec)
+    print("map_raster:", {c: rec[f"{c}_per_channel"].astype(int).tolist() for c in rec["cases"]})
+
+
 def gen_cnn_small():
     """The reference's OWN IntentNetCNN (model_cnn.py) at a 32x48 grid with its default channels,
     filled by the seeded filler in its state_dict order: eval outputs, train outputs + loss
@@ -485,3 +522,5 @@ if __name__ == "__main__":
     gen_lidar_bev()
     gen_bev_augment()
     gen_cnn_small()
+    gen_loss_options()
+    gen_map_raster()

@@ -13,9 +13,11 @@ calls:
   published source (unpinned, README.md:115); ``nms`` follows the CPU kernel.
 * ``shapely.geometry.Polygon``: convex-polygon area/intersection in float64
   (GEOS restated for the convex rectangles ``utils.py:295-332`` builds).
-* ``cv2``: ``getRotationMatrix2D`` / ``warpAffine`` / ``resize`` (INTER_LINEAR, BORDER_CONSTANT) backed
-  by ``ivit_oracle``'s restatement of OpenCV's generic paths, so the reference's BEV augmentation
-  flow (utils.py:394-517) runs here; the resampling arithmetic itself is parity unpinned.
+* ``cv2``: ``getRotationMatrix2D`` / ``warpAffine`` / ``resize`` (INTER_LINEAR, BORDER_CONSTANT) and
+  ``fillPoly`` / ``polylines`` (LINE_8, 1 px) backed by ``ivit_oracle``'s restatement of OpenCV's
+  generic paths, so the reference's BEV augmentation (utils.py:394-517) and map rasterisation
+  (utils.py:108-182) flows run here; the resampling / scan-conversion arithmetic itself is parity
+  unpinned.
 """
 from __future__ import annotations
 
@@ -203,6 +205,19 @@ def install(reference_dir="/root/reference"):
         assert interpolation == 1, "stand-in: INTER_LINEAR only"
         return _O.cv2_resize_linear(src, dsize)
     cv2.warpAffine, cv2.resize = _warp, _resize
+
+    def _fill_poly(img, pts_list, color=1, *a, **k):
+        assert color == 1 and not a and not k, "stand-in: color 1, LINE_8, shift 0"
+        for pts in pts_list:
+            _O.cv_fill_poly(img, np.asarray(pts).reshape(-1, 2))
+        return img
+
+    def _polylines(img, pts_list, isClosed, color=1, thickness=1, *a, **k):
+        assert not isClosed and color == 1 and thickness == 1 and not a and not k, "stand-in: open, color 1, 1 px"
+        for pts in pts_list:
+            _O.cv_polyline(img, np.asarray(pts).reshape(-1, 2))
+        return img
+    cv2.fillPoly, cv2.polylines = _fill_poly, _polylines
     shp = types.ModuleType("shapely")
     geom = types.ModuleType("shapely.geometry")
     geom.Polygon = _Polygon

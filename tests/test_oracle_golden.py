@@ -207,3 +207,38 @@ def test_forward_sdpa_variant_matches_golden(small):
         c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=False, attn="sdpa")
     for got, key in ((c, "eval_cls"), (b, "eval_box"), (i, "eval_int")):
         np.testing.assert_allclose(got.numpy(), z[key], rtol=1e-4, atol=1e-4)
+
+
+def _map_case(z, name):
+    import json as _json
+    s = str(z[f"{name}_json"])
+    pose = dict(zip(("tx_m", "ty_m", "qx", "qy", "qz", "qw"), z[f"{name}_pose"].tolist()))
+    return (_json.loads(s) if s else None), pose
+
+
+def test_map_raster_oracle_vs_golden():
+    """rasterize_map_ego_centric (utils.py:108-182): the oracle reproduces the reference's own flow
+    (golden from the reference with cv2 backed by the oracle's OpenCV restatement)."""
+    z = golden("map_raster.npz")
+    for name in z["cases"]:
+        name = str(name)
+        m, pose = _map_case(z, name)
+        if m is None or name == "badquat":
+            assert z[f"{name}_idx"].size == 0
+            continue
+        got = O.rasterize_map_np(m, pose)
+        assert np.array_equal(np.flatnonzero(got.reshape(-1)), z[f"{name}_idx"]), name
+        assert np.array_equal(got.reshape(9, -1).sum(1), z[f"{name}_per_channel"]), name
+
+
+def test_cv_raster_primitives():
+    """The OpenCV LINE_8 / fillPoly restatement on hand-checked cases (parity unpinned: cv2 absent)."""
+    assert O.cv_line8_pixels((0, 0), (4, 2)) == [(0, 0), (1, 0), (2, 1), (3, 1), (4, 2)]
+    assert O.cv_line8_pixels((4, 2), (0, 0)) == O.cv_line8_pixels((0, 0), (4, 2))  # leftToRight
+    assert O.cv_line8_pixels((3, 0), (3, 3)) == [(3, 0), (3, 1), (3, 2), (3, 3)]
+    img = np.zeros((6, 6), np.uint8)
+    O.cv_fill_poly(img, [(1, 1), (4, 1), (4, 4), (1, 4)])  # axis-aligned square: rows 1..4, cols 1..4
+    assert img[1:5, 1:5].all() and img.sum() == 16
+    img = np.zeros((6, 6), np.uint8)
+    O.cv_fill_poly(img, [(0, 2), (5, 2), (3, 2)])  # all on one row: only the edge lines
+    assert img.sum() == 6 and img[2].all()

@@ -281,3 +281,116 @@ extern "C" int ivit_bev_augment(const void* passes, long n_passes, long H, long 
   IVIT_LAUNCH_CHECK();
   return 0;
 }
+
+// ---------------------------------------------------------------- HD-map rasterisation
+// rasterize_map_ego_centric (utils.py:108-182): cv2.polylines / cv2.fillPoly (LINE_8, thickness
+// 1, shift 0, colour 1) into zero-initialised f32 planes, as two launches over host-built tables:
+//   segments: every open-polyline segment and every polygon edge (cv::fillPoly draws each edge
+//             with cv::Line) — one thread walks cv::LineIterator's 8-connected pixels
+//             (leftToRight, err = major - 2 minor, step the minor axis when err < 0);
+//   fill rows: one thread per (polygon, scanline y): the x of every edge active at y
+//             (y0 <= y < y1) in 16.16 fixed point, x = x_top + (y - y0) * dx (the exact value
+//             FillEdgeCollection's per-scanline x += dx reaches), sorted, spans
+//             [x_2k >> 16, x_2k+1 >> 16] filled (delta 0 for LINE_8), clipped to the image.
+// Every write stores 1.0f: concurrent writers of one pixel agree, no atomics.
+namespace {
+constexpr int kMapMaxEdges = 256;
+
+IVIT_DEV void map_put(float* img, long HW, int mask, long off) {
+#pragma unroll 1
+  for (int c = 0; mask; ++c, mask >>= 1)
+    if (mask & 1) img[c * HW + off] = 1.0f;
+}
+
+__global__ void map_segments_kernel(const int* __restrict__ seg, long n, const long* __restrict__ base, int H,
+                                    int W, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int* s = seg + i * 5;  // x0, y0, x1, y1, plane mask
+  int x0 = s[0], y0 = s[1], x1 = s[2], y1 = s[3];
+  const int mask = s[4];
+  float* img = out + base[i];
+  const long HW = (long)H * W;
+  int dx = x1 - x0, dy = y1 - y0;
+  if (dx < 0) {  // leftToRight
+    dx = -dx;
+    dy = -dy;
+    x0 = x1;
+    y0 = y1;
+  }
+  int sy = 1;
+  if (dy < 0) {
+    dy = -dy;
+    sy = -1;
+  }
+  const bool vert = dy > dx;
+  const int major = vert ? dy : dx, minor = vert ? dx : dy;
+  int err = major - 2 * minor;
+  int x = x0, y = y0;
+  for (int k = 0; k <= major; ++k) {
+    if (x >= 0 && x < W && y >= 0 && y < H) map_put(img, HW, mask, (long)y * W + x);
+    const bool step = err < 0;
+    err += -2 * minor + (step ? 2 * major : 0);
+    if (vert) {
+      y += sy;
+      x += step ? 1 : 0;
+    } else {
+      x += 1;
+      y += step ? sy : 0;
+    }
+  }
+}
+
+__global__ void map_fill_kernel(const long* __restrict__ edges, const int* __restrict__ polys,
+                                const int* __restrict__ rows, long n_rows, const long* __restrict__ base, int H,
+                                int W, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rows) return;
+  const int p = rows[2 * i], y = rows[2 * i + 1];
+  const int e0 = polys[3 * p], ne = polys[3 * p + 1], mask = polys[3 * p + 2];
+  long xs[kMapMaxEdges];
+  int n = 0;
+  for (int e = 0; e < ne; ++e) {  // edge: y0, y1, x_top (16.16), dx (16.16)
+    const long* E = edges + 4 * (long)(e0 + e);
+    if (E[0] <= y && y < E[1]) {
+      const long x = E[2] + (long)(y - E[0]) * E[3];
+      int j = n++;
+      while (j > 0 && xs[j - 1] > x) {  // insertion sort
+        xs[j] = xs[j - 1];
+        --j;
+      }
+      xs[j] = x;
+    }
+  }
+  float* img = out + base[p];
+  const long HW = (long)H * W;
+  for (int k = 0; k + 1 < n; k += 2) {
+    int x1 = (int)(xs[k] >> 16), x2 = (int)(xs[k + 1] >> 16);
+    if (x1 < W && x2 >= 0) {
+      x1 = x1 < 0 ? 0 : x1;
+      x2 = x2 >= W ? W - 1 : x2;
+      for (int x = x1; x <= x2; ++x) map_put(img, HW, mask, (long)y * W + x);
+    }
+  }
+}
+}  // namespace
+
+extern "C" int ivit_map_raster(const int* seg, long n_seg, const long* seg_base, const long* edges,
+                               const int* polys, long n_polys, const long* poly_base, const int* rows, long n_rows,
+                               long max_edges, long H, long W, float* out, void* stream) {
+  IVIT_CHECK_ARG(H > 0 && W > 0 && H < 65536 && W < 65536, "ivit_map_raster: bad plane size %ldx%ld", H, W);
+  IVIT_CHECK_ARG(max_edges <= kMapMaxEdges, "ivit_map_raster: a polygon has %ld edges (max %d)", max_edges,
+                 kMapMaxEdges);
+  IVIT_CHECK_ARG(n_seg == 0 || (seg && seg_base), "ivit_map_raster: null segment table");
+  IVIT_CHECK_ARG(n_rows == 0 || (edges && polys && poly_base && rows), "ivit_map_raster: null fill tables");
+  (void)n_polys;
+  hipStream_t st = ivit_stream(stream);
+  if (n_seg > 0)
+    hipLaunchKernelGGL(map_segments_kernel, dim3(ivit_cdiv(n_seg, 256)), dim3(256), 0, st, seg, n_seg, seg_base,
+                       (int)H, (int)W, out);
+  if (n_rows > 0)
+    hipLaunchKernelGGL(map_fill_kernel, dim3(ivit_cdiv(n_rows, 256)), dim3(256), 0, st, edges, polys, rows, n_rows,
+                       poly_base, (int)H, (int)W, out);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}

@@ -133,6 +133,8 @@ class KernelTimer:
 
     @classmethod
     def span(cls, name):
+        """Record a start event on the CURRENT stream (the one the launch goes to) and return
+        the end event for the caller to record after the launch; None when not enabled."""
         if name not in cls.enabled:
             return None
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -144,6 +146,10 @@ class KernelTimer:
     def mean_ms(cls, name):
         r = cls.records.get(name, [])
         return sum(s.elapsed_time(e) for s, e in r) / len(r) if r else float("nan")
+
+    @classmethod
+    def count(cls, name):
+        return len(cls.records.get(name, []))
 
 
 def attn_fwd(qkv, B, N, H, cdt):
@@ -160,9 +166,8 @@ def attn_fwd(qkv, B, N, H, cdt):
 
 # bf16 ViT blocks: the qkv projection writes its Q block as q * log2(e)/sqrt(64)
 # (ivit_linear_fwd_qs) and attention runs on the prescaled Q (ivit_attn_fwd_q2 / _bwd_q2):
-# no per-score scaling FMA in the forward and dQ kernels. IVIT_ATTN_Q2=0 restores the
-# unscaled form (A/B).
-ATTN_Q2 = os.environ.get("IVIT_ATTN_Q2", "1") == "1"
+# no per-score scaling FMA in the forward and dQ kernels. The f32 parity path keeps the plain
+# layout (ivit_attn_fwd / _bwd).
 Q2_SCALE = 1.4426950408889634 / 8.0  # log2(e) / sqrt(Dh), Dh = 64
 
 
@@ -190,8 +195,11 @@ def attn_fwd_q2(qkv, B, N, H):
 def attn_bwd_q2(qkv, out, dout, lse, B, N, H):
     dqkv = torch.empty_like(qkv)
     ws = workspace(lib.ivit_attn_workspace(BF16, B, N, H, 64, 1), qkv.device)
+    ev = KernelTimer.span("attn_bwd")
     lib.ivit_attn_bwd_q2(ptr(qkv), ptr(out), ptr(dout), ptr(lse), B, N, H, 64, ptr(dqkv), ptr(ws), ws.numel(),
                          stream())
+    if ev is not None:
+        ev.record()
     return dqkv
 
 
@@ -389,7 +397,7 @@ class ViTBlockFn(torch.autograd.Function):
         cd = tdtype(cdt)
         wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
         ln1, m1, r1 = layernorm_fwd(x, n1w, n1b, eps, cd)
-        q2 = ATTN_Q2 and cdt == BF16
+        q2 = cdt == BF16
         if q2:
             qkv = qkv_fwd_q2(ln1, wq, qkvb, H * 64)
             o, lse = attn_fwd_q2(qkv, B, N, H)

@@ -12,7 +12,7 @@ import torch
 
 from _lib import lib, ptr, stream, workspace
 from constants import (ANCHOR_CONFIGS_PAPER, BEV_PIXEL_OFFSET_X, BEV_PIXEL_OFFSET_Y, GRID_HEIGHT_PX, GRID_WIDTH_PX,
-                       INTENTIONS_MAP, LIDAR_HEIGHT_CHANNELS, LIDAR_SWEEPS, VOXEL_SIZE_M, Z_MAX, Z_MIN)
+                       INTENTIONS_MAP, LIDAR_HEIGHT_CHANNELS, LIDAR_SWEEPS, MAP_CHANNELS, VOXEL_SIZE_M, Z_MAX, Z_MIN)
 
 
 def _dev(device):
@@ -471,3 +471,173 @@ def augment_bev_batch(lidar_bev: torch.Tensor, map_bev: torch.Tensor, gt_list, o
         params.append(p)
     _run_bev_passes(jobs)
     return lo, mo, gts, params
+
+
+# ---------------------------------------------------------------------------- HD-map raster
+# rasterize_map_ego_centric (utils.py:108-182). The host part is the
+# reference's own flow (JSON, ego yaw from the quaternion, world -> pixel with np.round, in-grid
+# point filtering, which primitive goes to which channel); the scan conversion — cv2.polylines /
+# cv2.fillPoly, the CPU-heavy part — runs on the GPU (ivit_map_raster): one launch draws every
+# segment and polygon edge (cv::Line, 8-connected), one fills every polygon scanline.
+MAP_MARK_CHANNELS = {"DASHED_WHITE": 6, "SOLID_WHITE": 7, "SOLID_YELLOW": 8}
+
+
+def get_ego_centric_transform_matrix(ego_translation_xy: np.ndarray, ego_yaw: float) -> np.ndarray:
+    """utils.py:35-45: world -> ego 2-D homogeneous transform (rotation by -yaw)."""
+    c, s = np.cos(-ego_yaw), np.sin(-ego_yaw)
+    rot = np.array([[c, -s], [s, c]])
+    T = np.eye(3)
+    T[:2, :2] = rot
+    T[:2, 2] = -rot @ ego_translation_xy
+    return T
+
+
+def world_to_bev_pixel(points_world_xy: np.ndarray, ego_tf_matrix: np.ndarray, H: int = GRID_HEIGHT_PX,
+                       W: int = GRID_WIDTH_PX) -> np.ndarray:
+    """utils.py:47-60: (x, y) world -> (col, row) pixels, np.round (half to even) then int."""
+    if points_world_xy.shape[0] == 0:
+        return np.empty((0, 2), dtype=int)
+    homo = np.hstack([points_world_xy, np.ones((points_world_xy.shape[0], 1))])
+    ego = (ego_tf_matrix @ homo.T).T[:, :2]
+    px = W / 2.0 + ego[:, 1] / VOXEL_SIZE_M
+    py = H * 3.0 / 4.0 - ego[:, 0] / VOXEL_SIZE_M
+    return np.round(np.vstack([px, py]).T).astype(int)
+
+
+def _map_pixels(points, T, H, W):
+    """to_bev_pixel_local (utils.py:131-145)."""
+    if not points:
+        return np.empty((0, 2), dtype=int)
+    valid = [p for p in points if isinstance(p, dict) and 'x' in p and 'y' in p]
+    if not valid:
+        return np.empty((0, 2), dtype=int)
+    pix = world_to_bev_pixel(np.array([[p['x'], p['y']] for p in valid]), T, H, W)
+    keep = (pix[:, 0] >= 0) & (pix[:, 0] < W) & (pix[:, 1] >= 0) & (pix[:, 1] < H)
+    return pix[keep]
+
+
+def _map_primitives(map_data, ego_pose, H, W):
+    """-> (polylines [(pts, plane mask)], polygons [(pts, plane mask)]) in the reference's order
+    (utils.py:147-180); None when the ego quaternion is invalid (the reference's empty map)."""
+    from scipy.spatial.transform import Rotation
+    q = [ego_pose['qx'], ego_pose['qy'], ego_pose['qz'], ego_pose['qw']]
+    try:
+        yaw = Rotation.from_quat(q).as_euler('xyz')[2]
+    except ValueError:
+        return None
+    T = get_ego_centric_transform_matrix(np.array([ego_pose['tx_m'], ego_pose['ty_m']]), yaw)
+    lines, polys = [], []
+    for _, lane in map_data.get("lane_segments", {}).items():
+        lpx = _map_pixels(lane.get("left_lane_boundary", []), T, H, W)
+        rpx = _map_pixels(lane.get("right_lane_boundary", []), T, H, W)
+        if len(lpx) > 1 and len(rpx) > 1:
+            poly = np.vstack([lpx, np.flipud(rpx)])
+            if poly.shape[0] >= 3:
+                mask = 1 | (16 if lane.get("is_intersection", False) else 0) | (32 if lane.get("lane_type") == "BUS" else 0)
+                polys.append((poly, mask))
+        lm, rm = lane.get("left_lane_mark_type", ""), lane.get("right_lane_mark_type", "")
+        if len(lpx) > 1:
+            lines.append((lpx, 2 | (1 << MAP_MARK_CHANNELS[lm] if lm in MAP_MARK_CHANNELS else 0)))
+        if len(rpx) > 1:
+            lines.append((rpx, 4 | (1 << MAP_MARK_CHANNELS[rm] if rm in MAP_MARK_CHANNELS else 0)))
+    for _, cw in map_data.get("pedestrian_crossings", {}).items():
+        poly = cw.get('polygon', [])
+        if poly:
+            px = _map_pixels(poly, T, H, W)
+            if len(px) >= 3:
+                polys.append((px, 8))
+    return lines, polys
+
+
+def _map_tables(prims_per_image, H, W, img_stride):
+    """Host tables of ivit_map_raster for a batch (image b's planes start at b * img_stride)."""
+    seg, seg_base, edges, polys, poly_base, rows = [], [], [], [], [], []
+    max_edges = 0
+    for b, prims in enumerate(prims_per_image):
+        if prims is None:
+            continue
+        lines, pgs = prims
+        base = b * img_stride
+        for pts, mask in lines:
+            p = np.asarray(pts, np.int64)
+            s = np.concatenate([p[:-1], p[1:], np.full((len(p) - 1, 1), mask)], 1)
+            seg.append(s)
+            seg_base.append(np.full(len(s), base))
+        for pts, mask in pgs:
+            p = np.asarray(pts, np.int64)
+            prev = np.roll(p, 1, axis=0)  # edge i: vertex i-1 -> vertex i (the closing edge first)
+            s = np.concatenate([prev, p, np.full((len(p), 1), mask)], 1)
+            seg.append(s)
+            seg_base.append(np.full(len(s), base))
+            xa, ya, xb, yb = prev[:, 0], prev[:, 1], p[:, 0], p[:, 1]
+            nh = ya != yb
+            if nh.sum() < 2:
+                continue
+            xa, ya, xb, yb = xa[nh], ya[nh], xb[nh], yb[nh]
+            num, den = (xb - xa) << 16, yb - ya
+            dx = np.abs(num) // np.abs(den) * np.where((num >= 0) == (den > 0), 1, -1)  # C truncation
+            top_a = ya < yb
+            e = np.stack([np.where(top_a, ya, yb), np.where(top_a, yb, ya),
+                          np.where(top_a, xa, xb) << 16, dx], 1)
+            first = sum(len(x) for x in edges)
+            edges.append(e)
+            max_edges = max(max_edges, len(e))
+            pi = len(polys)
+            polys.append((first, len(e), mask))
+            poly_base.append(base)
+            y0, y1 = max(int(e[:, 0].min()), 0), min(int(e[:, 1].max()), H)
+            if y1 > y0:
+                rows.append(np.stack([np.full(y1 - y0, pi), np.arange(y0, y1)], 1))
+    cat = (lambda xs, shape, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(shape, dt))
+    return (cat(seg, (0, 5), np.int32), cat(seg_base, (0,), np.int64), cat(edges, (0, 4), np.int64),
+            np.array(polys, np.int32).reshape(-1, 3), np.array(poly_base, np.int64), cat(rows, (0, 2), np.int32),
+            max_edges)
+
+
+def _load_map(m):
+    import json
+    if m is None or isinstance(m, dict):
+        return m
+    try:
+        with open(m, "r") as f:
+            return json.load(f)
+    except Exception as e:  # noqa: BLE001  (the reference's behaviour, utils.py:111-116)
+        print(f"Error loading map JSON {m}: {e}. Returning empty map.")
+        return None
+
+
+def rasterize_map_batch(items, H: int = GRID_HEIGHT_PX, W: int = GRID_WIDTH_PX, out: torch.Tensor | None = None,
+                        device=None) -> torch.Tensor:
+    """rasterize_map_ego_centric for a batch: items = [(map JSON path or parsed dict, ego pose
+    with tx_m, ty_m, qx, qy, qz, qw)] -> (B, 9, H, W) f32 on the GPU (``out`` may be a collated
+    map_bev tensor: it is zero-filled and drawn in place), one launch per stage."""
+    d = _dev(device if out is None else out.device)
+    B = len(items)
+    if out is None:
+        out = torch.zeros((B, MAP_CHANNELS, H, W), dtype=torch.float32, device=d)
+    else:
+        if out.shape != (B, MAP_CHANNELS, H, W) or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError("rasterize_map_batch: out must be a contiguous (B, 9, H, W) float32 tensor")
+        out.zero_()
+    prims = []
+    for m, pose in items:
+        md = _load_map(m)
+        pr = None if md is None else _map_primitives(md, pose, H, W)
+        if md is not None and pr is None:
+            print("Warning: Invalid ego quaternion. Returning empty map.")
+        prims.append(pr)
+    seg, seg_base, edges, polys, poly_base, rows, max_edges = _map_tables(prims, H, W, MAP_CHANNELS * H * W)
+    if len(seg) == 0 and len(rows) == 0:
+        return out
+    t = [torch.from_numpy(a).pin_memory().to(d, non_blocking=True) if a.size else None
+         for a in (seg, seg_base, edges, polys, poly_base, rows)]
+    lib.ivit_map_raster(ptr(t[0]), len(seg), ptr(t[1]), ptr(t[2]), ptr(t[3]), len(polys), ptr(t[4]), ptr(t[5]),
+                        len(rows), max_edges, H, W, ptr(out), stream())
+    return out
+
+
+def rasterize_map_ego_centric(map_json_path, current_ego_pose, device=None) -> torch.Tensor:
+    """utils.py:108-182 -> (9, GRID_H, GRID_W) float32 {0, 1} on the GPU (the reference returns
+    the same array on the host). Channels: 0 lane area, 1 / 2 left / right boundaries, 3
+    crosswalks, 4 intersections, 5 bus lanes, 6-8 dashed-white / solid-white / solid-yellow marks."""
+    return rasterize_map_batch([(map_json_path, current_ego_pose)], device=device)[0]
