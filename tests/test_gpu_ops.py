@@ -139,8 +139,10 @@ def test_attention(B, N, H, cd):
     assert _rel(o.float(), oref.detach()) < tol
     # bf16 path: the row sums l are accumulated on the MFMA pipe over the bf16-rounded
     # probabilities (exactly the weights P.V uses), so lse = m + log l carries their rounding
-    # (~1e-4 relative at N <= 4501); the f32 path sums f32 probabilities.
-    assert _rel(lse, lref.detach()) < (1e-5 if cdt == F32 else 3e-4)
+    # (~1e-4 relative at N <= 4501), plus the in-kernel bf16 rounding of q * log2(e)/8 (the
+    # prescaled-Q forward serves the plain entry point too, as in the q2 test below); the f32
+    # path sums f32 probabilities.
+    assert _rel(lse, lref.detach()) < (1e-5 if cdt == F32 else 6e-4)
     do = torch.randn(B * N, H * 64)
     dod = ops.cast(do.to(DEV), cd)
     oref.backward(dod.float().cpu().double())
@@ -201,7 +203,7 @@ def test_attention_large_grid_bf16():
     oref = (torch.softmax(s, -1) @ vv).transpose(1, 2).reshape(B * N, H * 64)
     lref = torch.logsumexp(s, -1)
     assert _rel(o.float(), oref.detach()) < 2e-2
-    assert _rel(lse, lref.detach()) < 1e-4
+    assert _rel(lse, lref.detach()) < 3e-4  # incl. the in-kernel bf16 rounding of q * log2(e)/8
     oref.backward(dod.float())
     g = qr.grad.reshape(B * N, 3, H * 64)
     d = dq.reshape(B * N, 3, H * 64)
