@@ -376,3 +376,38 @@ def test_full_grid_fp32_forward_vs_oracle():
         sd = make_state_dict(cfg, seed=0)
         rc, rb, ri = O.intentnet_forward(sd, lidar, mp, cfg, training=False)
     assert _rel(c, rc) < 1e-3 and _rel(b, rb) < 1e-3 and _rel(i, ri) < 1e-3
+
+
+def test_config4_eval_batch32_full_grid_vs_oracle():
+    """BASELINE config 4 end to end (eval_vit.py:136-187): B = 32 full-grid bf16 inference, then
+    sigmoid >= 0.1, decode, NMS(0.2), intention argmax for all 32 samples through the batched
+    device post-processing (ivit_nms_batched), against the oracle: decode within 1e-5 rel of the
+    oracle's decode, NMS keep indices bit-exact (torchvision CPU semantics) per sample on the same
+    boxes / scores, scores and intentions equal."""
+    import model_vit
+    import utils
+    from synthetic import synthetic_batch
+    torch.manual_seed(0)
+    m = model_vit.IntentNetViT(backbone_cfg={"img_size": (400, 720)}).to(DEV).set_compute_dtype(torch.bfloat16).eval()
+    batch = synthetic_batch(32, (400, 720), torch.Generator().manual_seed(1234), device=DEV)
+    anchors = utils.generate_anchors(400, 720, 8, device=DEV)
+    with torch.inference_mode():
+        cls, box, it = m(batch["lidar_bev"], batch["map_bev"])
+        preds = utils.postprocess_batch(cls, box, it, anchors, 0.1, 0.2)
+    assert len(preds) == 32
+    a_cpu = anchors.cpu()
+    total = 0
+    for b in range(32):
+        sc = torch.sigmoid(cls[b].reshape(-1).float())
+        idx = torch.nonzero(sc >= 0.1).squeeze(1)
+        dec = utils.decode_box_predictions(box[b].reshape(-1, 6)[idx], anchors[idx])
+        rdec = O.decode_boxes(box[b].reshape(-1, 6)[idx].float().cpu(), a_cpu[idx.cpu()])
+        assert _rel(dec, rdec) < 1e-5
+        keep = O.nms_numpy(dec.cpu().numpy(), sc[idx].cpu().numpy(), 0.2)
+        p = preds[b]
+        assert torch.equal(p["pred_scores"].cpu(), sc[idx].cpu()[keep])
+        assert torch.equal(p["pred_boxes_xywha"].cpu(), dec.cpu()[keep])
+        ri = torch.argmax(it[b].reshape(-1, 8)[idx].float().cpu()[keep], dim=-1)
+        assert torch.equal(p["pred_intentions"].cpu(), ri)
+        total += len(keep)
+    assert total > 32 * 100  # random init: every anchor passes 0.1, NMS keeps thousands
