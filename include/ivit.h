@@ -137,6 +137,11 @@ int ivit_cast(const void* x, int x_dtype, void* y, int y_dtype, long n, void* st
 /* out = (a [+ b]) [* gelu'(pre)] [* row_scale[i / (cols * rows_per_scale)]] elementwise over n values. */
 int ivit_add_act_grad(const void* a, int a_dtype, const void* b, int b_dtype, const void* pre, int pre_dtype,
                       const float* row_scale, long row_elems, void* out, int out_dtype, long n, void* stream);
+/* Standalone activation modules (nn.GELU exact-erf / nn.ReLU used outside the fused GEMM
+ * epilogues, e.g. a caller running adapter_lidar[2] on its own): y = act(x); dx = dy * act'(x). */
+int ivit_act_fwd(int act, const void* x, int x_dtype, void* y, int y_dtype, long n, void* stream);
+int ivit_act_bwd(int act, const void* dy, int dy_dtype, const void* x, int x_dtype, void* dx, int dx_dtype, long n,
+                 void* stream);
 int ivit_colsum(const void* X, int x_dtype, long ld, long rpb, long rstride, long roff, long M, long N, float* out,
                 int accumulate, void* work, long work_bytes, void* stream);
 long ivit_colsum_workspace(long M, long N);

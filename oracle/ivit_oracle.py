@@ -105,15 +105,17 @@ def _bn(x, sd, p, training, momentum=0.1):
                         training=training, momentum=momentum, eps=1e-5)
 
 
-def fusion_forward(sd, x, layers=2, training=True):
-    """model_vit.py:19-34 BasicBlock ×layers (+1×1 downsample on block 0), :125-132."""
+def fusion_forward(sd, x, layers=2, training=True, stride=1):
+    """model_vit.py:19-34 BasicBlock ×layers (+1×1 downsample on block 0; block 0 carries
+    fusion_block_stride on conv1 and the downsample), :125-132."""
     for li in range(layers):
         p = f"backbone.fusion_block.{li}."
+        s = stride if li == 0 else 1
         idn = x
-        o = F.relu(_bn(F.conv2d(x, sd[p + "conv1.weight"], padding=1), sd, p + "bn1.", training))
+        o = F.relu(_bn(F.conv2d(x, sd[p + "conv1.weight"], padding=1, stride=s), sd, p + "bn1.", training))
         o = _bn(F.conv2d(o, sd[p + "conv2.weight"], padding=1), sd, p + "bn2.", training)
         if (p + "downsample.0.weight") in sd:
-            idn = _bn(F.conv2d(x, sd[p + "downsample.0.weight"]), sd, p + "downsample.1.", training)
+            idn = _bn(F.conv2d(x, sd[p + "downsample.0.weight"], stride=s), sd, p + "downsample.1.", training)
         x = F.relu(o + idn)
     return x
 
@@ -141,7 +143,7 @@ def intentnet_forward(sd, lidar, map_bev, cfg, training=False, drop_path_scales=
         dl, dm = drop_path_scales
     fl = _stream(sd, "lidar", lidar, al["num_heads"], depth_l, dl, attn, checkpoint)
     fm = _stream(sd, "map", map_bev, am["num_heads"], depth_m, dm, attn, checkpoint)
-    feat = fusion_forward(sd, torch.cat([fl, fm], dim=1), cfg["layers"], training)
+    feat = fusion_forward(sd, torch.cat([fl, fm], dim=1), cfg["layers"], training, cfg.get("fusion_stride", 1))
     return heads_forward(sd, feat, cfg["num_anchors"], cfg["num_classes"])
 
 

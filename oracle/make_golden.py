@@ -103,6 +103,50 @@ def gen_model_small():
     print("model_small: loss", rec["train_loss"], "ds", rec["train_loss_ds"])
 
 
+def gen_model_stride2():
+    """The reference's OWN IntentNetViT with fusion_block_stride=2 (model_vit.py:55,125-128: block
+    0's conv1 and downsample strided, heads at H/16 x W/16, effective_head_stride 16) at the
+    32x48 grid: eval + train outputs, loss (downsampling off), gradient samples, BN stats."""
+    import loss as ref_loss
+    import model_vit as ref_model
+    import utils as ref_utils
+    cfg = model_cfg(img_size=SMALL_IMG, fusion_stride=2)
+    sd = make_state_dict(cfg, seed=0)
+    lidar, mp, _ = O.synthetic_batch(2, SMALL_IMG, seed=1234)
+    gts = small_gt()
+    anchors = ref_utils.generate_anchors(SMALL_IMG[0], SMALL_IMG[1], 16)
+    m = ref_model.IntentNetViT(backbone_cfg={"img_size": SMALL_IMG, "lidar_input_channels": 290,
+                                             "map_input_channels": 9, "drop_path_rate_lidar": 0.0,
+                                             "drop_path_rate_map": 0.0, "fusion_block_stride": 2})
+    assert m.effective_head_stride == 16
+    m.load_state_dict(refshim.timm_to_hf_state(sd), strict=True)
+    rec = {"cfg": json.dumps(cfg), "anchors": anchors.numpy()}
+    m.eval()
+    with torch.no_grad():
+        c, b, it = m(lidar, mp)
+    rec.update(eval_cls=c.numpy(), eval_box=b.numpy(), eval_int=it.numpy())
+    m.train()
+    c, b, it = m(lidar, mp)
+    d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False)(c, b, it, anchors, gts)
+    d["loss"].backward()
+    rec.update(train_cls=c.detach().numpy(), train_box=b.detach().numpy(), train_int=it.detach().numpy(),
+               train_loss=np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]),
+                                    float(d["intent_loss"]), float(d["num_pos_anchors"])]))
+    grads = refshim.hf_grads_to_timm({k: p.grad for k, p in m.named_parameters() if p.grad is not None})
+    names = sorted(grads)
+    samples, strides = zip(*[_sample(grads[k]) for k in names])
+    rec.update(grad_names=np.array(names), grad_abssum=np.array([float(grads[k].double().abs().sum()) for k in names]),
+               grad_samples=np.stack(samples), grad_strides=np.array(strides))
+    bn = {k: v for k, v in m.state_dict().items() if "running_" in k}
+    rec.update(bn_names=np.array(sorted(bn)), bn_values=np.stack([bn[k].numpy() for k in sorted(bn)]))
+    osd = {k: v.clone() for k, v in sd.items()}
+    with torch.no_grad():
+        oc, _, _ = O.intentnet_forward(osd, lidar, mp, cfg, training=False)
+    assert float((oc - torch.from_numpy(rec["eval_cls"])).abs().max()) < 1e-4, "oracle != reference (stride 2)"
+    np.savez_compressed(os.path.join(OUT, "model_stride2.npz"), **rec)
+    print("model_stride2: cls", c.shape, "loss", rec["train_loss"])
+
+
 def gen_geometry():
     import loss as ref_loss
     import utils as ref_utils
@@ -524,3 +568,4 @@ if __name__ == "__main__":
     gen_cnn_small()
     gen_loss_options()
     gen_map_raster()
+    gen_model_stride2()

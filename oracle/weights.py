@@ -24,12 +24,12 @@ VIT_ARCH = {
 
 def model_cfg(img_size=(400, 720), lidar_ch=290, map_ch=9, vit_lidar="vit_small_patch8_224",
               vit_map="vit_small_patch8_224", lidar_adapter=192, map_adapter=192, planes=512,
-              layers=2, num_anchors=5, num_classes=8, depth=None):
+              layers=2, num_anchors=5, num_classes=8, depth=None, fusion_stride=1):
     """Flat description of the IntentNetViT shapes (model_vit.py:145-177 defaults)."""
     return dict(img_size=tuple(img_size), lidar_ch=lidar_ch, map_ch=map_ch, vit_lidar=vit_lidar,
                 vit_map=vit_map, lidar_adapter=lidar_adapter, map_adapter=map_adapter,
                 planes=planes, layers=layers, num_anchors=num_anchors, num_classes=num_classes,
-                depth=depth)
+                depth=depth, fusion_stride=fusion_stride)
 
 
 def _vit_shapes(prefix, arch, in_ch, img_size, depth_override=None):

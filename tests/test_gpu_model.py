@@ -51,6 +51,52 @@ def test_small_eval_vs_golden(small):
     assert _rel(c, z["eval_cls"]) < 1e-3 and _rel(b, z["eval_box"]) < 1e-3 and _rel(i, z["eval_int"]) < 1e-3
 
 
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_fusion_stride2_vs_golden(cd):
+    """fusion_block_stride=2 (model_vit.py:55,125-128): strided block-0 conv1 / downsample as
+    im2col + GEMM, heads at H/16 x W/16, effective_head_stride 16 — eval and train outputs, loss,
+    parameter gradients and BN running stats vs the reference's own model (f32: 1e-3 rel; bf16:
+    outputs within 6e-2)."""
+    import loss as L
+    import model_vit
+    import utils
+    z = golden("model_stride2.npz")
+    cfg = json.loads(str(z["cfg"]))
+    cfg["img_size"] = tuple(cfg["img_size"])
+    m = model_vit.IntentNetViT(backbone_cfg={"img_size": cfg["img_size"], "drop_path_rate_lidar": 0.0,
+                                             "drop_path_rate_map": 0.0, "fusion_block_stride": 2})
+    assert m.effective_head_stride == 16
+    m.load_state_dict(make_state_dict(cfg, seed=0), strict=True)
+    m = m.to(DEV).set_compute_dtype(cd)
+    lidar, mp, _ = O.synthetic_batch(2, cfg["img_size"], seed=1234)
+    tol = 1e-3 if cd == torch.float32 else 6e-2
+    m.eval()
+    with torch.no_grad():
+        c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    assert c.shape == (2, 30, 1) and b.shape == (2, 30, 6) and i.shape == (2, 30, 8)
+    assert _rel(c, z["eval_cls"]) < tol and _rel(b, z["eval_box"]) < tol and _rel(i, z["eval_int"]) < tol
+    m.train()
+    c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    assert _rel(c.detach(), z["train_cls"]) < tol
+    anchors = utils.generate_anchors(*cfg["img_size"], 16)
+    assert np.array_equal(anchors.cpu().numpy(), z["anchors"])
+    d = L.DetectionIntentionLoss(apply_intention_downsampling=False)(c, b, i, anchors, _gts(golden("model_small.npz"), 2))
+    got = [float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]),
+           float(d["num_pos_anchors"])]
+    np.testing.assert_allclose(got, z["train_loss"], rtol=1e-3 if cd == torch.float32 else 5e-2)
+    if cd != torch.float32:
+        return
+    d["loss"].backward()
+    sd = dict(m.named_parameters())
+    for name, gas, smp, st in zip(z["grad_names"], z["grad_abssum"], z["grad_samples"], z["grad_strides"]):
+        g = sd[str(name)].grad
+        assert g is not None, name
+        assert float(g.double().abs().sum()) == pytest.approx(gas, rel=1e-3, abs=1e-6), name
+    bufs = dict(m.named_buffers())
+    for name, val in zip(z["bn_names"], z["bn_values"]):
+        np.testing.assert_allclose(bufs[str(name)].cpu().numpy(), val, rtol=1e-4, atol=1e-5)
+
+
 def test_small_train_loss_grads_vs_golden(small):
     import loss as L
     import utils

@@ -402,3 +402,33 @@ def test_nms_random_vs_oracle():
         s = torch.round(torch.rand(n, generator=g) * 8) / 8
         keep = utils.apply_nms(b.to(DEV), s.to(DEV), 0.2).cpu().numpy()
         assert np.array_equal(keep, O.nms_numpy(b.numpy(), s.numpy(), 0.2)), n
+
+
+def test_standalone_activation_and_head_modules():
+    """Module forwards outside the fused path run the device kernels too: nn.GELU / nn.ReLU
+    (ivit_act_fwd / _bwd) and the det / intention heads' 35 / 40-channel 3x3 convs (im2col +
+    GEMM; heads.py:18-25,39-43 view / permute) vs torch f32 references."""
+    import heads
+    import layers
+    x = torch.randn(3, 5, 7, 11)
+    for mod, ref in ((layers.GELU(), torch.nn.functional.gelu), (layers.ReLU(), torch.relu)):
+        xd = x.to(DEV).requires_grad_(True)
+        y = mod(xd)
+        y.backward(torch.ones_like(y))
+        xr = x.clone().requires_grad_(True)
+        yr = ref(xr)
+        yr.backward(torch.ones_like(yr))
+        assert _rel(y.detach(), yr.detach()) < 1e-6 and _rel(xd.grad, xr.grad) < 1e-6
+    f = torch.randn(2, 64, 6, 9)
+    dh = heads.DetectionHead(64).to(DEV)
+    ih = heads.IntentionHead(64).to(DEV)
+    c, b = dh(f.to(DEV))
+    it = ih(f.to(DEV))
+    w = {k: v.detach().cpu() for k, v in dh.state_dict().items()}
+    o = torch.nn.functional.conv2d(f, w["conv.weight"], w["conv.bias"], padding=1)
+    o = o.view(2, 5, 7, 6, 9).permute(0, 3, 4, 1, 2)
+    assert c.shape == (2, 6, 9, 5) and b.shape == (2, 6, 9, 5, 6)
+    assert _rel(c, o[..., 0]) < 1e-5 and _rel(b, o[..., 1:]) < 1e-5
+    wi = {k: v.detach().cpu() for k, v in ih.state_dict().items()}
+    oi = torch.nn.functional.conv2d(f, wi["conv.weight"], wi["conv.bias"], padding=1).view(2, 5, 8, 6, 9)
+    assert _rel(it, oi.permute(0, 3, 4, 1, 2)) < 1e-5

@@ -242,3 +242,20 @@ def test_cv_raster_primitives():
     img = np.zeros((6, 6), np.uint8)
     O.cv_fill_poly(img, [(0, 2), (5, 2), (3, 2)])  # all on one row: only the edge lines
     assert img.sum() == 6 and img[2].all()
+
+
+def test_fusion_stride2_oracle_vs_golden():
+    """fusion_block_stride=2 (model_vit.py:55,125-128): the oracle's strided fusion block vs the
+    reference's own model."""
+    z = golden("model_stride2.npz")
+    cfg = json.loads(str(z["cfg"]))
+    cfg["img_size"] = tuple(cfg["img_size"])
+    sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v.clone())
+          for k, v in make_state_dict(cfg, seed=0).items()}
+    lidar, mp, _ = O.synthetic_batch(2, cfg["img_size"], seed=1234)
+    c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=True)
+    np.testing.assert_allclose(c.detach().numpy(), z["train_cls"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(i.detach().numpy(), z["train_int"], rtol=1e-4, atol=1e-4)
+    d = O.detection_loss(c, b, i, torch.from_numpy(z["anchors"]), _gts(golden("model_small.npz"), 2),
+                         downsampling=False)
+    np.testing.assert_allclose(_vec(d), z["train_loss"], rtol=1e-5)

@@ -29,6 +29,21 @@ __global__ void add_act_grad_kernel(const void* a, int adt, const void* b, int b
   stv(out, odt, i, v);
 }
 
+// standalone activation modules (nn.GELU exact erf / nn.ReLU) and their input gradients
+__global__ void act_fwd_kernel(int act, const void* x, int xdt, void* y, int ydt, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = ldv(x, xdt, i);
+  stv(y, ydt, i, act == IVIT_ACT_GELU ? gelu_erf(v) : (act == IVIT_ACT_RELU ? (v > 0.f ? v : 0.f) : v));
+}
+__global__ void act_bwd_kernel(int act, const void* dy, int dydt, const void* x, int xdt, void* dx, int dxdt,
+                               long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float g = ldv(dy, dydt, i), v = ldv(x, xdt, i);
+  stv(dx, dxdt, i, act == IVIT_ACT_GELU ? g * gelu_erf_grad(v) : (act == IVIT_ACT_RELU ? (v > 0.f ? g : 0.f) : g));
+}
+
 __global__ void copy_cols_kernel(const void* src, long lds, void* dst, long ldd, long rows, long cols, int dt) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows * cols) return;
@@ -172,6 +187,25 @@ extern "C" int ivit_adamw_shadow(long n_tensors, void* const* params, void* cons
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
                      exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, shadows);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_act_fwd(int act, const void* x, int x_dtype, void* y, int y_dtype, long n, void* stream) {
+  IVIT_CHECK_ARG(act == IVIT_ACT_GELU || act == IVIT_ACT_RELU || act == IVIT_ACT_NONE, "ivit_act_fwd: bad act %d", act);
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(act_fwd_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), act, x, x_dtype, y,
+                     y_dtype, n);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_act_bwd(int act, const void* dy, int dy_dtype, const void* x, int x_dtype, void* dx, int dx_dtype,
+                            long n, void* stream) {
+  IVIT_CHECK_ARG(act == IVIT_ACT_GELU || act == IVIT_ACT_RELU || act == IVIT_ACT_NONE, "ivit_act_bwd: bad act %d", act);
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), act, dy, dy_dtype, x,
+                     x_dtype, dx, dx_dtype, n);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

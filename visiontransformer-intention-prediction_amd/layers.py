@@ -11,7 +11,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 import ops
-from _lib import ACT_NONE, BF16, F32
+from _lib import ACT_GELU, ACT_NONE, ACT_RELU, BF16, F32, dt, lib, ptr, stream, tdtype
 
 
 def _cdt(dtype):
@@ -84,6 +84,76 @@ class _Conv2dFn(torch.autograd.Function):
         return dx.reshape(B, H, W, C).permute(0, 3, 1, 2).contiguous(), dw, db, None
 
 
+class _ConvColsFn(torch.autograd.Function):
+    """NHWC conv, any k / stride / zero pad (nn.Conv2d geometry): im2col + GEMM. The GEMM's K
+    (k*k*Cin) and N (Cout) are padded to multiples of 8 with zero columns / rows."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, s, p, cdt):
+        B, H, W, C = x.shape
+        Cout, Cin, k, _ = w.shape
+        if Cin != C:
+            raise ValueError(f"conv expects {Cin} input channels, got {C}")
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        K = k * k * C
+        Kp, Np = _r8(K), _r8(Cout)
+        x = x.contiguous()
+        cols = torch.empty((B * Ho * Wo, Kp), dtype=tdtype(cdt), device=x.device)
+        lib.ivit_im2col(dt(x), ptr(x), B, H, W, C, k, s, p, Ho, Wo, ptr(cols), Kp, cdt, stream())
+        wp = ops.pack_conv(w, cdt, cout_pad=Np).reshape(Np, K)
+        if Kp != K:
+            wp = F.pad(wp, (0, Kp - K))
+        wp = wp.contiguous()
+        bp = None if b is None else (b if Np == Cout else F.pad(b, (0, Np - Cout))).contiguous()
+        y, _ = ops.linear_fwd(cols, wp, bp, cdt, out_dtype=torch.float32)
+        ctx.save_for_backward(cols, wp)
+        ctx.meta = (B, H, W, C, Cout, k, s, p, Ho, Wo, K, Kp, Np, cdt, b is not None)
+        y = y.view(B, Ho, Wo, Np)
+        return y if Np == Cout else y[..., :Cout].contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        cols, wp = ctx.saved_tensors
+        B, H, W, C, Cout, k, s, p, Ho, Wo, K, Kp, Np, cdt, has_b = ctx.meta
+        dy = dy.contiguous()
+        if Np != Cout:
+            dy = F.pad(dy, (0, Np - Cout))
+        d2 = ops.cast(dy.reshape(B * Ho * Wo, Np).contiguous(), tdtype(cdt))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dcols = ops.linear_dgrad(d2, wp, cdt, torch.float32)
+            dx = torch.empty((B, H, W, C), dtype=torch.float32, device=dy.device)
+            lib.ivit_col2im(ptr(dcols), Kp, B, H, W, C, k, s, p, Ho, Wo, ptr(dx), stream())
+        dw2, db = ops.linear_wgrad(d2, cols, cdt, want_bias=has_b)
+        dw = ops.unpack_conv_grad(dw2[:Cout, :K].contiguous(), Cout, C, k)
+        return dx, dw, (db[:Cout] if has_b else None), None, None, None
+
+
+def _r8(n):
+    return (n + 7) // 8 * 8
+
+
+class _ActFn(torch.autograd.Function):
+    """Standalone nn.GELU (exact erf) / nn.ReLU on the device (ivit_act_fwd / _bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, act):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        lib.ivit_act_fwd(act, ptr(xc), dt(xc), ptr(y), dt(y), xc.numel(), stream())
+        ctx.save_for_backward(xc)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        lib.ivit_act_bwd(ctx.act, ptr(dy), dt(dy), ptr(x), dt(x), ptr(dx), dt(dx), x.numel(), stream())
+        return dx, None
+
+
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, g, b, rm, rv, nbt, training, momentum, eps, relu, resid):
@@ -132,8 +202,10 @@ class LayerNorm(nn.Module):
 
 
 class Conv2d(nn.Module):
-    """Conv2d parameter container (k x k, stride s, padding p). Standalone forward supports
-    the stride-1 'same' convolutions of the fusion block and heads."""
+    """Conv2d parameter container (k x k, stride s, padding p). Standalone forward (NCHW, as
+    nn.Conv2d): stride-1 'same' convolutions with channel counts % 8 on the implicit-GEMM conv
+    kernels, everything else (strided, odd channel counts, e.g. the 35 / 40-channel heads) as
+    im2col + GEMM."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, bias=True):
         super().__init__()
@@ -147,10 +219,12 @@ class Conv2d(nn.Module):
             nn.init.uniform_(self.bias, -bound, bound)
 
     def forward(self, x):
-        k = self.kernel_size[0]
-        if self.stride[0] != 1 or self.padding[0] != k // 2:
-            raise NotImplementedError("ivit Conv2d standalone forward: stride 1, same padding only")
-        return _Conv2dFn.apply(x, self.weight, self.bias, _cdt(getattr(self, "compute_dtype", torch.float32)))
+        k, s_, p = self.kernel_size[0], self.stride[0], self.padding[0]
+        cdt = _cdt(getattr(self, "compute_dtype", torch.float32))
+        if s_ == 1 and p == k // 2 and k in (1, 3, 5) and self.in_channels % 8 == 0 and self.out_channels % 8 == 0:
+            return _Conv2dFn.apply(x, self.weight, self.bias, cdt)
+        y = _ConvColsFn.apply(x.permute(0, 2, 3, 1).float().contiguous(), self.weight, self.bias, s_, p, cdt)
+        return y.permute(0, 3, 1, 2).contiguous()
 
 
 class BatchNorm2d(nn.Module):
@@ -169,10 +243,11 @@ class BatchNorm2d(nn.Module):
 
 
 class GELU(nn.Module):
-    """Marker module (exact-erf GELU). In the fused path it is the adapter GEMM epilogue."""
+    """nn.GELU (exact erf). In the fused path it is the adapter GEMM epilogue; standalone it runs
+    ivit_act_fwd."""
 
     def forward(self, x):
-        return F.gelu(x)
+        return _ActFn.apply(x, ACT_GELU)
 
 
 class ReLU(nn.Module):
@@ -180,4 +255,4 @@ class ReLU(nn.Module):
         super().__init__()
 
     def forward(self, x):
-        return F.relu(x)
+        return _ActFn.apply(x, ACT_RELU)

@@ -18,56 +18,7 @@ import ops
 from _lib import BF16, F32, dt, lib, ptr, stream, tdtype
 from constants import LIDAR_TOTAL_CHANNELS, MAP_CHANNELS, NUM_INTENTION_CLASSES
 from heads import DetectionHead, IntentionHead
-from layers import BatchNorm2d, Conv2d, ReLU
-
-
-def _r8(n):
-    return (n + 7) // 8 * 8
-
-
-class _ConvColsFn(torch.autograd.Function):
-    """NHWC conv, any k / stride / zero pad (nn.Conv2d geometry): im2col + GEMM. The GEMM's K
-    (k*k*Cin) and N (Cout) are padded to multiples of 8 with zero columns / rows."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, s, p, cdt):
-        B, H, W, C = x.shape
-        Cout, Cin, k, _ = w.shape
-        if Cin != C:
-            raise ValueError(f"conv expects {Cin} input channels, got {C}")
-        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-        K = k * k * C
-        Kp, Np = _r8(K), _r8(Cout)
-        x = x.contiguous()
-        cols = torch.empty((B * Ho * Wo, Kp), dtype=tdtype(cdt), device=x.device)
-        lib.ivit_im2col(dt(x), ptr(x), B, H, W, C, k, s, p, Ho, Wo, ptr(cols), Kp, cdt, stream())
-        wp = ops.pack_conv(w, cdt, cout_pad=Np).reshape(Np, K)
-        if Kp != K:
-            wp = F.pad(wp, (0, Kp - K))
-        wp = wp.contiguous()
-        bp = None if b is None else (b if Np == Cout else F.pad(b, (0, Np - Cout))).contiguous()
-        y, _ = ops.linear_fwd(cols, wp, bp, cdt, out_dtype=torch.float32)
-        ctx.save_for_backward(cols, wp)
-        ctx.meta = (B, H, W, C, Cout, k, s, p, Ho, Wo, K, Kp, Np, cdt, b is not None)
-        y = y.view(B, Ho, Wo, Np)
-        return y if Np == Cout else y[..., :Cout].contiguous()
-
-    @staticmethod
-    def backward(ctx, dy):
-        cols, wp = ctx.saved_tensors
-        B, H, W, C, Cout, k, s, p, Ho, Wo, K, Kp, Np, cdt, has_b = ctx.meta
-        dy = dy.contiguous()
-        if Np != Cout:
-            dy = F.pad(dy, (0, Np - Cout))
-        d2 = ops.cast(dy.reshape(B * Ho * Wo, Np).contiguous(), tdtype(cdt))
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dcols = ops.linear_dgrad(d2, wp, cdt, torch.float32)
-            dx = torch.empty((B, H, W, C), dtype=torch.float32, device=dy.device)
-            lib.ivit_col2im(ptr(dcols), Kp, B, H, W, C, k, s, p, Ho, Wo, ptr(dx), stream())
-        dw2, db = ops.linear_wgrad(d2, cols, cdt, want_bias=has_b)
-        dw = ops.unpack_conv_grad(dw2[:Cout, :K].contiguous(), Cout, C, k)
-        return dx, dw, (db[:Cout] if has_b else None), None, None, None
+from layers import BatchNorm2d, Conv2d, ReLU, _ConvColsFn, _r8
 
 
 class _BNFn(torch.autograd.Function):

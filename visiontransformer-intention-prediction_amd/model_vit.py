@@ -19,7 +19,7 @@ import vit as timm_like
 from _lib import BF16, F32
 from constants import GRID_HEIGHT_PX, GRID_WIDTH_PX, LIDAR_TOTAL_CHANNELS, MAP_CHANNELS, NUM_INTENTION_CLASSES
 from heads import DetectionHead, IntentionHead
-from layers import GELU, BatchNorm2d, Conv2d, LayerNorm, Linear, ReLU
+from layers import GELU, BatchNorm2d, Conv2d, LayerNorm, Linear, ReLU, _LayerNormFn
 
 
 def conv3x3_for_basic(in_planes, out_planes, stride=1, kernel_size=3):
@@ -37,8 +37,6 @@ class BasicBlock(nn.Module):
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, kernel_size=3):
         super().__init__()
-        if stride != 1:
-            raise NotImplementedError("ivit fusion BasicBlock: stride 1 only (the reference default)")
         self.conv1 = conv3x3_for_basic(inplanes, planes, stride, kernel_size=kernel_size)
         self.bn1 = BatchNorm2d(planes)
         self.relu = ReLU(inplace=True)
@@ -79,8 +77,11 @@ class TwoStreamViTBackbone(nn.Module):
         self.map_num_prefix_tokens = self.vit_map.num_prefix_tokens
         self.map_grid_size = tuple(self.vit_map.patch_embed.grid_size)
         if self.lidar_grid_size != self.map_grid_size:
-            raise NotImplementedError("ivit: LiDAR and map patch grids must match (the reference's bilinear "
-                                      "re-grid path, model_vit.py:139, is not part of the hot path)")
+            # model_vit.py:139 re-grids the map features bilinearly when the grids differ; with the
+            # patch-8 ViTs this build provides (vit.VIT_ARCH) and one img_size they never do
+            raise NotImplementedError("ivit: LiDAR and map patch grids must match (both streams use patch-8 "
+                                      "ViTs on the same img_size; the bilinear re-grid of model_vit.py:139 "
+                                      "is unreachable)")
         self.feature_map_grid_h, self.feature_map_grid_w = self.lidar_grid_size
         self.adapter_lidar = nn.Sequential(LayerNorm(self.lidar_embed_dim),
                                            Linear(self.lidar_embed_dim, lidar_adapter_out_channels), GELU())
@@ -150,9 +151,24 @@ class TwoStreamViTBackbone(nn.Module):
         tm.record_stream(main)
         return tl, tm
 
+    def features_generic(self, tl, tm, B):
+        """model_vit.py:116-142 through the modules' own forwards (final norm, adapter LN ->
+        Linear -> GELU, token -> map, fusion BasicBlocks with their strides): the path for
+        fusion_block_stride != 1, whose strided block-0 convs run as im2col + GEMM."""
+        Hf, Wf = self.feature_map_grid_h, self.feature_map_grid_w
+        maps = []
+        for vitm, adapter, t in ((self.vit_lidar, self.adapter_lidar, tl), (self.vit_map, self.adapter_map, tm)):
+            D = vitm.embed_dim
+            x = _LayerNormFn.apply(t, vitm.norm.weight, vitm.norm.bias, 1e-6).reshape(B, -1, D)
+            y = adapter(x[:, vitm.num_prefix_tokens:])
+            maps.append(y.permute(0, 2, 1).reshape(B, -1, Hf, Wf))
+        return self.fusion_block(torch.cat(maps, 1))
+
     def forward(self, lidar_bev, map_bev):
-        """model_vit.py:134-142 → fused feature map (B, C, Hf, Wf) f32."""
+        """model_vit.py:134-142 → fused feature map (B, C, Hf', Wf') f32."""
         tl, tm = self.stream_tokens(lidar_bev, map_bev)
+        if self.fusion_block_stride != 1:
+            return self.features_generic(tl, tm, lidar_bev.shape[0])
         names = self.neck_names()
         tens = _lookup(self, names)
         B = lidar_bev.shape[0]
@@ -230,6 +246,11 @@ class IntentNetViT(nn.Module):
         """model_vit.py:179-185 → cls (B, A*Hf*Wf, 1), box (.., 6), intent (.., K), all f32."""
         B = lidar_bev.shape[0]
         tl, tm = self.backbone.stream_tokens(lidar_bev, map_bev)
+        if self.backbone.fusion_block_stride != 1:  # strided fusion: module forwards, heads at H/s x W/s
+            f = self.backbone.features_generic(tl, tm, B)
+            c, b = self.det_head(f)
+            it = self.intention_head(f)
+            return c.reshape(B, -1, 1), b.reshape(B, -1, 6), it.reshape(B, -1, NUM_INTENTION_CLASSES)
         meta, names = self._neck_meta(B)
         bb = dict(self.backbone.named_parameters())
         bb.update(dict(self.backbone.named_buffers()))
