@@ -68,6 +68,16 @@ int ivit_patch_embed_fwd_cols(const void* cols, long B, long C, long H, long W, 
 int ivit_patch_embed_wgrad_cols(const void* dtok, const void* cols, long B, long C, long H, long W, long D,
                                 float* dW, float* dbias, float* dpos, float* dcls, int accumulate, void* work,
                                 long work_bytes, void* stream);
+/* Fused bf16 forward of the same PatchEmbed: the f32 raster streams through LDS once (converted to
+ * bf16 in the operand read), every workgroup computing all D columns of 144 patches; no patch
+ * matrix. The weight is first packed (once per weight version) into MFMA fragment order:
+ * wpack = ivit_patch_weight_pack_bytes(D, C) bytes, from W [D][C][8][8] f32. D = 384 or 192;
+ * img and wpack 16-byte aligned. Same output as ivit_patch_embed_fwd with dtype IVIT_BF16. */
+long ivit_patch_weight_pack_bytes(long D, long C);
+int ivit_patch_weight_pack(const float* w, long D, long C, void* wpack, void* stream);
+int ivit_patch_embed_fwd_packed(const float* img, long B, long C, long H, long W, const void* wpack,
+                                const float* bias, const float* pos, const float* cls, long D, float* out,
+                                void* stream);
 
 /* ---- k x k stride-1 "same" convolution on NHWC maps (BasicBlock conv3x3/conv1x1,
  *      model_vit.py:12-17; DetectionHead/IntentionHead conv, heads.py:16,37; k = 5: model_cnn.py:7-9).

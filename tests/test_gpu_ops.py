@@ -240,11 +240,14 @@ def test_conv_nhwc(k, Cin, cd):
 
 
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
-def test_patch_embed(cd):
+@pytest.mark.parametrize("D", [64, 384])
+def test_patch_embed(cd, D):
+    """D = 64: bf16 through the patch matrix (im2col + GEMM); D = 384: the fused forward
+    (ivit_patch_embed_fwd_packed) and the raster-reading weight gradient."""
     import ops
     from _lib import BF16, F32
     cdt = BF16 if cd == torch.bfloat16 else F32
-    B, C, H, W, D = 2, 20, 32, 48, 64
+    B, C, H, W = 2, 20, 32, 48
     img = torch.rand(B, C, H, W)
     w = torch.randn(D, C, 8, 8) / math.sqrt(C * 64)
     b, pos, cls = 0.1 * torch.randn(D), 0.02 * torch.randn(1, 25, D), 0.02 * torch.randn(1, 1, D)
@@ -260,6 +263,76 @@ def test_patch_embed(cd):
     ref.backward(g.double())
     for p, r in zip(params, (wr, br, pr, cr)):
         assert _rel(p.grad, r.grad) < tol
+
+
+@pytest.mark.parametrize("B,C,H,W,D", [(2, 9, 32, 48, 384), (3, 5, 64, 40, 192), (1, 1, 16, 16, 384),
+                                       (2, 290, 96, 720, 384), (1, 7, 24, 1448, 192)])
+def test_patch_embed_fused_exact(B, C, H, W, D):
+    """Fused bf16 forward vs the same products in f64 (bf16-rounded raster and weight): only the
+    f32 accumulation order differs. Tiles spanning several images (Np < 144), partial last
+    tiles, a single channel, the LiDAR channel count and both widths."""
+    from _lib import lib, ptr, stream
+    g = torch.Generator().manual_seed(B * 1000 + C)
+    img = torch.rand(B, C, H, W, generator=g)
+    w = torch.randn(D, C, 8, 8, generator=g) / math.sqrt(C * 64)
+    b, pos, cls = 0.1 * torch.randn(D, generator=g), torch.randn(1, (H // 8) * (W // 8) + 1, D, generator=g), \
+        torch.randn(1, 1, D, generator=g)
+    Np = (H // 8) * (W // 8)
+    wd, imgd = w.to(DEV), img.to(DEV)
+    wp = torch.empty(lib.ivit_patch_weight_pack_bytes(D, C) // 2, dtype=torch.bfloat16, device=DEV)
+    assert lib.ivit_patch_weight_pack(ptr(wd), D, C, ptr(wp), stream()) == 0
+    out = torch.full((B * (Np + 1), D), float("nan"), device=DEV)
+    bd, pd, cd_ = b.to(DEV), pos.to(DEV), cls.to(DEV)
+    assert lib.ivit_patch_embed_fwd_packed(ptr(imgd), B, C, H, W, ptr(wp), ptr(bd), ptr(pd), ptr(cd_), D, ptr(out),
+                                           stream()) == 0
+    t = F.conv2d(img.to(torch.bfloat16).double(), w.to(torch.bfloat16).double(), b.double(), stride=8)
+    ref = torch.cat([cls.double().expand(B, -1, -1), t.flatten(2).transpose(1, 2)], 1) + pos.double()
+    o = out.reshape(B, Np + 1, D).double().cpu()
+    assert torch.isfinite(o).all()
+    err = (o - ref).abs().max().item()
+    assert err < 2e-5 * max(1.0, math.sqrt(C * 64) / 8), err
+    # the patch-matrix path agrees to the same accuracy
+    wc = w.to(torch.bfloat16).reshape(D, C * 64).to(DEV)
+    cols = torch.empty((B * Np, C * 64), dtype=torch.bfloat16, device=DEV)
+    out2 = torch.empty_like(out)
+    assert lib.ivit_patch_im2col(ptr(imgd), B, C, H, W, ptr(cols), stream()) == 0
+    assert lib.ivit_patch_embed_fwd_cols(ptr(cols), B, C, H, W, ptr(wc), ptr(bd), ptr(pd), ptr(cd_), D, ptr(out2),
+                                         stream()) == 0
+    assert (out2.double().cpu().reshape(B, Np + 1, D) - o).abs().max().item() < 2 * err + 1e-5
+
+
+@pytest.mark.parametrize("B,C,H,W", [(2, 9, 32, 48), (3, 290, 24, 40), (2, 4, 400, 720), (1, 3, 16, 16)])
+def test_patch_wgrad_raster_exact(B, C, H, W):
+    """bf16 weight gradient straight from the raster (ivit_patch_embed_wgrad, D = 384: the
+    persistent channel-pair kernel + slab reduction) vs the same products in f64: odd channel
+    counts, 32-patch chunks crossing images, workgroups spanning two channel pairs, tiny grids
+    with idle workgroups; dbias / dpos / dcls as before."""
+    from _lib import BF16, lib, ptr, stream
+    D = 384
+    g = torch.Generator().manual_seed(7 * C + B)
+    img = torch.rand(B, C, H, W, generator=g)
+    Np = (H // 8) * (W // 8)
+    dtok = torch.randn(B * (Np + 1), D, generator=g).to(torch.bfloat16)
+    dw = torch.full((D, C, 8, 8), float("nan"), device=DEV)
+    db, dpos, dcls = (torch.empty(D, device=DEV), torch.empty(Np + 1, D, device=DEV), torch.empty(D, device=DEV))
+    nws = lib.ivit_patch_embed_wgrad_workspace(B, C, H, W, D)
+    ws = torch.empty(nws, dtype=torch.uint8, device=DEV)
+    imgd, dtd = img.to(DEV), dtok.to(DEV)
+    assert lib.ivit_patch_embed_wgrad(BF16, ptr(dtd), ptr(imgd), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos),
+                                      ptr(dcls), 0, ptr(ws), nws, stream()) == 0
+    X = img.to(torch.bfloat16).double().reshape(B, C, H // 8, 8, W // 8, 8).permute(0, 2, 4, 1, 3, 5)
+    X = X.reshape(B * Np, C * 64)
+    dt = dtok.double().reshape(B, Np + 1, D)
+    ref = dt[:, 1:].reshape(B * Np, D).t() @ X
+    got = dw.double().cpu().reshape(D, C * 64)
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs().max().item()
+    assert err < 1e-5 * max(1.0, (B * Np) ** 0.5), err
+    assert _rel(db, dt[:, 1:].sum((0, 1))) < 1e-5 and _rel(dpos, dt.sum(0)) < 1e-5
+    # accumulate = 1 adds onto the previous result
+    assert lib.ivit_patch_embed_wgrad(BF16, ptr(dtd), ptr(imgd), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos),
+                                      ptr(dcls), 1, ptr(ws), nws, stream()) == 0
+    assert (dw.double().cpu().reshape(D, C * 64) - 2 * ref).abs().max().item() < 2 * err + 1e-5
 
 
 def test_patch_im2col_bitexact():

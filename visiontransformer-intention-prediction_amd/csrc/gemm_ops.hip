@@ -3,6 +3,7 @@
 #include <stdio.h>
 
 #include "gemm_engine.h"
+#include "patch_embed.h"
 
 using namespace ivit;
 
@@ -300,7 +301,10 @@ extern "C" long ivit_patch_embed_wgrad_workspace(long B, long C, long H, long W,
   long s = wgrad_splits(D, C * 64, B * Np, false);
   const long s2 = wgrad_splits(D, C * 64, B * Np, true);
   if (s2 > s) s = s2;
-  return s * D * C * 64 * 4 + ivit_colsum_workspace(B * Np, D);
+  long main = s * D * C * 64 * 4;
+  if (patch_wgrad_raster_ok(B, C, H, W, D) && patch_wgrad_raster_workspace(D) > main)
+    main = patch_wgrad_raster_workspace(D);
+  return main + ivit_colsum_workspace(B * Np, D);
 }
 
 template <typename S>
@@ -322,13 +326,22 @@ extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* 
   hipStream_t st = ivit_stream(stream);
   const bool bf = dtype == IVIT_BF16;
   const long Np = (H / 8) * (W / 8), Ntok = Np + 1;
-  const int splits = (int)wgrad_splits(D, C * 64, B * Np, bf);
-  float* slab = (float*)work;
-  int rc = bf ? patch_wgrad_t<bf16>(dtok, img, B, C, H, W, D, slab, splits, st)
-              : patch_wgrad_t<float>(dtok, img, B, C, H, W, D, slab, splits, st);
-  if (rc) return rc;
   const long n = D * C * 64;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dW, accumulate);
+  const int splits = (int)wgrad_splits(D, C * 64, B * Np, bf);
+  long cw_off = (long)splits * n * 4;  // colsum workspace after the slab
+  if (bf && patch_wgrad_raster_ok(B, C, H, W, D)) {  // raster read once (patch_embed.hip)
+    cw_off = patch_wgrad_raster_workspace(D);
+    int rc = patch_wgrad_raster((const bf16*)dtok, img, B, C, H, W, D, dW, accumulate, work, st);
+    if (rc) return rc;
+    IVIT_LAUNCH_CHECK();
+  } else {
+    float* slab = (float*)work;
+    int rc = bf ? patch_wgrad_t<bf16>(dtok, img, B, C, H, W, D, slab, splits, st)
+                : patch_wgrad_t<float>(dtok, img, B, C, H, W, D, slab, splits, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dW,
+                       accumulate);
+  }
   if (bf)
     hipLaunchKernelGGL(pos_grad_kernel<bf16>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const bf16*)dtok, B,
                        Ntok, D, dpos, dcls, accumulate);
@@ -336,7 +349,7 @@ extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* 
     hipLaunchKernelGGL(pos_grad_kernel<float>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const float*)dtok,
                        B, Ntok, D, dpos, dcls, accumulate);
   IVIT_LAUNCH_CHECK();
-  char* cw = (char*)work + (long)splits * n * 4;
+  char* cw = (char*)work + cw_off;
   return ivit_colsum(dtok, dtype, D, Np, Ntok, 1, B * Np, D, dbias, accumulate, cw, ivit_colsum_workspace(B * Np, D),
                      stream);
 }

@@ -168,11 +168,15 @@ IVIT_DEV float wave_max(float v) {
 }
 
 
+// Two f32 -> packed bf16 pair (round to nearest even): one v_cvt_pk_bf16_f32. (Element-wise
+// casts assembled into a vector compiled to the same conversions plus and/shift/or re-packing.)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+IVIT_DEV unsigned pk_bf16(float a, float b) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+}
 IVIT_DEV uint4 f32x8_to_bf16x8(float4 a, float4 b) {
-  Pack8 p;
-  p.h[0] = f2bf(a.x); p.h[1] = f2bf(a.y); p.h[2] = f2bf(a.z); p.h[3] = f2bf(a.w);
-  p.h[4] = f2bf(b.x); p.h[5] = f2bf(b.y); p.h[6] = f2bf(b.z); p.h[7] = f2bf(b.w);
-  return p.u;
+  return make_uint4(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w), pk_bf16(b.x, b.y), pk_bf16(b.z, b.w));
 }
 
 // Column reduction of per-block partial sums: out[c] (+)= sum_b part[b * pstride + c].

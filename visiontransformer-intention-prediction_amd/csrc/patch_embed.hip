@@ -1,0 +1,627 @@
+// Fused bf16 patch embedding (timm PatchEmbed, Conv2d k = s = 8) over an f32 NCHW BEV raster:
+//
+//   x[b, 1 + p, n] = sum_{c, ky, kx} img[b, c, 8 gy + ky, 8 gx + kx] * W[n, c, ky, kx] + bias[n] + pos[1 + p, n]
+//
+// one pass, no im2col buffer (north_star: "a fused Conv2d patch-embed with coalesced HBM reads of
+// the multi-channel BEV grid into LDS tiles"). The raster is the only large operand (LiDAR:
+// 8 x 290 x 400 x 720 f32 = 2.67 GB, read once); the weight (D x 64C bf16, 14 MB) is re-read by
+// every workgroup from L2.
+//
+// Workgroup = 144 consecutive patches (9 MFMA row blocks of 16; 36 000 LiDAR patches = 250
+// workgroups, one per CU) x ALL D output columns, so each raster byte is fetched exactly once.
+// K loop = one input channel (8 x 8 taps = 64 k) per stage:
+//   * A (raster): LDS-DMA of raw f32 into a 3-stage ring, 36 KiB per stage, two stages in flight
+//     (72 KiB of HBM reads per CU, the depth the guide measures for ~6 TB/s streaming). A stage is
+//     [ky][patch][8 kx] — 32-byte records, consecutive lanes fetch consecutive 16-B halves so each
+//     DMA wave-instruction reads one contiguous 1 KiB run of raster rows; the two halves of a
+//     record swap places on every other 8-record group, which makes the MFMA operand reads
+//     (16 patches x 16 B per lane group) bank-conflict-free. f32 -> bf16 happens in the operand
+//     read (4 v_cvt_pk_bf16_f32 per fragment).
+//   * B (weight): pre-packed in MFMA fragment order (ivit_patch_weight_pack), loaded straight into
+//     VGPRs one stage ahead — 1 KiB contiguous per wave-instruction.
+//   * 4 waves, wave w owns output columns [w D/4, (w+1) D/4): 9 x (D/64) accumulators of
+//     v_mfma_f32_16x16x32_bf16 (216 AGPRs at D = 384).
+// Every memory operation of the loop is inline asm retired by counted vmcnt waits: the compiler's
+// waitcnt pass cannot see the DMAs, and a compiler-placed wait on a register load would drain the
+// in-flight raster stages (the counter retires in issue order). Issue order per stage kt-1 ->
+// kt: B(kt), then A(kt+1), so waiting for B(kt) leaves A(kt+1) in flight (vmcnt(9)).
+#include "patch_embed.h"
+
+namespace ivit {
+namespace {
+
+constexpr int PE_MT = 144;                    // patches per workgroup
+constexpr int PE_MB = PE_MT / 16;             // 16-row MFMA blocks
+constexpr int PE_STAGE = PE_MT * 8 * 32;      // bytes per LDS stage: [ky 8][patch][32 B]
+constexpr int PE_NS = 3;                      // f32 LDS stages (raster DMA ring)
+constexpr int PE_BSTAGE = PE_MT * 8 * 16;     // bf16 operand stage: [ky 8][patch][16 B]
+constexpr int PE_PIECES = PE_STAGE / 1024;    // 1-KiB DMA pieces per stage (36)
+constexpr int NBW = 3;                        // 16-column MFMA blocks per wave (48 columns)
+
+// s_waitcnt vmcnt(n) for the counts that occur: n = {0, 1, 2} x piece count (4, 5 or 9) + {0, 6}
+// (the field is an immediate; n is wave-uniform)
+#define PE_VM(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+IVIT_DEV void wait_vm(int n) {
+  switch (n) {
+    PE_VM(4) PE_VM(5) PE_VM(6) PE_VM(8) PE_VM(9) PE_VM(10) PE_VM(11) PE_VM(14) PE_VM(15) PE_VM(16) PE_VM(18)
+    PE_VM(24)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+#undef PE_VM
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Wave-uniform 64-bit address -> SGPR pair (the saddr operand of the loads below).
+IVIT_DEV const char* uniform_ptr(const void* p) {
+  const unsigned long v = (unsigned long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (const char*)(((unsigned long)hi << 32) | lo);
+}
+
+// 16 B per lane from sbase + voff + OFF into VGPRs (saddr form: one VGPR of per-lane offset).
+template <int OFF>
+IVIT_DEV void gload_b128(u32x4& r, unsigned voff, const char* sbase) {
+  static_assert(OFF >= 0 && OFF < 4096, "global offset field");
+  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(r) : "v"(voff), "s"(sbase), "i"(OFF) : "memory");
+}
+
+// LDS-DMA, saddr form: lane's 16 B from sbase + voff land at lds + 16 * lane (lds wave-uniform -> M0).
+// NT: the raster is read once, non-temporal (measured 0.54 vs 0.61 ms per LiDAR forward).
+template <bool NT = true>
+IVIT_DEV void glds_s(unsigned voff, const char* sbase, void* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  if constexpr (NT)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2 nt" ::"v"(voff), "s"(a), "s"(sbase)
+                 : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2" ::"v"(voff), "s"(a), "s"(sbase)
+                 : "memory");
+}
+
+IVIT_DEV bf16x8 cvt8(const float4 a, const float4 b) {
+  Pack8 p;
+  p.u = f32x8_to_bf16x8(a, b);
+  return p.v;
+}
+
+// The 2*NBW fragment registers of one stage become visible to the compiler only here, after the
+// counted wait that retired their loads.
+IVIT_DEV void tie(u32x4 (&r)[2 * NBW]) {
+  asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]));
+}
+
+// NW waves = D / 48 (8 at D = 384: two per SIMD; 4 at D = 192).
+//
+// Pipeline, iteration kt (one input channel): the raster of channels kt+1 .. kt+3 and the weight
+// fragments of kt+1 .. kt+2 are in flight or landed. Each wave converts ITS OWN landed f32
+// pieces of channel kt+1 to bf16 (its own DMA data needs no barrier), which frees its f32 region
+// for channel kt+4 at once — three raster stages (108 KiB per CU) stay in flight while the
+// MFMAs of channel kt read the bf16 image the whole workgroup converted one iteration earlier.
+// vmcnt retires in issue order, so weights are issued two channels ahead, between the raster
+// stages they must not drain: ... A(kt+1) B(kt) A(kt+2) B(kt+1) A(kt+3) | B(kt+2) A(kt+4).
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void patch_fwd_kernel(const float* __restrict__ img, int C, int H, int W,
+                                                           int Wp, int Np, int M, const u32x4* __restrict__ wpack,
+                                                           const float* __restrict__ bias,
+                                                           const float* __restrict__ pos, int D,
+                                                           float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char smem[PE_NS * PE_STAGE + 2 * PE_BSTAGE];
+  char* const bimg = smem + PE_NS * PE_STAGE;  // two bf16 stages [ky][patch][8 kx]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * PE_MT;
+  const long HW = (long)H * W;
+
+  // pieces of a stage per wave: 36 / NW, the first 36 % NW waves one more
+  constexpr int PW = (PE_PIECES + NW - 1) / NW, PREM = PE_PIECES % NW;
+  const int npc = (PREM == 0 || wv < PREM) ? PW : PW - 1;
+  const int pc0 = (PREM == 0 || wv < PREM) ? wv * PW : PREM * PW + (wv - PREM) * (PW - 1);
+  // per-lane DMA sources: piece q covers records 32q .. 32q+31 (record = (ky, patch)); byte
+  // offsets from the first image of the tile at channel c (the host checks they fit 32 bits)
+  const int b0 = m0 / Np;
+  unsigned voff[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int rec = min(pc0 + i, PE_PIECES - 1) * 32 + (lane >> 1);
+    const int ky = rec / PE_MT, p = rec - ky * PE_MT;
+    const int half = (lane & 1) ^ ((rec >> 3) & 1);  // stored position (lane & 1) holds this half
+    const int m = min(m0 + p, M - 1);                // rows past M are computed, never stored
+    const int b = m / Np, pi = m - b * Np, gy = pi / Wp, gx = pi - gy * Wp;
+    voff[i] = (unsigned)((((long)(b - b0) * C * H + gy * 8 + ky) * W + gx * 8 + half * 4) * 4);
+  }
+  const float* img0 = img + (long)b0 * C * HW;
+  char* const freg = smem + pc0 * 1024;  // this wave's pieces inside each f32 stage
+  auto issue_a = [&](int c) {
+    char* st = freg + (c % PE_NS) * PE_STAGE;
+    const char* sb = uniform_ptr(img0 + c * HW);
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      if (i < npc) glds_s(voff[i], sb, st + i * 1024);
+  };
+  // own pieces of channel c (landed) -> bf16 stage (c & 1): lane l of piece q holds half h of
+  // record 32q + (l >> 1); it writes those 4 kx as 8 bytes of the 16-B bf16 record
+  auto convert = [&](int c) {
+    const char* fs = freg + (c % PE_NS) * PE_STAGE + lane * 16;
+    char* bs = bimg + (c & 1) * PE_BSTAGE;
+    float4 v[PW];
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      if (i < npc) v[i] = *(const float4*)(fs + i * 1024);
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      if (i < npc) {
+        const int rec = (pc0 + i) * 32 + (lane >> 1);
+        const int half = (lane & 1) ^ ((rec >> 3) & 1);
+        *(uint2*)(bs + rec * 16 + half * 8) = make_uint2(pk_bf16(v[i].x, v[i].y), pk_bf16(v[i].z, v[i].w));
+      }
+  };
+  // weight fragments: wpack[s][nb][lane] (16 B), s = 32-k step, nb = 16-column block; the wave's
+  // NBW blocks of a step are NBW contiguous KiB
+  const int NB16 = D / 16;
+  const unsigned vb = lane * 16;
+  auto issue_b = [&](int c, u32x4 (&r)[2 * NBW]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const char* sb = uniform_ptr(wpack + ((long)(2 * c + t) * NB16 + wv * NBW) * 64);
+      gload_b128<0>(r[t * NBW + 0], vb, sb);
+      gload_b128<1024>(r[t * NBW + 1], vb, sb);
+      gload_b128<2048>(r[t * NBW + 2], vb, sb);
+    }
+  };
+
+  f32x4 acc[PE_MB][NBW];
+#pragma unroll
+  for (int i = 0; i < PE_MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 breg[3][2 * NBW];
+  // operand read: lane group g = lane >> 4 takes ky = 4t + g, patches 16 mb + (lane & 15)
+  const int rl = ((lane >> 4) * PE_MT + (lane & 15)) * 16;
+
+  auto stage = [&](int kt, u32x4 (&cur)[2 * NBW], u32x4 (&nb2)[2 * NBW]) {
+    // outstanding after A(kt+1), B(kt): A(kt+2), B(kt+1), A(kt+3) (those that exist)
+    const bool a2 = kt + 2 < C, a3 = kt + 3 < C, b1 = kt + 1 < C;
+    wait_vm((a2 ? npc : 0) + (b1 ? 2 * NBW : 0) + (a3 ? npc : 0));
+    tie(cur);
+    __builtin_amdgcn_s_barrier();  // bf16 stage kt&1 complete; bf16 stage (kt+1)&1 free
+    if (kt + 2 < C) issue_b(kt + 2, nb2);
+    // operand fragments f = 0..17 (t = f / 9: 32-k step, mb = f % 9: row block) are read three
+    // ahead of their MFMAs; sched barriers pin that distance (the scheduler otherwise sinks each
+    // read next to its use and every pair of fragments waits out the LDS latency). The wave's
+    // own raster pieces of channel kt+1 are converted after the first fragments' MFMAs are
+    // queued, then its f32 region is refilled with channel kt+4.
+    const char* ia = bimg + (kt & 1) * PE_BSTAGE + rl;
+    auto rdf = [&](int f) { return *(const bf16x8*)(ia + (4 * (f / PE_MB) * PE_MT + 16 * (f % PE_MB)) * 16); };
+    bf16x8 fr[4];
+    fr[0] = rdf(0);
+    fr[1] = rdf(1);
+    fr[2] = rdf(2);
+#pragma unroll
+    for (int f = 0; f < 2 * PE_MB; ++f) {
+      const int t = f / PE_MB, mb = f % PE_MB;
+      if (f + 3 < 2 * PE_MB) fr[(f + 3) % 4] = rdf(f + 3);
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) {
+        union { u32x4 u; bf16x8 v; } bw;
+        bw.u = cur[t * NBW + j];
+        acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[f % 4], bw.v, acc[mb][j], 0, 0, 0);
+      }
+      if (f == 1 && kt + 1 < C) {
+        convert(kt + 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // f32 region read before it is refilled
+        if (kt + 4 < C) issue_a(kt + 4);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of bf16 stage kt are done
+  };
+
+  // prologue: A(0) landed and converted; then A(1) B(0) A(2) B(1) A(3) in flight (the invariant)
+  issue_a(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  convert(0);
+  if (C > 1) issue_a(1);
+  issue_b(0, breg[0]);
+  if (C > 2) issue_a(2);
+  if (C > 1) issue_b(1, breg[1]);
+  if (C > 3) issue_a(3);
+  for (int kt = 0; kt < C; kt += 3) {
+    stage(kt, breg[0], breg[2]);
+    if (kt + 1 < C) stage(kt + 1, breg[1], breg[0]);
+    if (kt + 2 < C) stage(kt + 2, breg[2], breg[1]);
+  }
+
+  // epilogue: lane holds rows 4(lane>>4) + i of each 16-row block, column 16 nb + (lane & 15)
+  float bv[NBW];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) bv[j] = bias[(wv * NBW + j) * 16 + (lane & 15)];
+#pragma unroll
+  for (int mb = 0; mb < PE_MB; ++mb) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + 16 * mb + 4 * (lane >> 4) + i;
+      if (m >= M) continue;
+      const int b = m / Np, p = m - b * Np;
+      const float* pr = pos + (long)(1 + p) * D;
+      float* orow = out + ((long)b * (Np + 1) + 1 + p) * D;
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) {
+        const int n = (wv * NBW + j) * 16 + (lane & 15);
+        orow[n] = acc[mb][j][i] + bv[j] + pr[n];
+      }
+    }
+  }
+}
+
+// W [D][K] f32 (K = 64 C) -> wpack[s][nb][lane][8] bf16: lane l of 16-column block nb at 32-k
+// step s holds W[16 nb + (l & 15)][32 s + 8 (l >> 4) + 0..7] (the 16x16x32 B operand).
+__global__ __launch_bounds__(256) void patch_pack_kernel(const float* __restrict__ w, long D, long K,
+                                                         uint4* __restrict__ wp) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long NB16 = D / 16, total = (K / 32) * NB16 * 64;
+  if (i >= total) return;
+  const int lane = (int)(i & 63);
+  const long snb = i >> 6, s = snb / NB16, nb = snb - s * NB16;
+  const float* q = w + (nb * 16 + (lane & 15)) * K + s * 32 + 8 * (lane >> 4);
+  wp[i] = f32x8_to_bf16x8(*(const float4*)q, *(const float4*)(q + 4));
+}
+
+__global__ void patch_cls_kernel(float* out, long B, long Ntok, long D, const float* cls, const float* pos) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * D) return;
+  const long b = i / D, d = i - b * D;
+  out[b * Ntok * D + d] = cls[d] + pos[d];
+}
+
+}  // namespace
+}  // namespace ivit
+
+using namespace ivit;
+
+extern "C" long ivit_patch_weight_pack_bytes(long D, long C) { return D * C * 64 * 2; }
+
+extern "C" int ivit_patch_weight_pack(const float* w, long D, long C, void* wpack, void* stream) {
+  IVIT_CHECK_ARG(D > 0 && D % 16 == 0 && C > 0, "ivit_patch_weight_pack: D must be a positive multiple of 16");
+  const long K = C * 64, n = (K / 32) * (D / 16) * 64;
+  hipLaunchKernelGGL(patch_pack_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), w, D, K,
+                     (uint4*)wpack);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_patch_embed_fwd_packed(const float* img, long B, long C, long H, long W, const void* wpack,
+                                           const float* bias, const float* pos, const float* cls, long D,
+                                           float* out, void* stream) {
+  IVIT_CHECK_ARG(H % 8 == 0 && W % 8 == 0 && H > 0 && W > 0 && B > 0 && C > 0,
+                 "ivit_patch_embed_fwd_packed: H, W must be positive multiples of the patch (8)");
+  IVIT_CHECK_ARG(D == 384 || D == 192, "ivit_patch_embed_fwd_packed: D must be 384 or 192 (got %ld)", D);
+  // a 144-patch tile spans at most 1 + ceil(143 / Np) images; per-lane DMA offsets are 32-bit
+  const long span = 1 + (PE_MT - 1 + (H / 8) * (W / 8) - 1) / ((H / 8) * (W / 8));
+  IVIT_CHECK_ARG((H / 8) * (W / 8) * B < (1L << 31) && span * C * H * W * 4 < (1L << 32),
+                 "ivit_patch_embed_fwd_packed: raster too large");
+  IVIT_CHECK_ARG(((uintptr_t)img & 15) == 0 && ((uintptr_t)wpack & 15) == 0,
+                 "ivit_patch_embed_fwd_packed: raster and packed weight must be 16-byte aligned");
+  hipStream_t st = ivit_stream(stream);
+  const int Wp = (int)(W / 8), Np = (int)((H / 8) * Wp), M = (int)(B * Np);
+  const dim3 grid(ivit_cdiv(M, PE_MT));
+  if (D == 384)
+    hipLaunchKernelGGL(patch_fwd_kernel<8>, grid, dim3(512), 0, st, img, (int)C, (int)H, (int)W, Wp, Np, M,
+                       (const u32x4*)wpack, bias, pos, (int)D, out);
+  else
+    hipLaunchKernelGGL(patch_fwd_kernel<4>, grid, dim3(256), 0, st, img, (int)C, (int)H, (int)W, Wp, Np, M,
+                       (const u32x4*)wpack, bias, pos, (int)D, out);
+  IVIT_LAUNCH_CHECK();
+  const long Ntok = (long)Np + 1;
+  hipLaunchKernelGGL(patch_cls_kernel, dim3(ivit_cdiv(B * D, 256)), dim3(256), 0, st, out, B, Ntok, D, cls, pos);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+// ============================================================================= weight gradient
+// dW[n][k] = sum_m dtok[token(m)][n] * X[m][k],  X[m][c*64 + ky*8 + kx] = bf16(img[b][c][8gy+ky][8gx+kx])
+// straight from the f32 raster (no patch matrix). The raster must again be read once, so a
+// workgroup owns ALL D rows of its output tile; the tile spans one channel pair (128 k) and the
+// reduction runs over patches. Work = (channel pair g, 32-patch chunk j) units, g-major, split
+// evenly over 256 persistent workgroups (a range of <= J units meets at most two channel pairs;
+// patch_wgrad_raster_ok checks it); each
+// workgroup writes its per-pair partial tile to a slab and a reduction kernel sums the partials
+// of every pair in a fixed order (deterministic). Per unit: raster 2 ch x 8 ky x 32 patches
+// (16 KiB f32 by LDS-DMA, converted per wave like the forward), dtok 32 token rows x D (bf16 by
+// LDS-DMA); both operands are MN-contiguous images read with ds_read_b64_tr_b16;
+// v_mfma_f32_32x32x16_bf16, 8 waves, a wave = 3 n-blocks x NBK k-blocks of 32 x 32.
+namespace ivit {
+namespace {
+
+constexpr int WG_NWG = 256;                   // persistent workgroups
+constexpr int WG_MU = 32;                     // patches per unit
+constexpr int WG_RST = 2 * 8 * WG_MU * 32;    // raster f32 region per unit: 16 KiB (16 pieces)
+constexpr int WG_XST = WG_MU * 256;           // X bf16 image [32 m][128 k]: 8 KiB
+constexpr int WG_TIMG = WG_MU * 256;          // one 128-column dtok image [32 m][128 n]: 8 KiB
+
+IVIT_DEV int wg_mn_off(int r, int c) { return r * 256 + ((c ^ ((r & 3) << 2)) << 4); }
+
+IVIT_DEV s16x4 wg_tr(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+// 32x32x16 operand from an MN-contiguous [k rows][128 cols] image, rows kbase .. kbase+15:
+// lane l gets column colbase + (l & 31)'s k = kbase + 8 (l >> 5) + 0..7 (two transposing reads)
+IVIT_DEV bf16x8 wg_frag(const char* img, int kbase, int colbase, int lane) {
+  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = colbase + 16 * (G & 1) + 4 * p;
+  const int r0 = kbase + 8 * (G >> 1) + q;
+  const int c = col >> 3, e = (col & 7) * 2;
+  union { s16x4 s[2]; bf16x8 v; } u;
+  u.s[0] = wg_tr(img + wg_mn_off(r0, c) + e);
+  u.s[1] = wg_tr(img + wg_mn_off(r0 + 4, c) + e);
+  return u.v;
+}
+
+IVIT_DEV long wg_unit_start(int w, long U) { return (long)w * U / WG_NWG; }
+
+// LDS-DMA from a per-lane 64-bit address (lds wave-uniform -> M0).
+template <bool NT>
+IVIT_DEV void glds_v(const void* src, void* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  if constexpr (NT)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(src), "s"(a) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(a) : "memory");
+}
+
+#define WG_VM(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+IVIT_DEV void wg_wait_vm(int n) {
+  switch (n) {
+    WG_VM(2) WG_VM(3) WG_VM(4) WG_VM(5) WG_VM(6) WG_VM(7) WG_VM(8) WG_VM(10)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+#undef WG_VM
+
+// NT = D / 128 dtok images; NBK = k-blocks (of 32) per wave (D = 384: NT = 3, NBK = 2).
+template <int NT, int NBK>
+__global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restrict__ dtok,
+                                                            const float* __restrict__ img, int C, int H, int W,
+                                                            int Wp, int Np, int M, int J, float* __restrict__ slab) {
+  constexpr int D = NT * 128, NBN = 3;
+  constexpr int TPW = NT;                            // dtok pieces (4 rows x 256 B) per wave per unit
+  constexpr int RPW = 2;                             // raster pieces per wave per unit
+  constexpr int TST = NT * WG_TIMG;                  // dtok stage bytes
+  constexpr int NGRP = D / 32 / NBN;                 // wave groups along n (4 or 2)
+  static_assert(NGRP * (4 / NBK) == 8, "8 waves");
+  constexpr int RN = 4;                              // raster ring (three units in flight)
+  __shared__ __attribute__((aligned(16))) char smem[RN * WG_RST + 3 * TST + 2 * WG_XST];
+  char* const rreg = smem;
+  char* const treg = smem + RN * WG_RST;
+  char* const ximg = treg + 3 * TST;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ng = wv % NGRP, kg = wv / NGRP;
+  const long U = (long)((C + 1) / 2) * J;
+  const int w = blockIdx.x;
+  const long u0 = wg_unit_start(w, U), u1 = wg_unit_start(w + 1, U);
+  const int nu = (int)(u1 - u0);
+  if (nu <= 0) return;
+  const int g0 = (int)(u0 / J), j0 = (int)(u0 - (long)g0 * J);
+  const int Hp = H / 8, Bn = M / Np;
+
+  // Per-unit addressing is incremental (no integer division in the loop: a runtime-divisor
+  // division is a ~40-instruction VALU sequence, and the loop would be VALU-bound on it).
+  // A cursor = (g, j) of one unit, advanced by one unit per iteration; the lane positions of
+  // its 32-patch chunk advance by 32 patches with carries.
+  struct Cur { int g, j; };
+  auto cnext = [&](Cur& c) { if (++c.j == J) { c.j = 0; ++c.g; } };
+  // raster lane position: patch (lane >> 1) of the chunk as (b, gy, gx)
+  struct RPos { int b, gy, gx; };
+  auto rpos_at = [&](int m) { RPos r; r.b = m / Np; const int pi = m - r.b * Np; r.gy = pi / Wp; r.gx = pi - r.gy * Wp; return r; };
+  auto radv = [&](RPos& r) {
+    r.gx += WG_MU;
+    while (r.gx >= Wp) { r.gx -= Wp; if (++r.gy == Hp) { r.gy = 0; ++r.b; } }
+  };
+  // dtok lane rows: patches row_i of the chunk as (b, p), i = the wave's pieces
+  struct TPos { int b, p; };
+  auto tadv = [&](TPos& t) { t.p += WG_MU; while (t.p >= Np) { t.p -= Np; ++t.b; } };
+  const RPos r_first = rpos_at(min(lane >> 1, M - 1));
+  TPos t_first[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int row = ((wv * TPW + i) & 7) * 4 + (lane >> 4), m = min(row, M - 1);
+    t_first[i].b = m / Np; t_first[i].p = m - t_first[i].b * Np;
+  }
+  // cursors: raster issue (runs 4 ahead of compute), dtok issue (2 ahead), convert (1 ahead), compute
+  Cur cr{g0, j0}, ct{g0, j0}, cc{g0, j0}, cm{g0, j0};
+  RPos rp = rpos_at(min(j0 * WG_MU + (lane >> 1), M - 1));
+  TPos tp[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int row = ((wv * TPW + i) & 7) * 4 + (lane >> 4), m = min(j0 * WG_MU + row, M - 1);
+    tp[i].b = m / Np; tp[i].p = m - tp[i].b * Np;
+  }
+  const long HWl = (long)H * W;
+
+  // raster pieces of the raster cursor's unit into ring region k % RN: piece q = (channel of the
+  // pair cl, ky); lane = (patch l >> 1, 16-B half l & 1); then advance the cursor
+  auto issue_r = [&](int k) {
+    const bool mok = cr.j * WG_MU + (lane >> 1) < M;
+    const int b = mok ? rp.b : Bn - 1, gy = mok ? rp.gy : Hp - 1, gx = mok ? rp.gx : Wp - 1;
+    char* st = rreg + (k % RN) * WG_RST;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int q = wv * RPW + i, cl = q >> 3, ky = q & 7;
+      const int c = min(2 * cr.g + cl, C - 1);  // a missing odd channel is zeroed in convert
+      const float* src = img + ((long)b * C + c) * HWl + (long)(gy * 8 + ky) * W + gx * 8 + (lane & 1) * 4;
+      glds_v<true>(src, st + q * 1024);
+    }
+    cnext(cr);
+    if (cr.j == 0) rp = r_first; else radv(rp);
+  };
+  // dtok rows of the dtok cursor's unit: piece = (image ti = 128-column block, 4-row group)
+  auto issue_t = [&](int k) {
+    char* st = treg + (k % 3) * TST;
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      const int piece = wv * TPW + i, ti = piece >> 3, row = (piece & 7) * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ ((row & 3) << 2);
+      const bool mok = ct.j * WG_MU + row < M;
+      const int b = mok ? tp[i].b : Bn - 1, p = mok ? tp[i].p : Np - 1;
+      const bf16* src = dtok + ((long)b * (Np + 1) + 1 + p) * D + ti * 128 + c * 8;
+      glds_v<false>(src, st + ti * WG_TIMG + (piece & 7) * 1024);
+    }
+    cnext(ct);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      if (ct.j == 0) tp[i] = t_first[i];
+      else tadv(tp[i]);
+    }
+  };
+  // own raster pieces of the convert cursor's unit (landed) -> X image k & 1 in MN-contiguous
+  // layout: lane's 4 kx of (cl, ky, patch) -> 8 bytes of chunk cl*8 + ky of row = patch; zero
+  // past M / C
+  auto convert = [&](int k) {
+    const char* st = rreg + (k % RN) * WG_RST + lane * 16;
+    char* xi = ximg + (k & 1) * WG_XST;
+    float4 v[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) v[i] = *(const float4*)(st + (wv * RPW + i) * 1024);
+    const int p = lane >> 1;
+    const bool pok = cc.j * WG_MU + p < M;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int q = wv * RPW + i, cl = q >> 3, ky = q & 7;
+      const bool ok = pok && 2 * cc.g + cl < C;
+      const uint2 val = ok ? make_uint2(pk_bf16(v[i].x, v[i].y), pk_bf16(v[i].z, v[i].w)) : make_uint2(0u, 0u);
+      *(uint2*)(xi + wg_mn_off(p, cl * 8 + ky) + (lane & 1) * 8) = val;
+    }
+    cnext(cc);
+  };
+
+  f32x16 acc[NBN][NBK];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < NBN; ++i)
+#pragma unroll
+      for (int j = 0; j < NBK; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  };
+  // partial tile of pair g -> slab[w][g - g0][n][128]: C layout col = lane & 31 (k),
+  // row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (n); 32 lanes store one 128-B row segment
+  auto flush = [&](int g) {
+    float* o = slab + ((long)w * 2 + (g - g0)) * D * 128;
+#pragma unroll
+    for (int i = 0; i < NBN; ++i)
+#pragma unroll
+      for (int j = 0; j < NBK; ++j) {
+        const int n0 = (ng * NBN + i) * 32, k0 = (kg * NBK + j) * 32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int n = n0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          o[(long)n * 128 + k0 + (lane & 31)] = acc[i][j][r];
+        }
+      }
+  };
+  zero();
+
+  // Pipeline (unit index i = u - u0). vmcnt retires in issue order, so the dtok stage T(i) is
+  // issued between raster units: entering iteration i the order is
+  //   R(i+1) ... T(i) R(i+2) | T(i+1) R(i+3)
+  // and T(i), R(i+1) must land (vmcnt = pieces of R(i+2), T(i+1), R(i+3)). Iteration i issues
+  // T(i+2) R(i+4): R(i+4) reuses R(i)'s region (converted in iteration i-1, own pieces), T(i+2)
+  // reuses T(i-1)'s stage (read by iteration i-1's MFMAs, before this iteration's barrier).
+  issue_t(0);
+  issue_r(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  convert(0);
+  if (nu > 1) issue_r(1);
+  if (nu > 2) issue_r(2);
+  if (nu > 1) issue_t(1);
+  if (nu > 3) issue_r(3);
+  for (int i = 0; i < nu; ++i) {
+    wg_wait_vm((i + 2 < nu ? RPW : 0) + (i + 1 < nu ? TPW : 0) + (i + 3 < nu ? RPW : 0));
+    __builtin_amdgcn_s_barrier();
+    if (i + 2 < nu) issue_t(i + 2);
+    const char* ti = treg + (i % 3) * TST;
+    const char* xi = ximg + (i & 1) * WG_XST;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 fa[NBN], fb[NBK];
+#pragma unroll
+      for (int a = 0; a < NBN; ++a) {
+        const int nb = ng * NBN + a;  // 32-column block of D
+        fa[a] = wg_frag(ti + (nb >> 2) * WG_TIMG, 16 * t, (nb & 3) * 32, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < NBK; ++j) fb[j] = wg_frag(xi, 16 * t, (kg * NBK + j) * 32, lane);
+#pragma unroll
+      for (int a = 0; a < NBN; ++a)
+#pragma unroll
+        for (int j = 0; j < NBK; ++j)
+          acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[j], acc[a][j], 0, 0, 0);
+    }
+    // the next unit's raster converts while these MFMAs drain; then its region is refilled
+    if (i + 1 < nu) convert(i + 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (i + 4 < nu) issue_r(i + 4);
+    const int g = cm.g;
+    cnext(cm);
+    if (i + 1 == nu || cm.g != g) {
+      flush(g);
+      zero();
+    }
+  }
+}
+
+// dW[n][g*128 + k] (+)= sum of the partial tiles of pair g (workgroups whose unit range meets it)
+__global__ __launch_bounds__(256) void patch_wgrad_reduce_kernel(const float* __restrict__ slab, int C, int J, int D,
+                                                                 float* __restrict__ dW, int accumulate) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int G = (C + 1) / 2;
+  if (i >= (long)G * D * 128) return;
+  const int g = (int)(i / ((long)D * 128));
+  const int e = (int)(i - (long)g * D * 128), n = e >> 7, k = e & 127;
+  if (2 * g + (k >> 6) >= C) return;
+  const long U = (long)G * J, ga = (long)g * J, gb = ga + J;
+  int w = (int)(ga * WG_NWG / U);
+  while (w > 0 && wg_unit_start(w, U) > ga) --w;
+  float s = 0.f;
+  for (; w < WG_NWG && wg_unit_start(w, U) < gb; ++w) {
+    const long a = wg_unit_start(w, U), b = wg_unit_start(w + 1, U);
+    if (b <= ga || b <= a) continue;
+    const int slot = g - (int)(a / J);
+    s += slab[(((long)w * 2 + slot) * D + n) * 128 + k];
+  }
+  float* o = dW + (long)n * C * 64 + (long)g * 128 + k;
+  *o = accumulate ? *o + s : s;
+}
+
+}  // namespace
+
+long patch_wgrad_raster_workspace(long D) { return (long)WG_NWG * 2 * D * 128 * 4; }
+
+bool patch_wgrad_raster_ok(long B, long C, long H, long W, long D) {
+  if (D != 384 || H % 8 || W % 8 || B <= 0 || C <= 0) return false;
+  const long Np = (H / 8) * (W / 8), M = B * Np, J = (M + WG_MU - 1) / WG_MU, U = (C + 1) / 2 * J;
+  // every workgroup's unit range (<= ceil(U / 256) units) must meet at most two channel pairs
+  if ((U + WG_NWG - 1) / WG_NWG > J) return false;
+  const long span = 1 + (WG_MU - 1 + Np - 1) / Np;  // images a 32-patch chunk can touch
+  return M < (1L << 31) && span * C * H * W * 4 < (1L << 32) && span * (Np + 1) * D * 2 < (1L << 32);
+}
+
+int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long H, long W, long D, float* dW,
+                       int accumulate, void* work, hipStream_t st) {
+  const int Wp = (int)(W / 8), Np = (int)((H / 8) * Wp), M = (int)(B * Np), J = ivit_cdiv(M, WG_MU);
+  float* slab = (float*)work;
+  hipLaunchKernelGGL((patch_wgrad_kernel<3, 2>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H, (int)W,
+                     Wp, Np, M, J, slab);
+  const long n = (long)((C + 1) / 2) * D * 128;
+  hipLaunchKernelGGL(patch_wgrad_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, (int)C, J, (int)D, dW,
+                     accumulate);
+  return 0;
+}
+
+}  // namespace ivit

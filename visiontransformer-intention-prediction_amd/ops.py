@@ -50,6 +50,22 @@ def cast_weight(w, dtype):
     return y
 
 
+_PACKED = WeakIdKeyDictionary()
+
+
+def packed_patch_weight(w):
+    """PatchEmbed weight [D, C, 8, 8] f32 in the fused forward's MFMA fragment order (bf16),
+    rebuilt when the parameter changes (keyed by its version counter, like cast_weight)."""
+    e = _PACKED.get(w)
+    if e is not None and e[0] == w._version:
+        return e[1]
+    D, C = w.shape[0], w.shape[1]
+    wp = torch.empty(lib.ivit_patch_weight_pack_bytes(D, C) // 2, dtype=torch.bfloat16, device=w.device)
+    lib.ivit_patch_weight_pack(ptr(w.float().contiguous()), D, C, ptr(wp), stream())
+    _PACKED[w] = (w._version, wp)
+    return wp
+
+
 def shadow_of(p):
     """The live bf16 shadow of parameter p (None if there is none or it is stale)."""
     e = _SHADOWS.get(p)
@@ -313,18 +329,28 @@ class PatchEmbedFn(torch.autograd.Function):
         Ntok = (H // 8) * (W // 8) + 1
         wc = cast_weight(w, tdtype(cdt)).reshape(D, C * 64)
         out = torch.empty((B * Ntok, D), dtype=torch.float32, device=img.device)
-        if cdt == BF16:
-            # bf16: one coalesced pass writes the bf16 patch matrix; forward and weight gradient
-            # stream it by LDS-DMA (saved for backward instead of the f32 raster)
+        if cdt == BF16 and (D == 384 or (D == 192 and not ctx.needs_input_grad[1])) and img.data_ptr() % 16 == 0:
+            # bf16: fused forward, the raster streamed through LDS once (no patch matrix); the
+            # weight gradient re-reads the raster (ivit_patch_embed_wgrad: D = 384 kernel)
+            wp = packed_patch_weight(w)
+            lib.ivit_patch_embed_fwd_packed(ptr(img), B, C, H, W, ptr(wp), ptr(b), ptr(pos), ptr(cls), D, ptr(out),
+                                            stream())
+            ctx.save_for_backward(img)
+            ctx.cols = False
+        elif cdt == BF16:
+            # bf16, other widths: one coalesced pass writes the bf16 patch matrix; forward and
+            # weight gradient stream it by LDS-DMA (saved for backward instead of the f32 raster)
             cols = torch.empty((B * (Ntok - 1), C * 64), dtype=torch.bfloat16, device=img.device)
             lib.ivit_patch_im2col(ptr(img), B, C, H, W, ptr(cols), stream())
             lib.ivit_patch_embed_fwd_cols(ptr(cols), B, C, H, W, ptr(wc), ptr(b), ptr(pos), ptr(cls), D, ptr(out),
                                           stream())
             ctx.save_for_backward(cols)
+            ctx.cols = True
         else:
             lib.ivit_patch_embed_fwd(cdt, ptr(img), B, C, H, W, ptr(wc), ptr(b), ptr(pos), ptr(cls), D, ptr(out),
                                      stream())
             ctx.save_for_backward(img)
+            ctx.cols = False
         ctx.meta = (B, C, H, W, D, cdt, w.shape)
         return out
 
@@ -339,7 +365,7 @@ class PatchEmbedFn(torch.autograd.Function):
         dpos = torch.empty((1, Ntok, D), dtype=torch.float32, device=src.device)
         dcls = torch.empty((1, 1, D), dtype=torch.float32, device=src.device)
         ws = workspace(lib.ivit_patch_embed_wgrad_workspace(B, C, H, W, D), src.device)
-        if cdt == BF16:
+        if ctx.cols:
             lib.ivit_patch_embed_wgrad_cols(ptr(dtok), ptr(src), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos),
                                             ptr(dcls), 0, ptr(ws), ws.numel(), stream())
         else:
