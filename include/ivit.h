@@ -49,6 +49,14 @@ int ivit_linear_dgrad(int dtype, const void* dY, long lddy, const void* W, long 
 long ivit_linear_wgrad_workspace(long M, long N, long K);
 int ivit_linear_wgrad(int dtype, const void* dY, long lddy, const void* X, long ldx, long M, long N, long K,
                       float* dW, float* dbias, int accumulate, void* work, long work_bytes, void* stream);
+/* Residual GEMM + the following LayerNorm in one kernel (timm Block: x1 = x + dp1(proj(.)), then
+ * norm2(x1); model_vit.py:64,71 -> timm Block.forward), bf16 operands, N = 384:
+ *   X = R + scale[m / rps] * (A W^T + bias)  (f32)   Y = bf16(LN(X; gamma, beta, eps)), mean, rstd [M]
+ * W packed by ivit_patch_weight_pack(W f32 [N][K], N, K / 64, ...); K % 64 == 0; scale may be null. */
+int ivit_linear_resid_ln_fwd(const void* A, long lda, long M, long N, long K, const void* wpack, const float* bias,
+                             const float* R, long ldr, const float* scale, long rps, const float* gamma,
+                             const float* beta, float eps, float* X, long ldx, void* Y, long ldy, float* mean,
+                             float* rstd, void* stream);
 
 /* ---- timm PatchEmbed (Conv2d k=s=8) + CLS concat + pos_embed (model_vit.py:64,71 → timm). */
 int ivit_patch_embed_fwd(int dtype, const float* img, long B, long C, long H, long W, const void* Wt,

@@ -335,6 +335,36 @@ def test_patch_wgrad_raster_exact(B, C, H, W):
     assert (dw.double().cpu().reshape(D, C * 64) - 2 * ref).abs().max().item() < 2 * err + 1e-5
 
 
+@pytest.mark.parametrize("M,K,scale", [(36008, 384, True), (300, 1536, False), (1, 64, True), (145, 128, True)])
+def test_linear_resid_ln_fused(M, K, scale):
+    """ivit_linear_resid_ln_fwd (proj + residual + DropPath scale + norm2 in one kernel) vs a
+    torch f64 reference on the same bf16 operands: partial last row panel, one row, K = 64."""
+    import ops
+    g = torch.Generator().manual_seed(M + K)
+    N = 384
+    a = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    w = torch.randn(N, K, generator=g) / math.sqrt(K)
+    b = 0.1 * torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g)
+    s = (torch.rand(max(1, M // 7 + 1), generator=g) + 0.5) if scale else None
+    gm, bt = 1 + 0.1 * torch.randn(N, generator=g), 0.1 * torch.randn(N, generator=g)
+    x, y, mean, rstd = ops.linear_resid_ln_fwd(a.to(DEV), w.to(DEV), b.to(DEV), r.to(DEV),
+                                               s.to(DEV) if scale else None, 7, gm.to(DEV), bt.to(DEV), 1e-6)
+    z = a.double() @ w.to(torch.bfloat16).double().t() + b.double()
+    if scale:
+        z = z * s.double()[torch.arange(M) // 7][:, None]
+    xr = r.double() + z
+    mu = xr.mean(1)
+    var = ((xr - mu[:, None]) ** 2).mean(1)
+    rs = 1 / torch.sqrt(var + 1e-6)
+    yr = (xr - mu[:, None]) * rs[:, None] * gm.double() + bt.double()
+    assert (x.double().cpu() - xr).abs().max().item() < 2e-5 * math.sqrt(K)
+    assert (mean.double().cpu() - mu).abs().max().item() < 1e-5
+    assert ((rstd.double().cpu() - rs).abs() / rs).max().item() < 1e-4
+    assert (y.double().cpu() - yr).abs().max().item() < 0.02 * yr.abs().max().item()
+    assert _rel(y.float(), yr) < 4e-3
+
+
 def test_patch_im2col_bitexact():
     """bf16 patch matrix (the throughput path's GEMM operand) is exactly the rearranged, rounded raster."""
     from _lib import lib, ptr, stream

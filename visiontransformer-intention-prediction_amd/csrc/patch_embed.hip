@@ -26,6 +26,7 @@
 // in-flight raster stages (the counter retires in issue order). Issue order per stage kt-1 ->
 // kt: B(kt), then A(kt+1), so waiting for B(kt) leaves A(kt+1) in flight (vmcnt(9)).
 #include "patch_embed.h"
+#include "panel_common.h"
 
 namespace ivit {
 namespace {
@@ -36,61 +37,11 @@ constexpr int PE_STAGE = PE_MT * 8 * 32;      // bytes per LDS stage: [ky 8][pat
 constexpr int PE_NS = 3;                      // f32 LDS stages (raster DMA ring)
 constexpr int PE_BSTAGE = PE_MT * 8 * 16;     // bf16 operand stage: [ky 8][patch][16 B]
 constexpr int PE_PIECES = PE_STAGE / 1024;    // 1-KiB DMA pieces per stage (36)
-constexpr int NBW = 3;                        // 16-column MFMA blocks per wave (48 columns)
-
-// s_waitcnt vmcnt(n) for the counts that occur: n = {0, 1, 2} x piece count (4, 5 or 9) + {0, 6}
-// (the field is an immediate; n is wave-uniform)
-#define PE_VM(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-IVIT_DEV void wait_vm(int n) {
-  switch (n) {
-    PE_VM(4) PE_VM(5) PE_VM(6) PE_VM(8) PE_VM(9) PE_VM(10) PE_VM(11) PE_VM(14) PE_VM(15) PE_VM(16) PE_VM(18)
-    PE_VM(24)
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-}
-#undef PE_VM
-
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-// Wave-uniform 64-bit address -> SGPR pair (the saddr operand of the loads below).
-IVIT_DEV const char* uniform_ptr(const void* p) {
-  const unsigned long v = (unsigned long)p;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  return (const char*)(((unsigned long)hi << 32) | lo);
-}
-
-// 16 B per lane from sbase + voff + OFF into VGPRs (saddr form: one VGPR of per-lane offset).
-template <int OFF>
-IVIT_DEV void gload_b128(u32x4& r, unsigned voff, const char* sbase) {
-  static_assert(OFF >= 0 && OFF < 4096, "global offset field");
-  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3" : "=v"(r) : "v"(voff), "s"(sbase), "i"(OFF) : "memory");
-}
-
-// LDS-DMA, saddr form: lane's 16 B from sbase + voff land at lds + 16 * lane (lds wave-uniform -> M0).
-// NT: the raster is read once, non-temporal (measured 0.54 vs 0.61 ms per LiDAR forward).
-template <bool NT = true>
-IVIT_DEV void glds_s(unsigned voff, const char* sbase, void* lds) {
-  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
-  if constexpr (NT)
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2 nt" ::"v"(voff), "s"(a), "s"(sbase)
-                 : "memory");
-  else
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %2" ::"v"(voff), "s"(a), "s"(sbase)
-                 : "memory");
-}
 
 IVIT_DEV bf16x8 cvt8(const float4 a, const float4 b) {
   Pack8 p;
   p.u = f32x8_to_bf16x8(a, b);
   return p.v;
-}
-
-// The 2*NBW fragment registers of one stage become visible to the compiler only here, after the
-// counted wait that retired their loads.
-IVIT_DEV void tie(u32x4 (&r)[2 * NBW]) {
-  asm volatile("" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), "+v"(r[5]));
 }
 
 // NW waves = D / 48 (8 at D = 384: two per SIMD; 4 at D = 192).
@@ -363,25 +314,6 @@ IVIT_DEV bf16x8 wg_frag(const char* img, int kbase, int colbase, int lane) {
 
 IVIT_DEV long wg_unit_start(int w, long U) { return (long)w * U / WG_NWG; }
 
-// LDS-DMA from a per-lane 64-bit address (lds wave-uniform -> M0).
-template <bool NT>
-IVIT_DEV void glds_v(const void* src, void* lds) {
-  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
-  if constexpr (NT)
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(src), "s"(a) : "memory");
-  else
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(a) : "memory");
-}
-
-#define WG_VM(N) \
-  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-IVIT_DEV void wg_wait_vm(int n) {
-  switch (n) {
-    WG_VM(2) WG_VM(3) WG_VM(4) WG_VM(5) WG_VM(6) WG_VM(7) WG_VM(8) WG_VM(10)
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-}
-#undef WG_VM
 
 // NT = D / 128 dtok images; NBK = k-blocks (of 32) per wave (D = 384: NT = 3, NBK = 2).
 template <int NT, int NBK>
@@ -542,7 +474,7 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
   if (nu > 1) issue_t(1);
   if (nu > 3) issue_r(3);
   for (int i = 0; i < nu; ++i) {
-    wg_wait_vm((i + 2 < nu ? RPW : 0) + (i + 1 < nu ? TPW : 0) + (i + 3 < nu ? RPW : 0));
+    wait_vm((i + 2 < nu ? RPW : 0) + (i + 1 < nu ? TPW : 0) + (i + 3 < nu ? RPW : 0));
     __builtin_amdgcn_s_barrier();
     if (i + 2 < nu) issue_t(i + 2);
     const char* ti = treg + (i % 3) * TST;

@@ -1,0 +1,213 @@
+// Residual GEMM with the following LayerNorm fused into its epilogue (timm Block: x1 = x +
+// dp1(proj(attn)); then norm2(x1) — model_vit.py:64,71 -> timm Block.forward):
+//
+//   X[m][n] = R[m][n] + scale[m / rps] * (sum_k A[m][k] W[n][k] + bias[n])           f32, N = 384
+//   Y[m][n] = bf16((X[m][n] - mean_m) * rstd_m * gamma[n] + beta[n]),  mean_m, rstd_m   (eps)
+//
+// LayerNorm needs whole rows, so a workgroup owns a panel of 144 rows x ALL 384 columns (the
+// patch-embedding kernel's tiling: 250 workgroups for the 36 008 token rows of a B = 8 ViT
+// stream, one per CU). A (bf16 activations, K-contiguous) streams through a 4-stage LDS ring by
+// LDS-DMA; the weight, packed in MFMA fragment order (ivit_patch_weight_pack layout), goes to
+// VGPRs two K-stages ahead; 8 waves x (144 rows x 48 columns) of v_mfma_f32_16x16x32_bf16.
+// Epilogue per 16-row block: acc + bias through LDS into row-major order, then 32 lanes per row
+// add the residual (coalesced), store X, reduce the row mean and the centred variance by
+// cross-lane shuffles (two passes, as torch's LayerNorm) and store Y, mean, rstd. This replaces
+// the EpiResid GEMM + ln_fwd_vec_kernel pair (the LayerNorm re-read X from HBM).
+#include "panel_common.h"
+
+namespace ivit {
+namespace {
+
+constexpr int RP_MT = 144;                 // rows per workgroup
+constexpr int RP_MB = RP_MT / 16;          // 16-row MFMA blocks
+constexpr int RP_N = 384;                  // output columns (8 waves x 3 x 16)
+constexpr int RP_STAGE = RP_MT * 128;      // A stage: [144 rows][64 k] bf16, 16-B chunks swizzled
+constexpr int RP_NS = 4;                   // A ring (three stages in flight)
+constexpr int RP_PIECES = RP_STAGE / 1024; // 18 DMA pieces of 8 rows
+constexpr int RP_TLD = RP_N + 4;           // epilogue row stride (floats)
+
+IVIT_DEV int rp_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+__global__ __launch_bounds__(512, 1) void rowpanel_resid_ln_kernel(
+    const bf16* __restrict__ A, long lda, int M, int K, const u32x4* __restrict__ wpack,
+    const float* __restrict__ bias, const float* __restrict__ R, long ldr, const float* __restrict__ scale, int rps,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* __restrict__ X, long ldx,
+    bf16* __restrict__ Y, long ldy, float* __restrict__ mean, float* __restrict__ rstd) {
+  __shared__ __attribute__((aligned(16))) char smem[RP_NS * RP_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * RP_MT;
+  const int KT = K / 64;
+
+  // A pieces per wave: 18 over 8 waves, the first two take three
+  constexpr int PW = 3, PREM = RP_PIECES % 8;
+  const int npc = wv < PREM ? PW : PW - 1;
+  const int pc0 = wv < PREM ? wv * PW : PREM * PW + (wv - PREM) * (PW - 1);
+  unsigned voff[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int row = min(pc0 + i, RP_PIECES - 1) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);  // stored chunk (lane & 7) holds source chunk c
+    const int m = min(m0 + row, M - 1) - m0;      // rows past M are computed, never stored
+    voff[i] = (unsigned)(((long)m * lda + c * 8) * 2);
+  }
+  const bf16* A0 = A + (long)m0 * lda;
+  auto issue_a = [&](int kt) {
+    char* st = smem + (kt % RP_NS) * RP_STAGE + pc0 * 1024;
+    const char* sb = uniform_ptr(A0 + kt * 64);
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      if (i < npc) glds_s<false>(voff[i], sb, st + i * 1024);
+  };
+  const int NB16 = RP_N / 16;
+  const unsigned vb = lane * 16;
+  auto issue_b = [&](int kt, u32x4 (&r)[2 * NBW]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) load_wfrag(r, t, uniform_ptr(wpack + ((long)(2 * kt + t) * NB16 + wv * NBW) * 64), vb);
+  };
+
+  f32x4 acc[RP_MB][NBW];
+#pragma unroll
+  for (int i = 0; i < RP_MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 breg[3][2 * NBW];
+  // Issue order: A(kt) B(kt) ... with B(kt) between A(kt) and A(kt+1); iteration kt issues
+  // B(kt+2) A(kt+3), and waits for A(kt), B(kt) with A(kt+1) B(kt+1) A(kt+2) still in flight.
+  auto stage = [&](int kt, u32x4 (&cur)[2 * NBW], u32x4 (&nb2)[2 * NBW]) {
+    wait_vm((kt + 1 < KT ? npc + 2 * NBW : 0) + (kt + 2 < KT ? npc : 0));
+    tie(cur);
+    __builtin_amdgcn_s_barrier();  // every wave's pieces of A(kt); stage (kt-1) % 4 free
+    if (kt + 2 < KT) issue_b(kt + 2, nb2);
+    if (kt + 3 < KT) issue_a(kt + 3);
+    const char* ia = smem + (kt % RP_NS) * RP_STAGE;
+    // fragment f = (t = f / 9: 32-k half, mb = f % 9): rows 16 mb + (lane & 15), chunk 4t + lane/16;
+    // read three ahead of their MFMAs (sched barriers pin the distance)
+    auto rdf = [&](int f) {
+      const int row = 16 * (f % RP_MB) + (lane & 15), ch = 4 * (f / RP_MB) + (lane >> 4);
+      return *(const bf16x8*)(ia + rp_off(row, ch));
+    };
+    bf16x8 fr[4];
+    fr[0] = rdf(0);
+    fr[1] = rdf(1);
+    fr[2] = rdf(2);
+#pragma unroll
+    for (int f = 0; f < 2 * RP_MB; ++f) {
+      const int t = f / RP_MB, mb = f % RP_MB;
+      if (f + 3 < 2 * RP_MB) fr[(f + 3) % 4] = rdf(f + 3);
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) {
+        union { u32x4 u; bf16x8 v; } bw;
+        bw.u = cur[t * NBW + j];
+        acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[f % 4], bw.v, acc[mb][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of stage kt are done
+  };
+
+  issue_a(0);
+  issue_b(0, breg[0]);
+  if (KT > 1) issue_a(1);
+  if (KT > 1) issue_b(1, breg[1]);
+  if (KT > 2) issue_a(2);
+  for (int kt = 0; kt < KT; kt += 3) {
+    stage(kt, breg[0], breg[2]);
+    if (kt + 1 < KT) stage(kt + 1, breg[1], breg[0]);
+    if (kt + 2 < KT) stage(kt + 2, breg[2], breg[1]);
+  }
+
+  // ---- epilogue, one 16-row block at a time through LDS
+  __builtin_amdgcn_s_barrier();  // every wave is done with the A ring
+  float* T = (float*)smem;       // [16][RP_TLD]
+  float bv[NBW];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) bv[j] = bias ? bias[(wv * NBW + j) * 16 + (lane & 15)] : 0.f;
+  const int r = tid >> 5, c0 = (tid & 31) * 12;  // row phase: 32 lanes per row, 12 columns each
+  float gm[12], bt[12];
+#pragma unroll
+  for (int e = 0; e < 12; ++e) { gm[e] = gamma[c0 + e]; bt[e] = beta[c0 + e]; }
+  // residual rows of block mb + 1 are loaded while block mb is reduced
+  auto load_res = [&](int mb, float4 (&rv)[3], float& s) {
+    const int m = min(m0 + 16 * mb + r, M - 1);
+    const float* rrow = R + (long)m * ldr + c0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) rv[e] = *(const float4*)(rrow + 4 * e);
+    s = scale ? scale[m / rps] : 1.f;
+  };
+  float4 rv[3];
+  float sc;
+  load_res(0, rv, sc);
+#pragma unroll
+  for (int mb = 0; mb < RP_MB; ++mb) {
+#pragma unroll
+    for (int j = 0; j < NBW; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        T[(4 * (lane >> 4) + i) * RP_TLD + (wv * NBW + j) * 16 + (lane & 15)] = acc[mb][j][i] + bv[j];
+    __builtin_amdgcn_s_barrier();
+    const int m = m0 + 16 * mb + r;
+    const bool ok = m < M;
+    float x[12];
+#pragma unroll
+    for (int e = 0; e < 12; e += 4) {
+      const float4 tv = *(const float4*)(T + r * RP_TLD + c0 + e);
+      const float4 q = rv[e / 4];
+      x[e] = q.x + sc * tv.x; x[e + 1] = q.y + sc * tv.y; x[e + 2] = q.z + sc * tv.z; x[e + 3] = q.w + sc * tv.w;
+    }
+    if (mb + 1 < RP_MB) load_res(mb + 1, rv, sc);
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) sum += x[e];
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    const float mu = sum * (1.f / RP_N);
+    float sq = 0.f;
+#pragma unroll
+    for (int e = 0; e < 12; ++e) { const float d = x[e] - mu; sq += d * d; }
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) sq += __shfl_xor(sq, o, 64);
+    const float rs = rsqrtf(sq * (1.f / RP_N) + eps);
+    if (ok) {
+      float* xrow = X + (long)m * ldx + c0;
+#pragma unroll
+      for (int e = 0; e < 12; e += 4) *(float4*)(xrow + e) = make_float4(x[e], x[e + 1], x[e + 2], x[e + 3]);
+      unsigned pk[6];
+#pragma unroll
+      for (int e = 0; e < 12; e += 2)
+        pk[e / 2] = pk_bf16((x[e] - mu) * rs * gm[e] + bt[e], (x[e + 1] - mu) * rs * gm[e + 1] + bt[e + 1]);
+      bf16* yrow = Y + (long)m * ldy + c0;
+      *(uint2*)yrow = make_uint2(pk[0], pk[1]);
+      *(uint2*)(yrow + 4) = make_uint2(pk[2], pk[3]);
+      *(uint2*)(yrow + 8) = make_uint2(pk[4], pk[5]);
+      if ((tid & 31) == 0) { mean[m] = mu; rstd[m] = rs; }
+    }
+    __builtin_amdgcn_s_barrier();  // T is rewritten by the next block
+  }
+}
+
+}  // namespace
+}  // namespace ivit
+
+using namespace ivit;
+
+extern "C" int ivit_linear_resid_ln_fwd(const void* A, long lda, long M, long N, long K, const void* wpack,
+                                        const float* bias, const float* R, long ldr, const float* scale, long rps,
+                                        const float* gamma, const float* beta, float eps, float* X, long ldx, void* Y,
+                                        long ldy, float* mean, float* rstd, void* stream) {
+  IVIT_CHECK_ARG(N == RP_N, "ivit_linear_resid_ln_fwd: N must be %d (got %ld)", RP_N, N);
+  IVIT_CHECK_ARG(M > 0 && K > 0 && K % 64 == 0, "ivit_linear_resid_ln_fwd: K must be a positive multiple of 64");
+  IVIT_CHECK_ARG(lda >= K && lda % 8 == 0 && ldr >= N && ldr % 4 == 0 && ldx >= N && ldx % 4 == 0 && ldy >= N &&
+                     ldy % 4 == 0 && rps > 0,
+                 "ivit_linear_resid_ln_fwd: bad leading dimensions");
+  IVIT_CHECK_ARG(RP_MT * lda * 2 < (1L << 32) && M < (1L << 31), "ivit_linear_resid_ln_fwd: too large");
+  IVIT_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)wpack & 15) == 0 && ((uintptr_t)R & 15) == 0 &&
+                     ((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 7) == 0,
+                 "ivit_linear_resid_ln_fwd: misaligned operand");
+  hipLaunchKernelGGL(rowpanel_resid_ln_kernel, dim3(ivit_cdiv(M, RP_MT)), dim3(512), 0, ivit_stream(stream),
+                     (const bf16*)A, lda, (int)M, (int)K, (const u32x4*)wpack, bias, R, ldr, scale, (int)rps, gamma,
+                     beta, eps, X, ldx, (bf16*)Y, ldy, mean, rstd);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}

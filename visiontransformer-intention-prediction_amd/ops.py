@@ -53,13 +53,14 @@ def cast_weight(w, dtype):
 _PACKED = WeakIdKeyDictionary()
 
 
-def packed_patch_weight(w):
-    """PatchEmbed weight [D, C, 8, 8] f32 in the fused forward's MFMA fragment order (bf16),
-    rebuilt when the parameter changes (keyed by its version counter, like cast_weight)."""
+def packed_weight(w):
+    """A [D, K] weight (PatchEmbed [D, C, 8, 8]: K = 64 C) f32 in the row-panel kernels' MFMA
+    fragment order (bf16), rebuilt when the parameter changes (keyed by its version counter,
+    like cast_weight)."""
     e = _PACKED.get(w)
     if e is not None and e[0] == w._version:
         return e[1]
-    D, C = w.shape[0], w.shape[1]
+    D, C = w.shape[0], w[0].numel() // 64
     wp = torch.empty(lib.ivit_patch_weight_pack_bytes(D, C) // 2, dtype=torch.bfloat16, device=w.device)
     lib.ivit_patch_weight_pack(ptr(w.float().contiguous()), D, C, ptr(wp), stream())
     _PACKED[w] = (w._version, wp)
@@ -124,6 +125,21 @@ def layernorm_fwd(x, g, b, eps, out_dtype, rowmap=(0, 0, 0), M=None):
     lib.ivit_layernorm_fwd(ptr(x), x.stride(0), rowmap[0], rowmap[1], rowmap[2], M, D, ptr(g), ptr(b), eps, ptr(y),
                            D, dt(y), ptr(mean), ptr(rstd), stream())
     return y, mean, rstd
+
+
+def linear_resid_ln_fwd(a, w, b, resid, row_scale, rps, g, beta, eps):
+    """bf16 a [M, K] @ w[384, K]^T + b, times row_scale[m / rps], plus the f32 residual → x (f32),
+    then LayerNorm(x) → y (bf16), mean, rstd: one kernel (ivit_linear_resid_ln_fwd)."""
+    M, K = a.shape
+    N = w.shape[0]
+    x = torch.empty((M, N), dtype=torch.float32, device=a.device)
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    mean = torch.empty((M,), dtype=torch.float32, device=a.device)
+    rstd = torch.empty((M,), dtype=torch.float32, device=a.device)
+    lib.ivit_linear_resid_ln_fwd(ptr(a), a.stride(0), M, N, K, ptr(packed_weight(w)), ptr(b), ptr(resid),
+                                 resid.stride(0), ptr(row_scale), rps, ptr(g), ptr(beta), eps, ptr(x), N, ptr(y), N,
+                                 ptr(mean), ptr(rstd), stream())
+    return x, y, mean, rstd
 
 
 def layernorm_bwd(x, g, mean, rstd, dy, dres=None, dx=None, xs_dtype=None, row_scale=None, rps=1, rowmap=(0, 0, 0)):
@@ -332,7 +348,7 @@ class PatchEmbedFn(torch.autograd.Function):
         if cdt == BF16 and (D == 384 or (D == 192 and not ctx.needs_input_grad[1])) and img.data_ptr() % 16 == 0:
             # bf16: fused forward, the raster streamed through LDS once (no patch matrix); the
             # weight gradient re-reads the raster (ivit_patch_embed_wgrad: D = 384 kernel)
-            wp = packed_patch_weight(w)
+            wp = packed_weight(w)
             lib.ivit_patch_embed_fwd_packed(ptr(img), B, C, H, W, ptr(wp), ptr(b), ptr(pos), ptr(cls), D, ptr(out),
                                             stream())
             ctx.save_for_backward(img)
@@ -415,42 +431,78 @@ def _wgrad(fork, dy, x, cdt):
 
 class ViTBlockFn(torch.autograd.Function):
     """timm Block: x + dp1(proj(attn(norm1 x))); x + dp2(fc2(gelu(fc1(norm2 x)))).
-    x: (B*N, D) f32 residual stream; GEMM operands in the compute dtype (f32 or bf16)."""
+    x: (B*N, D) f32 residual stream; GEMM operands in the compute dtype (f32 or bf16).
+
+    bf16 row-panel fusion (D = 384): the proj GEMM's epilogue also applies norm2, and — when
+    the NEXT block's norm1 parameters are passed (nxw, nxb) — the fc2 GEMM's epilogue applies
+    that norm1 too and returns it as the second output; the next block then takes it as `ln_in`
+    (and skips its own norm1), and this block's backward owns that LayerNorm's backward (its
+    input gradient joins dx2; its parameter gradients are returned for nxw, nxb). The norm1
+    output is bf16 but its gradient is f32 (as in the unfused block), so the gradient does not
+    travel through autograd (which would cast it to the output's dtype): the output carries a
+    small holder the next block's backward fills, and the output itself is non-differentiable.
+    This block's backward runs after the next one's (it needs dx2 from it), so the holder is
+    filled by then. Without fusion the second output is an empty tensor."""
 
     @staticmethod
-    def forward(ctx, x, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, s1, s2, meta):
+    def forward(ctx, x, ln_in, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, nxw, nxb, s1, s2, meta):
         B, N, H, cdt, eps = meta
         cd = tdtype(cdt)
         wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
-        ln1, m1, r1 = layernorm_fwd(x, n1w, n1b, eps, cd)
+        own_ln1 = ln_in is None
+        if own_ln1:
+            ln1, m1, r1 = layernorm_fwd(x, n1w, n1b, eps, cd)
+        else:
+            ln1, m1, r1 = ln_in, None, None
         q2 = cdt == BF16
+        panel = q2 and x.shape[1] == 384
         if q2:
             qkv = qkv_fwd_q2(ln1, wq, qkvb, H * 64)
             o, lse = attn_fwd_q2(qkv, B, N, H)
         else:
             qkv, _ = linear_fwd(ln1, wq, qkvb, cdt)
             o, lse = attn_fwd(qkv, B, N, H, cdt)
-        x1, _ = linear_fwd(o, wp, pb, cdt, resid=x, row_scale=s1, rps=N)
-        ln2, m2, r2 = layernorm_fwd(x1, n2w, n2b, eps, cd)
+        if panel:
+            x1, ln2, m2, r2 = linear_resid_ln_fwd(o, pw, pb, x, s1, N, n2w, n2b, eps)
+        else:
+            x1, _ = linear_fwd(o, wp, pb, cdt, resid=x, row_scale=s1, rps=N)
+            ln2, m2, r2 = layernorm_fwd(x1, n2w, n2b, eps, cd)
         # inference (torch.inference_mode): nothing is saved, and fc1 skips its pre-activation copy
         infer = torch.is_inference_mode_enabled()
         a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=not infer)
-        x2, _ = linear_fwd(a, w2, f2b, cdt, resid=x1, row_scale=s2, rps=N)
+        nx = nxw is not None and panel
+        if nx:
+            x2, lnx, mx, rx = linear_resid_ln_fwd(a, f2w, f2b, x1, s2, N, nxw, nxb, eps)
+        else:
+            x2, _ = linear_fwd(a, w2, f2b, cdt, resid=x1, row_scale=s2, rps=N)
+            lnx, mx, rx = x2.new_empty(0), None, None
+        ctx.mark_non_differentiable(lnx)
+        ctx.carrier = {}
+        if nx:
+            lnx._ivit_grad_carrier = ctx.carrier
+        ctx.in_carrier = None if own_ln1 else getattr(ln_in, "_ivit_grad_carrier", None)
         if infer:
             ctx.meta, ctx.q2 = meta, q2
-            return x2
-        ctx.save_for_backward(x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2)
+            return x2, lnx
+        ctx.save_for_backward(x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2,
+                              x2 if nx else None, nxw if nx else None, mx, rx)
         ctx.meta = meta
         ctx.q2 = q2
-        return x2
+        ctx.own_ln1, ctx.nx = own_ln1, nx
+        return x2, lnx
 
     @staticmethod
-    def backward(ctx, dx2):
-        (x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2) = ctx.saved_tensors
+    def backward(ctx, dx2, _unused):
+        (x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2,
+         x2, nxw, mx, rx) = ctx.saved_tensors
         B, N, H, cdt, eps = ctx.meta
         cd = tdtype(cdt)
         dx2 = dx2.contiguous()
         D = x.shape[1]
+        dnxw = dnxb = None
+        dlnx = ctx.carrier.pop("dln", None)
+        if ctx.nx and dlnx is not None:  # the next block's norm1 ran in our fc2 epilogue: its backward is ours
+            dx2, _, dnxw, dnxb = layernorm_bwd(x2, nxw, mx, rx, dlnx, dres=dx2, dx=torch.empty_like(dx2))
         # The weight gradients are off the critical path: they run on a forked stream and
         # overlap the dgrad chain (notably the attention backward); joined before returning.
         fork = _WgradFork(dx2.device) if dx2.is_cuda and WGRAD_FORK else None
@@ -466,11 +518,18 @@ class ViTBlockFn(torch.autograd.Function):
         dqkv = attn_bwd_q2(qkv, o, do, lse, B, N, H) if ctx.q2 else attn_bwd(qkv, o, do, lse, B, N, H, cdt)
         dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
         gq = _wgrad(fork, dqkv, ln1, cdt)
-        dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
+        if ctx.own_ln1:
+            dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
+            dln_in = None
+        else:  # norm1 ran in the previous block, which takes dln1 (f32) and does its backward
+            dx0, dg1, dbe1, dln_in = dx1, None, None, None
+            if ctx.in_carrier is not None:
+                ctx.in_carrier["dln"] = dln1
         if fork is not None:
             fork.join((dx2s, dh, dx1s, dqkv, a, ln2, o, ln1))
         (dW2, db2), (dW1, db1), (dWp, dbp), (dWq, dbq) = g2, g1, gp, gq
-        return dx0, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, None, None, None
+        return (dx0, dln_in, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, dnxw, dnxb,
+                None, None, None)
 
 
 class NeckFn(torch.autograd.Function):

@@ -75,17 +75,22 @@ class Block(nn.Module):
         self.last_scales = (s[0].contiguous(), s[1].contiguous())
         return self.last_scales
 
-    def forward_flat(self, x, B, N, cdt):
+    def forward_flat(self, x, B, N, cdt, ln_in=None, next_norm=None):
+        """-> (x_out, next norm1 output or an empty tensor): `ln_in` is this block's norm1 output
+        computed by the previous block's fc2 epilogue; `next_norm` the next block's norm1, whose
+        forward this block's fc2 epilogue runs (ops.ViTBlockFn, bf16 row-panel path)."""
         s1, s2 = self._scales(B, x.device)
-        return ops.ViTBlockFn.apply(x, self.norm1.weight, self.norm1.bias, self.attn.qkv.weight, self.attn.qkv.bias,
-                                    self.attn.proj.weight, self.attn.proj.bias, self.norm2.weight, self.norm2.bias,
-                                    self.mlp.fc1.weight, self.mlp.fc1.bias, self.mlp.fc2.weight, self.mlp.fc2.bias,
-                                    s1, s2, (B, N, self.attn.num_heads, cdt, 1e-6))
+        nxw = next_norm.weight if next_norm is not None else None
+        nxb = next_norm.bias if next_norm is not None else None
+        return ops.ViTBlockFn.apply(x, ln_in, self.norm1.weight, self.norm1.bias, self.attn.qkv.weight,
+                                    self.attn.qkv.bias, self.attn.proj.weight, self.attn.proj.bias, self.norm2.weight,
+                                    self.norm2.bias, self.mlp.fc1.weight, self.mlp.fc1.bias, self.mlp.fc2.weight,
+                                    self.mlp.fc2.bias, nxw, nxb, s1, s2, (B, N, self.attn.num_heads, cdt, 1e-6))
 
     def forward(self, x):
         B, N, D = x.shape
         cdt = BF16 if getattr(self, "compute_dtype", torch.float32) == torch.bfloat16 else F32
-        return self.forward_flat(x.reshape(B * N, D).contiguous().float(), B, N, cdt).reshape(B, N, D)
+        return self.forward_flat(x.reshape(B * N, D).contiguous().float(), B, N, cdt)[0].reshape(B, N, D)
 
 
 class VisionTransformer(nn.Module):
@@ -123,8 +128,13 @@ class VisionTransformer(nn.Module):
         t = ops.PatchEmbedFn.apply(x.float().contiguous(), self.patch_embed.proj.weight, self.patch_embed.proj.bias,
                                    self.pos_embed, self.cls_token, cdt)
         N = self.patch_embed.num_patches + 1
-        for blk in self.blocks:
-            t = blk.forward_flat(t, B, N, cdt)
+        # bf16 at D = 384: block i's fc2 epilogue also produces block i+1's norm1 (ops.ViTBlockFn)
+        fuse = cdt == BF16 and self.embed_dim == 384
+        ln = None
+        for i, blk in enumerate(self.blocks):
+            nxt = self.blocks[i + 1].norm1 if fuse and i + 1 < len(self.blocks) else None
+            t, lnx = blk.forward_flat(t, B, N, cdt, ln_in=ln, next_norm=nxt)
+            ln = lnx if nxt is not None else None
         return t
 
     def forward_features(self, x):
