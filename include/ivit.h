@@ -58,6 +58,18 @@ int ivit_linear_resid_ln_fwd(const void* A, long lda, long M, long N, long K, co
                              const float* beta, float eps, float* X, long ldx, void* Y, long ldy, float* mean,
                              float* rstd, void* stream);
 
+/* Backward twin: the LayerNorm input's dgrad with the LayerNorm backward in the epilogue (timm
+ * norm1 / norm2 backward after Attention.qkv / Mlp.fc1 dgrad), N = 384, bf16 dY [M][K]:
+ *   G = dY W (W [K][N], packed transposed by ivit_weight_pack_t);  dX = dres + LN_bwd(G; X, gamma,
+ *   mean, rstd);  dXs = bf16(dX * scale[m / rps]) if non-null;  dgamma / dbeta (+)= column sums.
+ * dX may alias dres; work >= ivit_linear_dgrad_ln_bwd_workspace(M, N). */
+long ivit_linear_dgrad_ln_bwd_workspace(long M, long N);
+int ivit_linear_dgrad_ln_bwd(const void* dY, long lddy, long M, long N, long K, const void* wpack_t, const float* X,
+                             long ldx, const float* gamma, const float* mean, const float* rstd, const float* dres,
+                             long ldr, float* dX, long lddx, void* dXs, const float* scale, long rps, float* dgamma,
+                             float* dbeta, int accumulate, void* work, long work_bytes, void* stream);
+/* W [K][N] f32 -> the row-panel packed bf16 layout of W^T (ivit_patch_weight_pack_bytes(N, K / 64) bytes). */
+int ivit_weight_pack_t(const float* w, long K, long N, void* wpack, void* stream);
 /* ---- timm PatchEmbed (Conv2d k=s=8) + CLS concat + pos_embed (model_vit.py:64,71 → timm). */
 int ivit_patch_embed_fwd(int dtype, const float* img, long B, long C, long H, long W, const void* Wt,
                          const float* bias, const float* pos, const float* cls, long D, float* out, void* stream);

@@ -365,6 +365,38 @@ def test_linear_resid_ln_fused(M, K, scale):
     assert _rel(y.float(), yr) < 4e-3
 
 
+@pytest.mark.parametrize("M,K,xs", [(36008, 1536, True), (300, 1152, False), (1, 64, True), (145, 128, False)])
+def test_linear_dgrad_ln_bwd_fused(M, K, xs):
+    """ivit_linear_dgrad_ln_bwd (fc1 / qkv dgrad with the norm2 / norm1 backward in the epilogue)
+    vs torch autograd in f64 of LayerNorm(x) fed by the same bf16 dgrad product."""
+    import ops
+    g = torch.Generator().manual_seed(3 * M + K)
+    N = 384
+    dy = torch.randn(M, K, generator=g).to(torch.bfloat16)
+    w = torch.randn(K, N, generator=g) / math.sqrt(K)
+    x = torch.randn(M, N, generator=g) * 2 + 0.5
+    gm, bt = 1 + 0.1 * torch.randn(N, generator=g), 0.1 * torch.randn(N, generator=g)
+    dres = torch.randn(M, N, generator=g)
+    sc = torch.rand(M // 5 + 1, generator=g) + 0.5
+    mu = x.double().mean(1)
+    rs = 1 / torch.sqrt(((x.double() - mu[:, None]) ** 2).mean(1) + 1e-6)
+    dx, dxs, dg, db = ops.linear_dgrad_ln_bwd(dy.to(DEV), w.to(DEV), x.to(DEV), gm.to(DEV), mu.float().to(DEV),
+                                              rs.float().to(DEV), dres=dres.to(DEV).clone(),
+                                              xs_dtype=torch.bfloat16 if xs else None,
+                                              row_scale=sc.to(DEV) if xs else None, rps=5)
+    G = dy.double() @ w.to(torch.bfloat16).double()
+    xr = x.double().requires_grad_(True)
+    gr, br = gm.double().requires_grad_(True), bt.double().requires_grad_(True)
+    y = torch.nn.functional.layer_norm(xr, (N,), gr, br, 1e-6)
+    y.backward(G)
+    ref = xr.grad + dres.double()
+    assert (dx.double().cpu() - ref).abs().max().item() < 1e-4 * ref.abs().max().item()
+    assert _rel(dg, gr.grad) < 1e-4 and _rel(db, br.grad) < 1e-4
+    if xs:
+        r2 = ref * sc.double()[torch.arange(M) // 5][:, None]
+        assert _rel(dxs.float(), r2) < 4e-3
+
+
 def test_patch_im2col_bitexact():
     """bf16 patch matrix (the throughput path's GEMM operand) is exactly the rearranged, rounded raster."""
     from _lib import lib, ptr, stream

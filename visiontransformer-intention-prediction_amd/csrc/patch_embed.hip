@@ -222,6 +222,20 @@ __global__ __launch_bounds__(256) void patch_pack_kernel(const float* __restrict
   wp[i] = f32x8_to_bf16x8(*(const float4*)q, *(const float4*)(q + 4));
 }
 
+// W [K][N] f32 (a dgrad operand, e.g. fc1.weight [1536][384]) packed as its transpose [N][K].
+__global__ __launch_bounds__(256) void pack_t_kernel(const float* __restrict__ w, long K, long N, uint4* __restrict__ wp) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long NB16 = N / 16, total = (K / 32) * NB16 * 64;
+  if (i >= total) return;
+  const int lane = (int)(i & 63);
+  const long snb = i >> 6, s = snb / NB16, nb = snb - s * NB16;
+  const long n = nb * 16 + (lane & 15), k0 = s * 32 + 8 * (lane >> 4);
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = w[(k0 + e) * N + n];
+  wp[i] = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
+}
+
 __global__ void patch_cls_kernel(float* out, long B, long Ntok, long D, const float* cls, const float* pos) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * D) return;
@@ -241,6 +255,14 @@ extern "C" int ivit_patch_weight_pack(const float* w, long D, long C, void* wpac
   const long K = C * 64, n = (K / 32) * (D / 16) * 64;
   hipLaunchKernelGGL(patch_pack_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), w, D, K,
                      (uint4*)wpack);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_weight_pack_t(const float* w, long K, long N, void* wpack, void* stream) {
+  IVIT_CHECK_ARG(N > 0 && N % 16 == 0 && K > 0 && K % 32 == 0, "ivit_weight_pack_t: N % 16, K % 32 must be 0");
+  const long n = (K / 32) * (N / 16) * 64;
+  hipLaunchKernelGGL(pack_t_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), w, K, N, (uint4*)wpack);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -28,11 +28,18 @@ constexpr int RP_TLD = RP_N + 4;           // epilogue row stride (floats)
 
 IVIT_DEV int rp_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
-__global__ __launch_bounds__(512, 1) void rowpanel_resid_ln_kernel(
+// Backward form (BWD = true): the GEMM is the LayerNorm input's dgrad, dY[m][n] = sum_k A[m][k] W[k][n]
+// (W packed transposed), and the epilogue is the LayerNorm backward of timm's norm:
+//   xh = (X - mean) rstd,  g = dY gamma,  dX = dres + rstd (g - mean_n(g) - xh mean_n(g xh)),
+//   dXs = bf16(dX * scale[m / rps]) (optional), per-workgroup partial column sums of dY xh / dY.
+// Pointer roles in BWD: R = dres (nullable), X = X (read), Y = dXs, mean / rstd read, bias unused,
+// part = [gridDim.x][2][384] partials (reduced by colreduce_kernel).
+template <bool BWD>
+__global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
     const bf16* __restrict__ A, long lda, int M, int K, const u32x4* __restrict__ wpack,
-    const float* __restrict__ bias, const float* __restrict__ R, long ldr, const float* __restrict__ scale, int rps,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* __restrict__ X, long ldx,
-    bf16* __restrict__ Y, long ldy, float* __restrict__ mean, float* __restrict__ rstd) {
+    const float* __restrict__ bias, const float* R, long ldr, const float* __restrict__ scale, int rps,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* X, long ldx,
+    bf16* __restrict__ Y, long ldy, float* mean, float* rstd, float* dX, long lddx, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) char smem[RP_NS * RP_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -123,22 +130,41 @@ __global__ __launch_bounds__(512, 1) void rowpanel_resid_ln_kernel(
   float* T = (float*)smem;       // [16][RP_TLD]
   float bv[NBW];
 #pragma unroll
-  for (int j = 0; j < NBW; ++j) bv[j] = bias ? bias[(wv * NBW + j) * 16 + (lane & 15)] : 0.f;
+  for (int j = 0; j < NBW; ++j) bv[j] = (!BWD && bias) ? bias[(wv * NBW + j) * 16 + (lane & 15)] : 0.f;
   const int r = tid >> 5, c0 = (tid & 31) * 12;  // row phase: 32 lanes per row, 12 columns each
   float gm[12], bt[12];
 #pragma unroll
-  for (int e = 0; e < 12; ++e) { gm[e] = gamma[c0 + e]; bt[e] = beta[c0 + e]; }
-  // residual rows of block mb + 1 are loaded while block mb is reduced
-  auto load_res = [&](int mb, float4 (&rv)[3], float& s) {
+  for (int e = 0; e < 12; ++e) { gm[e] = gamma[c0 + e]; bt[e] = BWD ? 0.f : beta[c0 + e]; }
+  // row operands of block mb + 1 (residual; or X and dres) are loaded while block mb is reduced
+  struct RowIn { float4 a[3], b[3]; float s, mu, rs; };
+  auto load_row = [&](int mb, RowIn& in) {
     const int m = min(m0 + 16 * mb + r, M - 1);
-    const float* rrow = R + (long)m * ldr + c0;
+    in.s = scale ? scale[m / rps] : 1.f;
+    if constexpr (!BWD) {
+      const float* rrow = R + (long)m * ldr + c0;
 #pragma unroll
-    for (int e = 0; e < 3; ++e) rv[e] = *(const float4*)(rrow + 4 * e);
-    s = scale ? scale[m / rps] : 1.f;
+      for (int e = 0; e < 3; ++e) in.a[e] = *(const float4*)(rrow + 4 * e);
+    } else {
+      const float* xrow = X + (long)m * ldx + c0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) in.a[e] = *(const float4*)(xrow + 4 * e);
+      if (R) {
+        const float* drow = R + (long)m * ldr + c0;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) in.b[e] = *(const float4*)(drow + 4 * e);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) in.b[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      in.mu = mean[m];
+      in.rs = rstd[m];
+    }
   };
-  float4 rv[3];
-  float sc;
-  load_res(0, rv, sc);
+  float pg[12], pb[12];  // BWD: this thread's partial column sums of dY xh, dY
+#pragma unroll
+  for (int e = 0; e < 12; ++e) { pg[e] = 0.f; pb[e] = 0.f; }
+  RowIn in;
+  load_row(0, in);
 #pragma unroll
   for (int mb = 0; mb < RP_MB; ++mb) {
 #pragma unroll
@@ -149,41 +175,106 @@ __global__ __launch_bounds__(512, 1) void rowpanel_resid_ln_kernel(
     __builtin_amdgcn_s_barrier();
     const int m = m0 + 16 * mb + r;
     const bool ok = m < M;
-    float x[12];
+    float t[12], u[12];
 #pragma unroll
     for (int e = 0; e < 12; e += 4) {
       const float4 tv = *(const float4*)(T + r * RP_TLD + c0 + e);
-      const float4 q = rv[e / 4];
-      x[e] = q.x + sc * tv.x; x[e + 1] = q.y + sc * tv.y; x[e + 2] = q.z + sc * tv.z; x[e + 3] = q.w + sc * tv.w;
+      t[e] = tv.x; t[e + 1] = tv.y; t[e + 2] = tv.z; t[e + 3] = tv.w;
+      const float4 q = in.a[e / 4];
+      u[e] = q.x; u[e + 1] = q.y; u[e + 2] = q.z; u[e + 3] = q.w;
     }
-    if (mb + 1 < RP_MB) load_res(mb + 1, rv, sc);
-    float sum = 0.f;
+    if constexpr (!BWD) {
+      const float sc = in.s;
+      float x[12];
 #pragma unroll
-    for (int e = 0; e < 12; ++e) sum += x[e];
+      for (int e = 0; e < 12; ++e) x[e] = u[e] + sc * t[e];
+      if (mb + 1 < RP_MB) load_row(mb + 1, in);
+      float sum = 0.f;
 #pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
-    const float mu = sum * (1.f / RP_N);
-    float sq = 0.f;
+      for (int e = 0; e < 12; ++e) sum += x[e];
 #pragma unroll
-    for (int e = 0; e < 12; ++e) { const float d = x[e] - mu; sq += d * d; }
+      for (int o = 16; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+      const float mu = sum * (1.f / RP_N);
+      float sq = 0.f;
 #pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) sq += __shfl_xor(sq, o, 64);
-    const float rs = rsqrtf(sq * (1.f / RP_N) + eps);
-    if (ok) {
-      float* xrow = X + (long)m * ldx + c0;
+      for (int e = 0; e < 12; ++e) { const float d = x[e] - mu; sq += d * d; }
 #pragma unroll
-      for (int e = 0; e < 12; e += 4) *(float4*)(xrow + e) = make_float4(x[e], x[e + 1], x[e + 2], x[e + 3]);
-      unsigned pk[6];
+      for (int o = 16; o >= 1; o >>= 1) sq += __shfl_xor(sq, o, 64);
+      const float rs = rsqrtf(sq * (1.f / RP_N) + eps);
+      if (ok) {
+        float* xrow = X + (long)m * ldx + c0;
 #pragma unroll
-      for (int e = 0; e < 12; e += 2)
-        pk[e / 2] = pk_bf16((x[e] - mu) * rs * gm[e] + bt[e], (x[e + 1] - mu) * rs * gm[e + 1] + bt[e + 1]);
-      bf16* yrow = Y + (long)m * ldy + c0;
-      *(uint2*)yrow = make_uint2(pk[0], pk[1]);
-      *(uint2*)(yrow + 4) = make_uint2(pk[2], pk[3]);
-      *(uint2*)(yrow + 8) = make_uint2(pk[4], pk[5]);
-      if ((tid & 31) == 0) { mean[m] = mu; rstd[m] = rs; }
+        for (int e = 0; e < 12; e += 4) *(float4*)(xrow + e) = make_float4(x[e], x[e + 1], x[e + 2], x[e + 3]);
+        unsigned pk[6];
+#pragma unroll
+        for (int e = 0; e < 12; e += 2)
+          pk[e / 2] = pk_bf16((x[e] - mu) * rs * gm[e] + bt[e], (x[e + 1] - mu) * rs * gm[e + 1] + bt[e + 1]);
+        bf16* yrow = Y + (long)m * ldy + c0;
+        *(uint2*)yrow = make_uint2(pk[0], pk[1]);
+        *(uint2*)(yrow + 4) = make_uint2(pk[2], pk[3]);
+        *(uint2*)(yrow + 8) = make_uint2(pk[4], pk[5]);
+        if ((tid & 31) == 0) { mean[m] = mu; rstd[m] = rs; }
+      }
+    } else {
+      const float mu = in.mu, rs = in.rs, sc = in.s;
+      float dr[12];
+#pragma unroll
+      for (int e = 0; e < 12; e += 4) {
+        const float4 q = in.b[e / 4];
+        dr[e] = q.x; dr[e + 1] = q.y; dr[e + 2] = q.z; dr[e + 3] = q.w;
+      }
+      if (mb + 1 < RP_MB) load_row(mb + 1, in);
+      float xh[12], gy[12], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 12; ++e) {
+        xh[e] = (u[e] - mu) * rs;
+        gy[e] = t[e] * gm[e];
+        s1 += gy[e];
+        s2 += gy[e] * xh[e];
+      }
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+      s1 *= 1.f / RP_N;
+      s2 *= 1.f / RP_N;
+      if (ok) {
+        float o[12];
+#pragma unroll
+        for (int e = 0; e < 12; ++e) {
+          o[e] = rs * (gy[e] - s1 - xh[e] * s2) + dr[e];
+          pg[e] += t[e] * xh[e];
+          pb[e] += t[e];
+        }
+        float* drow = dX + (long)m * lddx + c0;
+#pragma unroll
+        for (int e = 0; e < 12; e += 4) *(float4*)(drow + e) = make_float4(o[e], o[e + 1], o[e + 2], o[e + 3]);
+        if (Y) {
+          unsigned pk[6];
+#pragma unroll
+          for (int e = 0; e < 12; e += 2) pk[e / 2] = pk_bf16(o[e] * sc, o[e + 1] * sc);
+          bf16* yrow = Y + (long)m * ldy + c0;
+          *(uint2*)yrow = make_uint2(pk[0], pk[1]);
+          *(uint2*)(yrow + 4) = make_uint2(pk[2], pk[3]);
+          *(uint2*)(yrow + 8) = make_uint2(pk[4], pk[5]);
+        }
+      }
     }
     __builtin_amdgcn_s_barrier();  // T is rewritten by the next block
+  }
+  if constexpr (BWD) {
+    // column partials of the 16 row slots -> one [2][384] partial row per workgroup
+    float* red = (float*)smem;  // [16][2][384]
+#pragma unroll
+    for (int e = 0; e < 12; ++e) {
+      red[(r * 2 + 0) * RP_N + c0 + e] = pg[e];
+      red[(r * 2 + 1) * RP_N + c0 + e] = pb[e];
+    }
+    __builtin_amdgcn_s_barrier();
+    for (int c = tid; c < 2 * RP_N; c += 512) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a += red[k * 2 * RP_N + c];
+      part[(long)blockIdx.x * 2 * RP_N + c] = a;
+    }
   }
 }
 
@@ -205,9 +296,37 @@ extern "C" int ivit_linear_resid_ln_fwd(const void* A, long lda, long M, long N,
   IVIT_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)wpack & 15) == 0 && ((uintptr_t)R & 15) == 0 &&
                      ((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 7) == 0,
                  "ivit_linear_resid_ln_fwd: misaligned operand");
-  hipLaunchKernelGGL(rowpanel_resid_ln_kernel, dim3(ivit_cdiv(M, RP_MT)), dim3(512), 0, ivit_stream(stream),
+  hipLaunchKernelGGL(rowpanel_ln_kernel<false>, dim3(ivit_cdiv(M, RP_MT)), dim3(512), 0, ivit_stream(stream),
                      (const bf16*)A, lda, (int)M, (int)K, (const u32x4*)wpack, bias, R, ldr, scale, (int)rps, gamma,
-                     beta, eps, X, ldx, (bf16*)Y, ldy, mean, rstd);
+                     beta, eps, X, ldx, (bf16*)Y, ldy, mean, rstd, nullptr, 0L, nullptr);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" long ivit_linear_dgrad_ln_bwd_workspace(long M, long N) { return (long)ivit_cdiv(M, RP_MT) * 2 * N * 4; }
+
+extern "C" int ivit_linear_dgrad_ln_bwd(const void* dY, long lddy, long M, long N, long K, const void* wpack_t,
+                                        const float* X, long ldx, const float* gamma, const float* mean,
+                                        const float* rstd, const float* dres, long ldr, float* dX, long lddx,
+                                        void* dXs, const float* scale, long rps, float* dgamma, float* dbeta,
+                                        int accumulate, void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(N == RP_N, "ivit_linear_dgrad_ln_bwd: N must be %d (got %ld)", RP_N, N);
+  IVIT_CHECK_ARG(M > 0 && K > 0 && K % 64 == 0, "ivit_linear_dgrad_ln_bwd: K must be a positive multiple of 64");
+  IVIT_CHECK_ARG(lddy >= K && lddy % 8 == 0 && ldx >= N && ldx % 4 == 0 && lddx >= N && lddx % 4 == 0 &&
+                     (!dres || (ldr >= N && ldr % 4 == 0)) && rps > 0,
+                 "ivit_linear_dgrad_ln_bwd: bad leading dimensions");
+  IVIT_CHECK_ARG(RP_MT * lddy * 2 < (1L << 32) && M < (1L << 31), "ivit_linear_dgrad_ln_bwd: too large");
+  IVIT_CHECK_ARG(work_bytes >= ivit_linear_dgrad_ln_bwd_workspace(M, N), "ivit_linear_dgrad_ln_bwd: workspace too small");
+  IVIT_CHECK_ARG(((uintptr_t)dY & 15) == 0 && ((uintptr_t)wpack_t & 15) == 0 && ((uintptr_t)X & 15) == 0 &&
+                     ((uintptr_t)dX & 15) == 0 && ((uintptr_t)dres & 15) == 0 && ((uintptr_t)dXs & 7) == 0,
+                 "ivit_linear_dgrad_ln_bwd: misaligned operand");
+  hipStream_t st = ivit_stream(stream);
+  const int nb = ivit_cdiv(M, RP_MT);
+  hipLaunchKernelGGL(rowpanel_ln_kernel<true>, dim3(nb), dim3(512), 0, st, (const bf16*)dY, lddy, (int)M, (int)K,
+                     (const u32x4*)wpack_t, nullptr, dres, ldr, scale, (int)rps, gamma, nullptr, 0.f,
+                     (float*)X, ldx, (bf16*)dXs, (long)RP_N, (float*)mean, (float*)rstd, dX, lddx, (float*)work);
+  IVIT_LAUNCH_CHECK();
+  launch_colreduce(st, (const float*)work, nb, 2 * N, (int)(2 * N), dgamma, (int)N, dbeta, accumulate);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -67,6 +67,22 @@ def packed_weight(w):
     return wp
 
 
+_PACKED_T = WeakIdKeyDictionary()
+
+
+def packed_weight_t(w):
+    """A [K, N] weight used as a dgrad operand (fc1 / qkv weights [out, in] with in = N) packed as
+    its transpose in the row-panel fragment order, cached per parameter version."""
+    e = _PACKED_T.get(w)
+    if e is not None and e[0] == w._version:
+        return e[1]
+    K, N = w.shape
+    wp = torch.empty(lib.ivit_patch_weight_pack_bytes(N, K // 64) // 2, dtype=torch.bfloat16, device=w.device)
+    lib.ivit_weight_pack_t(ptr(w.float().contiguous()), K, N, ptr(wp), stream())
+    _PACKED_T[w] = (w._version, wp)
+    return wp
+
+
 def shadow_of(p):
     """The live bf16 shadow of parameter p (None if there is none or it is stale)."""
     e = _SHADOWS.get(p)
@@ -140,6 +156,25 @@ def linear_resid_ln_fwd(a, w, b, resid, row_scale, rps, g, beta, eps):
                                  resid.stride(0), ptr(row_scale), rps, ptr(g), ptr(beta), eps, ptr(x), N, ptr(y), N,
                                  ptr(mean), ptr(rstd), stream())
     return x, y, mean, rstd
+
+
+def linear_dgrad_ln_bwd(dy, w, x, g, mean, rstd, dres=None, dx=None, xs_dtype=None, row_scale=None, rps=1):
+    """dgrad G = dy [M, K] (bf16) @ w [K, 384] with the LayerNorm backward of (x, g, mean, rstd) in
+    the epilogue: dx = dres + LN_bwd(G) (f32, may alias dres), optional bf16 dxs = dx * row_scale,
+    dgamma, dbeta — one kernel + the column reduction (ivit_linear_dgrad_ln_bwd)."""
+    M, K = dy.shape
+    N = w.shape[1]
+    if dx is None:
+        dx = torch.empty((M, N), dtype=torch.float32, device=dy.device) if dres is None else dres
+    dxs = torch.empty((M, N), dtype=xs_dtype, device=dy.device) if xs_dtype is not None else None
+    dg = torch.empty((N,), dtype=torch.float32, device=dy.device)
+    db = torch.empty((N,), dtype=torch.float32, device=dy.device)
+    ws = workspace(lib.ivit_linear_dgrad_ln_bwd_workspace(M, N), dy.device)
+    lib.ivit_linear_dgrad_ln_bwd(ptr(dy), dy.stride(0), M, N, K, ptr(packed_weight_t(w)), ptr(x), x.stride(0), ptr(g),
+                                 ptr(mean), ptr(rstd), ptr(dres), dres.stride(0) if dres is not None else N, ptr(dx),
+                                 dx.stride(0), ptr(dxs), ptr(row_scale), rps, ptr(dg), ptr(db), 0, ptr(ws),
+                                 ws.numel(), stream())
+    return dx, dxs, dg, db
 
 
 def layernorm_bwd(x, g, mean, rstd, dy, dres=None, dx=None, xs_dtype=None, row_scale=None, rps=1, rowmap=(0, 0, 0)):
@@ -435,25 +470,21 @@ class ViTBlockFn(torch.autograd.Function):
 
     bf16 row-panel fusion (D = 384): the proj GEMM's epilogue also applies norm2, and — when
     the NEXT block's norm1 parameters are passed (nxw, nxb) — the fc2 GEMM's epilogue applies
-    that norm1 too and returns it as the second output; the next block then takes it as `ln_in`
-    (and skips its own norm1), and this block's backward owns that LayerNorm's backward (its
-    input gradient joins dx2; its parameter gradients are returned for nxw, nxb). The norm1
-    output is bf16 but its gradient is f32 (as in the unfused block), so the gradient does not
-    travel through autograd (which would cast it to the output's dtype): the output carries a
-    small holder the next block's backward fills, and the output itself is non-differentiable.
-    This block's backward runs after the next one's (it needs dx2 from it), so the holder is
-    filled by then. Without fusion the second output is an empty tensor."""
+    that norm1 too and returns (y, mean, rstd) as extra, non-differentiable outputs. The next
+    block takes them as (ln_in, m_in, r_in) instead of running its norm1 and still does that
+    LayerNorm's backward itself (from its input x and the handed-over statistics), exactly as
+    in the unfused block. Without fusion the extra outputs are empty tensors."""
 
     @staticmethod
-    def forward(ctx, x, ln_in, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, nxw, nxb, s1, s2, meta):
+    def forward(ctx, x, ln_in, m_in, r_in, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, nxw, nxb,
+                s1, s2, meta):
         B, N, H, cdt, eps = meta
         cd = tdtype(cdt)
         wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
-        own_ln1 = ln_in is None
-        if own_ln1:
+        if ln_in is None:
             ln1, m1, r1 = layernorm_fwd(x, n1w, n1b, eps, cd)
         else:
-            ln1, m1, r1 = ln_in, None, None
+            ln1, m1, r1 = ln_in, m_in, r_in
         q2 = cdt == BF16
         panel = q2 and x.shape[1] == 384
         if q2:
@@ -470,65 +501,57 @@ class ViTBlockFn(torch.autograd.Function):
         # inference (torch.inference_mode): nothing is saved, and fc1 skips its pre-activation copy
         infer = torch.is_inference_mode_enabled()
         a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=not infer)
-        nx = nxw is not None and panel
-        if nx:
+        if nxw is not None and panel:
             x2, lnx, mx, rx = linear_resid_ln_fwd(a, f2w, f2b, x1, s2, N, nxw, nxb, eps)
         else:
             x2, _ = linear_fwd(a, w2, f2b, cdt, resid=x1, row_scale=s2, rps=N)
-            lnx, mx, rx = x2.new_empty(0), None, None
-        ctx.mark_non_differentiable(lnx)
-        ctx.carrier = {}
-        if nx:
-            lnx._ivit_grad_carrier = ctx.carrier
-        ctx.in_carrier = None if own_ln1 else getattr(ln_in, "_ivit_grad_carrier", None)
+            lnx = mx = rx = x2.new_empty(0)
+        ctx.mark_non_differentiable(lnx, mx, rx)
         if infer:
             ctx.meta, ctx.q2 = meta, q2
-            return x2, lnx
+            return x2, lnx, mx, rx
         ctx.save_for_backward(x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2,
-                              x2 if nx else None, nxw if nx else None, mx, rx)
+                              qkvw, f1w)
         ctx.meta = meta
         ctx.q2 = q2
-        ctx.own_ln1, ctx.nx = own_ln1, nx
-        return x2, lnx
+        ctx.panel = panel
+        return x2, lnx, mx, rx
 
     @staticmethod
-    def backward(ctx, dx2, _unused):
-        (x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2,
-         x2, nxw, mx, rx) = ctx.saved_tensors
+    def backward(ctx, dx2, *_unused):
+        (x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2, qkvw,
+         f1w) = ctx.saved_tensors
         B, N, H, cdt, eps = ctx.meta
         cd = tdtype(cdt)
         dx2 = dx2.contiguous()
         D = x.shape[1]
-        dnxw = dnxb = None
-        dlnx = ctx.carrier.pop("dln", None)
-        if ctx.nx and dlnx is not None:  # the next block's norm1 ran in our fc2 epilogue: its backward is ours
-            dx2, _, dnxw, dnxb = layernorm_bwd(x2, nxw, mx, rx, dlnx, dres=dx2, dx=torch.empty_like(dx2))
         # The weight gradients are off the critical path: they run on a forked stream and
         # overlap the dgrad chain (notably the attention backward); joined before returning.
         fork = _WgradFork(dx2.device) if dx2.is_cuda and WGRAD_FORK else None
         dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
         dh = linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
         g2 = _wgrad(fork, dx2s, a, cdt)
-        dln2 = linear_dgrad(dh, w1, cdt, torch.float32)
+        if ctx.panel:  # fc1 dgrad with norm2's backward in the epilogue
+            dx1, dx1s, dg2, dbe2 = linear_dgrad_ln_bwd(dh, f1w, x1, n2w, m2, r2, dres=dx2, dx=torch.empty_like(dx2),
+                                                       xs_dtype=cd, row_scale=s1, rps=N)
+        else:
+            dln2 = linear_dgrad(dh, w1, cdt, torch.float32)
+            dx1, dx1s, dg2, dbe2 = layernorm_bwd(x1, n2w, m2, r2, dln2, dres=dx2, dx=torch.empty_like(dx2),
+                                                 xs_dtype=cd, row_scale=s1, rps=N)
         g1 = _wgrad(fork, dh, ln2, cdt)
-        dx1, dx1s, dg2, dbe2 = layernorm_bwd(x1, n2w, m2, r2, dln2, dres=dx2, dx=torch.empty_like(dx2), xs_dtype=cd,
-                                             row_scale=s1, rps=N)
         do = linear_dgrad(dx1s, wp, cdt, cd)
         gp = _wgrad(fork, dx1s, o, cdt)
         dqkv = attn_bwd_q2(qkv, o, do, lse, B, N, H) if ctx.q2 else attn_bwd(qkv, o, do, lse, B, N, H, cdt)
-        dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
-        gq = _wgrad(fork, dqkv, ln1, cdt)
-        if ctx.own_ln1:
+        if ctx.panel:  # qkv dgrad with norm1's backward in the epilogue
+            dx0, _, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1)
+        else:
+            dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
             dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
-            dln_in = None
-        else:  # norm1 ran in the previous block, which takes dln1 (f32) and does its backward
-            dx0, dg1, dbe1, dln_in = dx1, None, None, None
-            if ctx.in_carrier is not None:
-                ctx.in_carrier["dln"] = dln1
+        gq = _wgrad(fork, dqkv, ln1, cdt)
         if fork is not None:
             fork.join((dx2s, dh, dx1s, dqkv, a, ln2, o, ln1))
         (dW2, db2), (dW1, db1), (dWp, dbp), (dWq, dbq) = g2, g1, gp, gq
-        return (dx0, dln_in, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, dnxw, dnxb,
+        return (dx0, None, None, None, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, None, None,
                 None, None, None)
 
 

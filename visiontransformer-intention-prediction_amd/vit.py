@@ -76,16 +76,19 @@ class Block(nn.Module):
         return self.last_scales
 
     def forward_flat(self, x, B, N, cdt, ln_in=None, next_norm=None):
-        """-> (x_out, next norm1 output or an empty tensor): `ln_in` is this block's norm1 output
-        computed by the previous block's fc2 epilogue; `next_norm` the next block's norm1, whose
-        forward this block's fc2 epilogue runs (ops.ViTBlockFn, bf16 row-panel path)."""
+        """-> (x_out, (y, mean, rstd) of the next block's norm1 or empty tensors): `ln_in` is
+        this block's (y, mean, rstd) of norm1 computed by the previous block's fc2 epilogue;
+        `next_norm` the next block's norm1, whose forward this block's fc2 epilogue runs
+        (ops.ViTBlockFn, bf16 row-panel path)."""
         s1, s2 = self._scales(B, x.device)
         nxw = next_norm.weight if next_norm is not None else None
         nxb = next_norm.bias if next_norm is not None else None
-        return ops.ViTBlockFn.apply(x, ln_in, self.norm1.weight, self.norm1.bias, self.attn.qkv.weight,
+        li, mi, ri = ln_in if ln_in is not None else (None, None, None)
+        out = ops.ViTBlockFn.apply(x, li, mi, ri, self.norm1.weight, self.norm1.bias, self.attn.qkv.weight,
                                     self.attn.qkv.bias, self.attn.proj.weight, self.attn.proj.bias, self.norm2.weight,
                                     self.norm2.bias, self.mlp.fc1.weight, self.mlp.fc1.bias, self.mlp.fc2.weight,
                                     self.mlp.fc2.bias, nxw, nxb, s1, s2, (B, N, self.attn.num_heads, cdt, 1e-6))
+        return out[0], tuple(out[1:])
 
     def forward(self, x):
         B, N, D = x.shape
@@ -133,8 +136,8 @@ class VisionTransformer(nn.Module):
         ln = None
         for i, blk in enumerate(self.blocks):
             nxt = self.blocks[i + 1].norm1 if fuse and i + 1 < len(self.blocks) else None
-            t, lnx = blk.forward_flat(t, B, N, cdt, ln_in=ln, next_norm=nxt)
-            ln = lnx if nxt is not None else None
+            t, nxt_ln = blk.forward_flat(t, B, N, cdt, ln_in=ln, next_norm=nxt)
+            ln = nxt_ln if nxt is not None else None
         return t
 
     def forward_features(self, x):
