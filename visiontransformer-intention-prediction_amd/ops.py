@@ -507,6 +507,7 @@ class ViTBlockFn(torch.autograd.Function):
             x2, _ = linear_fwd(a, w2, f2b, cdt, resid=x1, row_scale=s2, rps=N)
             lnx = mx = rx = x2.new_empty(0)
         ctx.mark_non_differentiable(lnx, mx, rx)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the three extra outputs
         if infer:
             ctx.meta, ctx.q2 = meta, q2
             return x2, lnx, mx, rx
@@ -523,7 +524,7 @@ class ViTBlockFn(torch.autograd.Function):
          f1w) = ctx.saved_tensors
         B, N, H, cdt, eps = ctx.meta
         cd = tdtype(cdt)
-        dx2 = dx2.contiguous()
+        dx2 = torch.zeros_like(x) if dx2 is None else dx2.contiguous()
         D = x.shape[1]
         # The weight gradients are off the critical path: they run on a forked stream and
         # overlap the dgrad chain (notably the attention backward); joined before returning.
@@ -699,7 +700,8 @@ class NeckFn(torch.autograd.Function):
             G[f"adapter_{s}.1.weight"], G[f"adapter_{s}.1.bias"] = linear_wgrad(dp, z, cdt)
             dy, _, G[f"adapter_{s}.0.weight"], G[f"adapter_{s}.0.bias"] = layernorm_bwd(
                 y, P[f"adapter_{s}.0.weight"], ma, ra, dz)
-            dt_ = torch.zeros_like(t)
+            dt_ = torch.empty_like(t)
+            dt_.view(B, Np + 1, -1)[:, 0].zero_()  # CLS rows: the neck drops them (no gradient)
             _, _, G[f"vit_{s}.norm.weight"], G[f"vit_{s}.norm.bias"] = layernorm_bwd(
                 t, P[f"vit_{s}.norm.weight"], mf, rf, dy, dx=dt_, rowmap=(Np, Np + 1, 1))
             outs[s] = dt_
@@ -731,6 +733,7 @@ class DetLossFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.shape = (B, NA, K)
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
         loss = stats[5:6].clone().reshape(())
         return loss, stats
 
@@ -739,6 +742,8 @@ class DetLossFn(torch.autograd.Function):
         cls, box, intent, keep, stats, ws = ctx.saved_tensors
         B, NA, K = ctx.shape
         cfg = ctx.cfg
+        if gloss is None:
+            return None, None, None, None, None, None, None, None, None
         g = gloss.reshape(1).float().contiguous()
         dcls, dbox, dint = torch.empty_like(cls), torch.empty_like(box), torch.empty_like(intent)
         lib.ivit_det_loss_bwd(ptr(cls), ptr(box), ptr(intent), B, NA, K, ptr(keep), cfg["dominant_mask"],
