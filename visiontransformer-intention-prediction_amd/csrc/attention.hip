@@ -397,9 +397,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
     d = half_swap_sum(d);  // the other 32 of the 64 dims sit in lane ^ 32
     lse2 = qv ? lse[(long)z * N + q] * LOG2E : 1e30f;
     dlt = qv ? d : 0.f;
-    if (hl == 0 && q < Npad) {
-      lse2p[(long)z * Npad + q] = lse2;
-      deltap[(long)z * Npad + q] = dlt;
+    if (hl == 0 && q < Npad) {  // negated: the dK/dV kernel starts its MFMA chains from them
+      lse2p[(long)z * Npad + q] = -lse2;
+      deltap[(long)z * Npad + q] = -dlt;
     }
   } else {
     lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
@@ -459,13 +459,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
 
 // One dK/dV tile step: queries of the Q/dO images (rows past N are zero with lse2 = 1e30,
 // so P = 0 there and no mask is needed) against this wave's 32 keys.
+// NEG (prescaled-Q path): lrow / drow hold -lse2 / -delta, which start the S and dP MFMA chains
+// as their initial accumulators (16 query rows per register block, loaded straight from LDS):
+// P = exp2(acc) and dS = P * acc come out without the per-score FMA and subtraction.
+template <bool NEG>
 IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, const float* drow,
                        const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], f32x16& dk0, f32x16& dk1, f32x16& dv0,
                        f32x16& dv1, float c2, int lane) {
   const int hl = lane >> 5;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    f32x16 s = zero16(), dp = zero16();
+    f32x16 s, dp;
+    if constexpr (NEG) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j
+        const float4 l4 = *(const float4*)(lrow + 32 * t + 8 * g + 4 * hl);
+        const float4 d4 = *(const float4*)(drow + 32 * t + 8 * g + 4 * hl);
+        s[4 * g] = l4.x; s[4 * g + 1] = l4.y; s[4 * g + 2] = l4.z; s[4 * g + 3] = l4.w;
+        dp[4 * g] = d4.x; dp[4 * g + 1] = d4.y; dp[4 * g + 2] = d4.z; dp[4 * g + 3] = d4.w;
+      }
+    } else {
+      s = zero16();
+      dp = zero16();
+    }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const bf16x8 qa = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
@@ -473,18 +489,27 @@ IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, co
       s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
       dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[ks], dp, 0, 0, 0);
     }
-    // row constants read after the MFMA chains are issued (off the chains' critical path)
+    if constexpr (NEG) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j
-      const float4 l4 = *(const float4*)(lrow + 32 * t + 8 * g + 4 * hl);
-      const float4 d4 = *(const float4*)(drow + 32 * t + 8 * g + 4 * hl);
-      const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-      const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+      for (int r = 0; r < 16; ++r) {
+        const float p = fast_exp2(s[r]);
+        s[r] = p;           // P[q][key]
+        dp[r] = p * dp[r];  // dS[q][key]
+      }
+    } else {
+      // row constants read after the MFMA chains are issued (off the chains' critical path)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = fast_exp2(fmaf(s[4 * g + j], c2, -lv[j]));
-        s[4 * g + j] = p;                             // P[q][key]
-        dp[4 * g + j] = p * (dp[4 * g + j] - dv[j]);  // dS[q][key]
+      for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j
+        const float4 l4 = *(const float4*)(lrow + 32 * t + 8 * g + 4 * hl);
+        const float4 d4 = *(const float4*)(drow + 32 * t + 8 * g + 4 * hl);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = fast_exp2(fmaf(s[4 * g + j], c2, -lv[j]));
+          s[4 * g + j] = p;                             // P[q][key]
+          dp[4 * g + j] = p * (dp[4 * g + j] - dv[j]);  // dS[q][key]
+        }
       }
     }
 #pragma unroll
@@ -504,7 +529,8 @@ IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, co
   }
 }
 
-// dK/dV: 4 waves x 32 keys; Q, dO tiles and their lse2 / delta rows by LDS-DMA.
+// dK/dV: 4 waves x 32 keys; Q, dO tiles and their lse2 / delta rows by LDS-DMA (NEG: negated rows).
+template <bool NEG>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ lse2p,
@@ -562,7 +588,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
   auto step = [&](auto stage, int qt) {
     constexpr int S = decltype(stage)::value;
     if (qt + 1 < nt) issue(qt + 1, S ^ 1);
-    dkv_tile(smem[S][0], smem[S][1], srow[S][0], srow[S][1], kf, vf, dk0, dk1, dv0, dv1, c2, lane);
+    dkv_tile<NEG>(smem[S][0], smem[S][1], srow[S][0], srow[S][1], kf, vf, dk0, dk1, dv0, dv1, c2, lane);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
@@ -698,8 +724,8 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
                        (const bf16*)out, (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
     hipLaunchKernelGGL(attn_bwd_dq_v2_kernel<false>, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
                        deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
-    hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
-                       deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel<false>, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout,
+                       lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
     IVIT_LAUNCH_CHECK();
     return 0;
   }
@@ -777,12 +803,12 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   const long Npad = (N + AK - 1) / AK * AK;
   float* lse2p = (float*)work;
   float* deltap = lse2p + B * H * Npad;
-  // dQ also forms the row constants (lse2, delta) the dK/dV kernel reads: no rows kernel
+  // dQ also forms the row constants (-lse2, -delta) the dK/dV kernel reads: no rows kernel
   hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<true, true>), g, dim3(256), 0, st, (const bf16*)qkv,
                      (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, scale,
                      (const bf16*)out, lse);
-  hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p, deltap,
-                     (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, 0.69314718055994531f);
+  hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel<true>, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
+                     deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, 0.69314718055994531f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
