@@ -68,6 +68,16 @@ int ivit_linear_dgrad_ln_bwd(const void* dY, long lddy, long M, long N, long K, 
                              long ldx, const float* gamma, const float* mean, const float* rstd, const float* dres,
                              long ldr, float* dX, long lddx, void* dXs, const float* scale, long rps, float* dgamma,
                              float* dbeta, int accumulate, void* work, long work_bytes, void* stream);
+/* Row-panel forms of the wide token GEMMs (bf16, N a multiple of 384, K of 64): each workgroup
+ * writes 144 whole output rows, walking the N / 384 column chunks (timm Attention.qkv, Mlp.fc1).
+ *   act NONE: Y = (A W^T + bias), columns n < qcols times qscale (qkv with the Q block prescaled)
+ *   act GELU: Ypre = A W^T + bias (if non-null), Y = gelu(Ypre)   (W packed by ivit_patch_weight_pack) */
+int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, long K, const void* wpack, const float* bias,
+                          int act, long qcols, float qscale, void* Y, long ldy, void* Ypre, long ldpre, void* stream);
+/* dX[M,N] = (dY[M,K] W[K,N]) * gelu'(pre[M,N])  (Mlp.fc2 dgrad into fc1's pre-activation; W packed
+ * transposed by ivit_weight_pack_t), bf16. */
+int ivit_linear_dgrad_gelu_panel(const void* dY, long lddy, long M, long N, long K, const void* wpack_t,
+                                 const void* pre, long ldpre, void* dX, long lddx, void* stream);
 /* W [K][N] f32 -> the row-panel packed bf16 layout of W^T (ivit_patch_weight_pack_bytes(N, K / 64) bytes). */
 int ivit_weight_pack_t(const float* w, long K, long N, void* wpack, void* stream);
 /* ---- timm PatchEmbed (Conv2d k=s=8) + CLS concat + pos_embed (model_vit.py:64,71 → timm). */

@@ -397,6 +397,36 @@ def test_linear_dgrad_ln_bwd_fused(M, K, xs):
         assert _rel(dxs.float(), r2) < 4e-3
 
 
+@pytest.mark.parametrize("M,N,K,mode", [(36008, 1152, 384, "qs"), (36008, 1536, 384, "gelu"), (300, 768, 128, "gelu"),
+                                        (145, 1536, 384, "dgelu"), (36008, 1536, 384, "dgelu"), (1, 384, 64, "qs")])
+def test_panel_wide(M, N, K, mode):
+    """Row-panel wide GEMMs (ivit_linear_fwd_panel / ivit_linear_dgrad_gelu_panel) vs the generic
+    engine on the same bf16 operands (qkv with the prescaled Q block, fc1 + GELU + pre-activation,
+    fc2 dgrad x GELU'): equal up to f32 summation order and the bf16 rounding of the output."""
+    import ops
+    from _lib import ACT_GELU, BF16
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    if mode == "dgelu":
+        w = (torch.randn(K, N, generator=g) / math.sqrt(K)).to(DEV)
+        pre = torch.randn(M, N, generator=g).to(torch.bfloat16).to(DEV)
+        got = ops.panel_dgrad_gelu(x, w, pre)
+        ref = ops.linear_dgrad(x, w.to(torch.bfloat16), BF16, torch.bfloat16, gelu_pre=pre)
+        assert _rel(got.float(), ref.float()) < 8e-3
+        return
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    b = (0.1 * torch.randn(N, generator=g)).to(DEV)
+    wb = w.to(torch.bfloat16)
+    if mode == "qs":
+        got, _ = ops.panel_fwd(x, w, b, qcols=384, qscale=ops.Q2_SCALE)
+        ref = ops.qkv_fwd_q2(x, wb, b, 384)
+        assert _rel(got.float(), ref.float()) < 8e-3
+    else:
+        got, pre = ops.panel_fwd(x, w, b, act=ACT_GELU, want_pre=True)
+        ref, rpre = ops.linear_fwd(x, wb, b, BF16, act=ACT_GELU, want_pre=True)
+        assert _rel(pre.float(), rpre.float()) < 8e-3 and _rel(got.float(), ref.float()) < 8e-3
+
+
 def test_patch_im2col_bitexact():
     """bf16 patch matrix (the throughput path's GEMM operand) is exactly the rearranged, rounded raster."""
     from _lib import lib, ptr, stream

@@ -28,58 +28,53 @@ constexpr int RP_TLD = RP_N + 4;           // epilogue row stride (floats)
 
 IVIT_DEV int rp_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
-// Backward form (BWD = true): the GEMM is the LayerNorm input's dgrad, dY[m][n] = sum_k A[m][k] W[k][n]
-// (W packed transposed), and the epilogue is the LayerNorm backward of timm's norm:
-//   xh = (X - mean) rstd,  g = dY gamma,  dX = dres + rstd (g - mean_n(g) - xh mean_n(g xh)),
-//   dXs = bf16(dX * scale[m / rps]) (optional), per-workgroup partial column sums of dY xh / dY.
-// Pointer roles in BWD: R = dres (nullable), X = X (read), Y = dXs, mean / rstd read, bias unused,
-// part = [gridDim.x][2][384] partials (reduced by colreduce_kernel).
-template <bool BWD>
-__global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
-    const bf16* __restrict__ A, long lda, int M, int K, const u32x4* __restrict__ wpack,
-    const float* __restrict__ bias, const float* R, long ldr, const float* __restrict__ scale, int rps,
-    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* X, long ldx,
-    bf16* __restrict__ Y, long ldy, float* mean, float* rstd, float* dX, long lddx, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) char smem[RP_NS * RP_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * RP_MT;
-  const int KT = K / 64;
+// The streamed operand's per-lane LDS-DMA sources (row-panel-invariant): 18 pieces of 8 rows per
+// stage over 8 waves, the first two waves take three.
+struct PanelA {
+  const bf16* A0;
+  unsigned voff[3];
+  int npc, pc0;
+};
 
-  // A pieces per wave: 18 over 8 waves, the first two take three
+IVIT_DEV PanelA panel_a_setup(const bf16* A, long lda, int M, int m0, int wv, int lane) {
   constexpr int PW = 3, PREM = RP_PIECES % 8;
-  const int npc = wv < PREM ? PW : PW - 1;
-  const int pc0 = wv < PREM ? wv * PW : PREM * PW + (wv - PREM) * (PW - 1);
-  unsigned voff[PW];
+  PanelA p;
+  p.npc = wv < PREM ? PW : PW - 1;
+  p.pc0 = wv < PREM ? wv * PW : PREM * PW + (wv - PREM) * (PW - 1);
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
-    const int row = min(pc0 + i, RP_PIECES - 1) * 8 + (lane >> 3);
+    const int row = min(p.pc0 + i, RP_PIECES - 1) * 8 + (lane >> 3);
     const int c = (lane & 7) ^ ((row >> 1) & 7);  // stored chunk (lane & 7) holds source chunk c
     const int m = min(m0 + row, M - 1) - m0;      // rows past M are computed, never stored
-    voff[i] = (unsigned)(((long)m * lda + c * 8) * 2);
+    p.voff[i] = (unsigned)(((long)m * lda + c * 8) * 2);
   }
-  const bf16* A0 = A + (long)m0 * lda;
+  p.A0 = A + (long)m0 * lda;
+  return p;
+}
+
+// acc[9][3] = rows m0 .. m0+143 of A (K = 64 KT) times the 48 columns of 16-column blocks
+// nb0 .. nb0+2 of a packed weight with NB16 blocks in total.
+IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA& pa, const u32x4* wpack, int NB16,
+                             int nb0, int KT, int wv, int lane) {
   auto issue_a = [&](int kt) {
-    char* st = smem + (kt % RP_NS) * RP_STAGE + pc0 * 1024;
-    const char* sb = uniform_ptr(A0 + kt * 64);
+    char* st = smem + (kt % RP_NS) * RP_STAGE + pa.pc0 * 1024;
+    const char* sb = uniform_ptr(pa.A0 + kt * 64);
 #pragma unroll
-    for (int i = 0; i < PW; ++i)
-      if (i < npc) glds_s<false>(voff[i], sb, st + i * 1024);
+    for (int i = 0; i < 3; ++i)
+      if (i < pa.npc) glds_s<false>(pa.voff[i], sb, st + i * 1024);
   };
-  const int NB16 = RP_N / 16;
   const unsigned vb = lane * 16;
   auto issue_b = [&](int kt, u32x4 (&r)[2 * NBW]) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) load_wfrag(r, t, uniform_ptr(wpack + ((long)(2 * kt + t) * NB16 + wv * NBW) * 64), vb);
+    for (int t = 0; t < 2; ++t) load_wfrag(r, t, uniform_ptr(wpack + ((long)(2 * kt + t) * NB16 + nb0) * 64), vb);
   };
-
-  f32x4 acc[RP_MB][NBW];
 #pragma unroll
   for (int i = 0; i < RP_MB; ++i)
 #pragma unroll
     for (int j = 0; j < NBW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 breg[3][2 * NBW];
+  const int npc = pa.npc;
   // Issue order: A(kt) B(kt) ... with B(kt) between A(kt) and A(kt+1); iteration kt issues
   // B(kt+2) A(kt+3), and waits for A(kt), B(kt) with A(kt+1) B(kt+1) A(kt+2) still in flight.
   auto stage = [&](int kt, u32x4 (&cur)[2 * NBW], u32x4 (&nb2)[2 * NBW]) {
@@ -124,6 +119,28 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
     if (kt + 1 < KT) stage(kt + 1, breg[1], breg[0]);
     if (kt + 2 < KT) stage(kt + 2, breg[2], breg[1]);
   }
+}
+
+// Backward form (BWD = true): the GEMM is the LayerNorm input's dgrad, dY[m][n] = sum_k A[m][k] W[k][n]
+// (W packed transposed), and the epilogue is the LayerNorm backward of timm's norm:
+//   xh = (X - mean) rstd,  g = dY gamma,  dX = dres + rstd (g - mean_n(g) - xh mean_n(g xh)),
+//   dXs = bf16(dX * scale[m / rps]) (optional), per-workgroup partial column sums of dY xh / dY.
+// Pointer roles in BWD: R = dres (nullable), X = X (read), Y = dXs, mean / rstd read, bias unused,
+// part = [gridDim.x][2][384] partials (reduced by colreduce_kernel).
+template <bool BWD>
+__global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
+    const bf16* __restrict__ A, long lda, int M, int K, const u32x4* __restrict__ wpack,
+    const float* __restrict__ bias, const float* R, long ldr, const float* __restrict__ scale, int rps,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* X, long ldx,
+    bf16* __restrict__ Y, long ldy, float* mean, float* rstd, float* dX, long lddx, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[RP_NS * RP_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * RP_MT;
+
+  PanelA pa = panel_a_setup(A, lda, M, m0, wv, lane);
+  f32x4 acc[RP_MB][NBW];
+  panel_mainloop(acc, smem, pa, wpack, RP_N / 16, wv * NBW, K / 64, wv, lane);
 
   // ---- epilogue, one 16-row block at a time through LDS
   __builtin_amdgcn_s_barrier();  // every wave is done with the A ring
@@ -278,6 +295,104 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
   }
 }
 
+// ============================================================================= wide outputs
+// The same row panel for outputs wider than 384 columns (qkv 1152, fc1 1536, fc2's dgrad 1536):
+// the workgroup walks the N / 384 column chunks, re-streaming its 144-row A panel (from L2) for
+// each, so every output row segment is written by one workgroup as whole rows.
+//   EPI_QS:     Y = bf16((acc + bias[n]) * (n < qcols ? qscale : 1))        (qkv, Q block prescaled)
+//   EPI_GELU:   P = bf16(acc + bias[n]), Y = bf16(gelu(acc + bias[n]))       (fc1 + pre-activation)
+//   EPI_DGELU:  Y = bf16(acc * gelu'(P[m][n]))                                (fc2 dgrad, W packed transposed)
+constexpr int EPI_QS = 0, EPI_GELU = 1, EPI_DGELU = 2;
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void rowpanel_wide_kernel(const bf16* __restrict__ A, long lda, int M, int K,
+                                                               const u32x4* __restrict__ wpack, int N,
+                                                               const float* __restrict__ bias, int qcols,
+                                                               float qscale, bf16* __restrict__ Y, long ldy,
+                                                               bf16* __restrict__ P, long ldp) {
+  __shared__ __attribute__((aligned(16))) char smem[RP_NS * RP_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * RP_MT;
+  const PanelA pa = panel_a_setup(A, lda, M, m0, wv, lane);
+  const int r = tid >> 5, c0 = (tid & 31) * 12;  // row phase: 32 lanes per row, 12 columns each
+  float* T = (float*)smem;                        // [16][RP_TLD] after the main loop
+#pragma unroll 1
+  for (int nc = 0; nc < N / RP_N; ++nc) {
+    f32x4 acc[RP_MB][NBW];
+    panel_mainloop(acc, smem, pa, wpack, N / 16, nc * (RP_N / 16) + wv * NBW, K / 64, wv, lane);
+    __builtin_amdgcn_s_barrier();  // every wave is done with the A ring
+    const int n0 = nc * RP_N;
+    float bv[NBW];
+#pragma unroll
+    for (int j = 0; j < NBW; ++j)
+      bv[j] = (EPI != EPI_DGELU && bias) ? bias[n0 + (wv * NBW + j) * 16 + (lane & 15)] : 0.f;
+    const float qs = (EPI == EPI_QS && n0 < qcols) ? qscale : 1.f;  // qcols is a multiple of 384
+    uint2 pv[3];
+    auto load_pre = [&](int mb) {
+      const int m = min(m0 + 16 * mb + r, M - 1);
+      const bf16* prow = P + (long)m * ldp + n0 + c0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) pv[e] = *(const uint2*)(prow + 4 * e);
+    };
+    if constexpr (EPI == EPI_DGELU) load_pre(0);
+#pragma unroll
+    for (int mb = 0; mb < RP_MB; ++mb) {
+#pragma unroll
+      for (int j = 0; j < NBW; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          T[(4 * (lane >> 4) + i) * RP_TLD + (wv * NBW + j) * 16 + (lane & 15)] = acc[mb][j][i] + bv[j];
+      __builtin_amdgcn_s_barrier();
+      const int m = m0 + 16 * mb + r;
+      float v[12];
+#pragma unroll
+      for (int e = 0; e < 12; e += 4) {
+        const float4 tv = *(const float4*)(T + r * RP_TLD + c0 + e);
+        v[e] = tv.x; v[e + 1] = tv.y; v[e + 2] = tv.z; v[e + 3] = tv.w;
+      }
+      float h[12];
+      if constexpr (EPI == EPI_DGELU) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          Pack4 q;
+          q.u = pv[e];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) h[4 * e + k] = (float)q.h[k];
+        }
+        if (mb + 1 < RP_MB) load_pre(mb + 1);
+      }
+      if (m < M) {
+        unsigned y[6], p[6];
+#pragma unroll
+        for (int e = 0; e < 12; e += 2) {
+          float a = v[e], b = v[e + 1];
+          if constexpr (EPI == EPI_QS) {
+            a *= qs; b *= qs;
+          } else if constexpr (EPI == EPI_GELU) {
+            p[e / 2] = pk_bf16(a, b);
+            a = gelu_t<bf16>(a); b = gelu_t<bf16>(b);
+          } else {
+            a *= gelu_grad_t<bf16>(h[e]); b *= gelu_grad_t<bf16>(h[e + 1]);
+          }
+          y[e / 2] = pk_bf16(a, b);
+        }
+        bf16* yrow = Y + (long)m * ldy + n0 + c0;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) *(uint2*)(yrow + 4 * e) = make_uint2(y[2 * e], y[2 * e + 1]);
+        if constexpr (EPI == EPI_GELU) {
+          if (P) {
+            bf16* prow = P + (long)m * ldp + n0 + c0;
+#pragma unroll
+            for (int e = 0; e < 3; ++e) *(uint2*)(prow + 4 * e) = make_uint2(p[2 * e], p[2 * e + 1]);
+          }
+        }
+      }
+      __builtin_amdgcn_s_barrier();  // T is rewritten by the next block (or the next chunk's ring)
+    }
+  }
+}
+
 }  // namespace
 }  // namespace ivit
 
@@ -327,6 +442,47 @@ extern "C" int ivit_linear_dgrad_ln_bwd(const void* dY, long lddy, long M, long 
                      (float*)X, ldx, (bf16*)dXs, (long)RP_N, (float*)mean, (float*)rstd, dX, lddx, (float*)work);
   IVIT_LAUNCH_CHECK();
   launch_colreduce(st, (const float*)work, nb, 2 * N, (int)(2 * N), dgamma, (int)N, dbeta, accumulate);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, long K, const void* wpack,
+                                     const float* bias, int act, long qcols, float qscale, void* Y, long ldy,
+                                     void* Ypre, long ldpre, void* stream) {
+  IVIT_CHECK_ARG(M > 0 && N > 0 && N % RP_N == 0 && K > 0 && K % 64 == 0 && qcols % RP_N == 0,
+                 "ivit_linear_fwd_panel: N and qcols must be multiples of %d, K of 64", RP_N);
+  IVIT_CHECK_ARG(act == IVIT_ACT_NONE || (act == IVIT_ACT_GELU && qcols == 0), "ivit_linear_fwd_panel: bad act");
+  IVIT_CHECK_ARG(lda >= K && lda % 8 == 0 && ldy >= N && ldy % 4 == 0 && (!Ypre || (ldpre >= N && ldpre % 4 == 0)),
+                 "ivit_linear_fwd_panel: bad leading dimensions");
+  IVIT_CHECK_ARG(RP_MT * lda * 2 < (1L << 32) && M < (1L << 31), "ivit_linear_fwd_panel: too large");
+  IVIT_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)wpack & 15) == 0 && ((uintptr_t)Y & 7) == 0 &&
+                     ((uintptr_t)Ypre & 7) == 0,
+                 "ivit_linear_fwd_panel: misaligned operand");
+  const dim3 g(ivit_cdiv(M, RP_MT));
+  hipStream_t st = ivit_stream(stream);
+  if (act == IVIT_ACT_GELU)
+    hipLaunchKernelGGL(rowpanel_wide_kernel<EPI_GELU>, g, dim3(512), 0, st, (const bf16*)A, lda, (int)M, (int)K,
+                       (const u32x4*)wpack, (int)N, bias, 0, 1.f, (bf16*)Y, ldy, (bf16*)Ypre, ldpre);
+  else
+    hipLaunchKernelGGL(rowpanel_wide_kernel<EPI_QS>, g, dim3(512), 0, st, (const bf16*)A, lda, (int)M, (int)K,
+                       (const u32x4*)wpack, (int)N, bias, (int)qcols, qscale, (bf16*)Y, ldy, nullptr, 0L);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_linear_dgrad_gelu_panel(const void* dY, long lddy, long M, long N, long K, const void* wpack_t,
+                                            const void* pre, long ldpre, void* dX, long lddx, void* stream) {
+  IVIT_CHECK_ARG(M > 0 && N > 0 && N % RP_N == 0 && K > 0 && K % 64 == 0,
+                 "ivit_linear_dgrad_gelu_panel: N must be a multiple of %d, K of 64", RP_N);
+  IVIT_CHECK_ARG(lddy >= K && lddy % 8 == 0 && lddx >= N && lddx % 4 == 0 && ldpre >= N && ldpre % 4 == 0,
+                 "ivit_linear_dgrad_gelu_panel: bad leading dimensions");
+  IVIT_CHECK_ARG(RP_MT * lddy * 2 < (1L << 32) && M < (1L << 31), "ivit_linear_dgrad_gelu_panel: too large");
+  IVIT_CHECK_ARG(((uintptr_t)dY & 15) == 0 && ((uintptr_t)wpack_t & 15) == 0 && ((uintptr_t)dX & 7) == 0 &&
+                     ((uintptr_t)pre & 7) == 0,
+                 "ivit_linear_dgrad_gelu_panel: misaligned operand");
+  hipLaunchKernelGGL(rowpanel_wide_kernel<EPI_DGELU>, dim3(ivit_cdiv(M, RP_MT)), dim3(512), 0, ivit_stream(stream),
+                     (const bf16*)dY, lddy, (int)M, (int)K, (const u32x4*)wpack_t, (int)N, nullptr, 0, 1.f,
+                     (bf16*)dX, lddx, (bf16*)pre, ldpre);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

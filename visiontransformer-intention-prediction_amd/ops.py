@@ -248,6 +248,29 @@ def qkv_fwd_q2(x, w, b, D):
     return out
 
 
+def panel_fwd(x, w, b, act=ACT_NONE, want_pre=False, qcols=0, qscale=1.0):
+    """Row-panel form of a wide bf16 token GEMM (ivit_linear_fwd_panel): x [M, K] bf16 @ w [N, K]
+    (f32 master, packed) + b; act GELU with the pre-activation copy, or columns < qcols scaled."""
+    M, K = x.shape
+    N = w.shape[0]
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
+    pre = torch.empty((M, N), dtype=torch.bfloat16, device=x.device) if want_pre else None
+    lib.ivit_linear_fwd_panel(ptr(x), x.stride(0), M, N, K, ptr(packed_weight(w)), ptr(b), act, qcols, qscale,
+                              ptr(y), N, ptr(pre), N, stream())
+    return y, pre
+
+
+def panel_dgrad_gelu(dy, w, pre):
+    """dy [M, K] bf16 @ w [K, N] (f32 master, packed transposed) * gelu'(pre) → bf16 [M, N]
+    (ivit_linear_dgrad_gelu_panel: fc2 dgrad into fc1's pre-activation)."""
+    M, K = dy.shape
+    N = w.shape[1]
+    dx = torch.empty((M, N), dtype=torch.bfloat16, device=dy.device)
+    lib.ivit_linear_dgrad_gelu_panel(ptr(dy), dy.stride(0), M, N, K, ptr(packed_weight_t(w)), ptr(pre),
+                                     pre.stride(0), ptr(dx), N, stream())
+    return dx
+
+
 def attn_fwd_q2(qkv, B, N, H):
     D = H * 64
     out = torch.empty((B * N, D), dtype=qkv.dtype, device=qkv.device)
@@ -487,7 +510,10 @@ class ViTBlockFn(torch.autograd.Function):
             ln1, m1, r1 = ln_in, m_in, r_in
         q2 = cdt == BF16
         panel = q2 and x.shape[1] == 384
-        if q2:
+        if panel:
+            qkv, _ = panel_fwd(ln1, qkvw, qkvb, qcols=H * 64, qscale=Q2_SCALE)
+            o, lse = attn_fwd_q2(qkv, B, N, H)
+        elif q2:
             qkv = qkv_fwd_q2(ln1, wq, qkvb, H * 64)
             o, lse = attn_fwd_q2(qkv, B, N, H)
         else:
@@ -500,7 +526,10 @@ class ViTBlockFn(torch.autograd.Function):
             ln2, m2, r2 = layernorm_fwd(x1, n2w, n2b, eps, cd)
         # inference (torch.inference_mode): nothing is saved, and fc1 skips its pre-activation copy
         infer = torch.is_inference_mode_enabled()
-        a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=not infer)
+        if panel:
+            a, h = panel_fwd(ln2, f1w, f1b, act=ACT_GELU, want_pre=not infer)
+        else:
+            a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=not infer)
         if nxw is not None and panel:
             x2, lnx, mx, rx = linear_resid_ln_fwd(a, f2w, f2b, x1, s2, N, nxw, nxb, eps)
         else:
@@ -512,7 +541,7 @@ class ViTBlockFn(torch.autograd.Function):
             ctx.meta, ctx.q2 = meta, q2
             return x2, lnx, mx, rx
         ctx.save_for_backward(x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2,
-                              qkvw, f1w)
+                              qkvw, f1w, f2w)
         ctx.meta = meta
         ctx.q2 = q2
         ctx.panel = panel
@@ -521,7 +550,7 @@ class ViTBlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx2, *_unused):
         (x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2, qkvw,
-         f1w) = ctx.saved_tensors
+         f1w, f2w) = ctx.saved_tensors
         B, N, H, cdt, eps = ctx.meta
         cd = tdtype(cdt)
         dx2 = torch.zeros_like(x) if dx2 is None else dx2.contiguous()
@@ -530,7 +559,7 @@ class ViTBlockFn(torch.autograd.Function):
         # overlap the dgrad chain (notably the attention backward); joined before returning.
         fork = _WgradFork(dx2.device) if dx2.is_cuda and WGRAD_FORK else None
         dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
-        dh = linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
+        dh = panel_dgrad_gelu(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
         g2 = _wgrad(fork, dx2s, a, cdt)
         if ctx.panel:  # fc1 dgrad with norm2's backward in the epilogue
             dx1, dx1s, dg2, dbe2 = linear_dgrad_ln_bwd(dh, f1w, x1, n2w, m2, r2, dres=dx2, dx=torch.empty_like(dx2),
