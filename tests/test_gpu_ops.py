@@ -153,7 +153,8 @@ def test_attention(B, N, H, cd):
         assert _rel(d[:, i], g[:, i]) < (1e-4 if cdt == F32 else 3e-2), ("qkv"[i], _rel(d[:, i], g[:, i]))
 
 
-@pytest.mark.parametrize("B,N,H", [(1, 64, 1), (2, 257, 3), (1, 4501, 2)])
+@pytest.mark.parametrize("B,N,H", [(1, 64, 1), (2, 257, 3), (1, 4501, 2), (1, 1, 1), (1, 33, 1), (1, 128, 2),
+                                   (1, 130, 1), (1, 200, 1), (1, 320, 2), (3, 449, 1)])
 def test_attention_q2_prescaled_path(B, N, H):
     """bf16 ViT-block path: the qkv projection stores q * log2(e)/8 (ivit_linear_fwd_qs) and the
     attention kernels run on it (ivit_attn_fwd_q2 / _bwd_q2). Outputs, lse and the gradient w.r.t.
@@ -177,7 +178,8 @@ def test_attention_q2_prescaled_path(B, N, H):
     qr = qkv.float().cpu().double().requires_grad_(True)
     oref, lref = _attn_ref(qr, B, N, H)
     assert _rel(o.float(), oref.detach()) < 2e-2
-    assert _rel(lse, lref.detach()) < 6e-4  # the extra bf16 rounding of q * c (the f32 test rounds q once)
+    # the extra bf16 rounding of q * c (the f32 test rounds q once); few rows: a single score's rounding
+    assert _rel(lse, lref.detach()) < (6e-4 if N >= 64 else 3e-3)
     dod = ops.cast(torch.randn(B * N, D).to(DEV), torch.bfloat16)
     oref.backward(dod.float().cpu().double())
     dq = ops.attn_bwd_q2(qs, o, dod, lse, B, N, H)

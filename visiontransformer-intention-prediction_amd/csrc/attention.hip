@@ -8,7 +8,9 @@
 //             P^T straight from the S^T accumulator (no LDS round trip) and V^T by the
 //             CDNA4 transposing LDS read.
 //   backward: dQ kernel (query block, sweep keys) and dK/dV kernel (key block, sweep
-//             queries); both recompute P from the saved LSE. No atomics.
+//             queries); both recompute P from the saved LSE. No atomics. The prescaled-Q
+//             (bf16 ViT block) path runs the software-pipelined v3 kernels; the plain bf16
+//             entry point keeps the v2 tile loops.
 // f32 path (parity): exact-f32 MFMA GEMMs through the generic engine with the score
 //             matrix materialised in the workspace, plus row-softmax kernels.
 #include "attn_common.h"
@@ -359,17 +361,13 @@ IVIT_DEV void dq_tile(const char* kimg, const char* vimg, const bf16x8 (&qf)[4],
 
 // dQ: 4 waves x 32 queries; K/V tiles by LDS-DMA (k-invariant offsets, ragged tail guarded),
 // tile loop unrolled by two so the LDS stage is a compile-time constant.
-// ROWS: this kernel also forms its queries' row constants (replacing attn_rows_v2_kernel):
-// lse2 = lse * log2(e) and delta = rowsum(dO * O) from the dO fragments it already holds and
-// the O rows, and writes both (padded rows: 1e30 / 0) for the dK/dV kernel that follows.
-template <bool Q2 = false, bool ROWS = false>
+// (plain bf16 entry point, unscaled Q; row constants from attn_rows_v2_kernel)
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __restrict__ qkv,
                                                                 const bf16* __restrict__ dout,
                                                                 float* __restrict__ lse2p,
                                                                 float* __restrict__ deltap, int N, int Npad,
                                                                 int H, bf16* __restrict__ dqkv, float c2,
-                                                                float scale, const bf16* __restrict__ out = nullptr,
-                                                                const float* __restrict__ lse = nullptr) {
+                                                                float scale) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -385,30 +383,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
   bf16x8 qf[4], gf[4];
   load_row_frags(Qb + (long)q * ld, qv, lane, qf);
   load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
-  float lse2, dlt;
-  if constexpr (ROWS) {
-    bf16x8 of[4];
-    load_row_frags(out + ((long)b * N + q) * D + h * 64, qv, lane, of);
-    float d = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d = fmaf((float)of[i][e], (float)gf[i][e], d);
-    d = half_swap_sum(d);  // the other 32 of the 64 dims sit in lane ^ 32
-    lse2 = qv ? lse[(long)z * N + q] * LOG2E : 1e30f;
-    dlt = qv ? d : 0.f;
-    if (hl == 0 && q < Npad) {  // negated: the dK/dV kernel starts its MFMA chains from them
-      lse2p[(long)z * Npad + q] = -lse2;
-      deltap[(long)z * Npad + q] = -dlt;
-    }
-  } else {
-    lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
-    dlt = qv ? deltap[(long)z * Npad + q] : 0.f;
-  }
+  const float lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
+  const float dlt = qv ? deltap[(long)z * Npad + q] : 0.f;
   f32x16 a0 = zero16(), a1 = zero16();
-  f32x16 nl;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) nl[r] = -lse2;
   const int nt = (N + AK - 1) / AK, nfull = N / AK;
   int off[2];
 #pragma unroll
@@ -432,9 +409,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
     constexpr int S = decltype(stage)::value;
     if (kt + 1 < nt) issue(kt + 1, smem[S ^ 1][0], smem[S ^ 1][1]);
     if (kt < nfull)
-      dq_tile<false, Q2>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane, nl);
+      dq_tile<false>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane);
     else
-      dq_tile<true, Q2>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane, nl);
+      dq_tile<true>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
@@ -459,29 +436,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __re
 
 // One dK/dV tile step: queries of the Q/dO images (rows past N are zero with lse2 = 1e30,
 // so P = 0 there and no mask is needed) against this wave's 32 keys.
-// NEG (prescaled-Q path): lrow / drow hold -lse2 / -delta, which start the S and dP MFMA chains
-// as their initial accumulators (16 query rows per register block, loaded straight from LDS):
-// P = exp2(acc) and dS = P * acc come out without the per-score FMA and subtraction.
-template <bool NEG>
 IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, const float* drow,
                        const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], f32x16& dk0, f32x16& dk1, f32x16& dv0,
                        f32x16& dv1, float c2, int lane) {
   const int hl = lane >> 5;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    f32x16 s, dp;
-    if constexpr (NEG) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j
-        const float4 l4 = *(const float4*)(lrow + 32 * t + 8 * g + 4 * hl);
-        const float4 d4 = *(const float4*)(drow + 32 * t + 8 * g + 4 * hl);
-        s[4 * g] = l4.x; s[4 * g + 1] = l4.y; s[4 * g + 2] = l4.z; s[4 * g + 3] = l4.w;
-        dp[4 * g] = d4.x; dp[4 * g + 1] = d4.y; dp[4 * g + 2] = d4.z; dp[4 * g + 3] = d4.w;
-      }
-    } else {
-      s = zero16();
-      dp = zero16();
-    }
+    f32x16 s = zero16(), dp = zero16();
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const bf16x8 qa = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
@@ -489,14 +450,7 @@ IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, co
       s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
       dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[ks], dp, 0, 0, 0);
     }
-    if constexpr (NEG) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fast_exp2(s[r]);
-        s[r] = p;           // P[q][key]
-        dp[r] = p * dp[r];  // dS[q][key]
-      }
-    } else {
+    {
       // row constants read after the MFMA chains are issued (off the chains' critical path)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j
@@ -529,8 +483,7 @@ IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, co
   }
 }
 
-// dK/dV: 4 waves x 32 keys; Q, dO tiles and their lse2 / delta rows by LDS-DMA (NEG: negated rows).
-template <bool NEG>
+// dK/dV: 4 waves x 32 keys; Q, dO tiles and their lse2 / delta rows by LDS-DMA.
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ lse2p,
@@ -588,7 +541,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
   auto step = [&](auto stage, int qt) {
     constexpr int S = decltype(stage)::value;
     if (qt + 1 < nt) issue(qt + 1, S ^ 1);
-    dkv_tile<NEG>(smem[S][0], smem[S][1], srow[S][0], srow[S][1], kf, vf, dk0, dk1, dv0, dv1, c2, lane);
+    dkv_tile(smem[S][0], smem[S][1], srow[S][0], srow[S][1], kf, vf, dk0, dk1, dv0, dv1, c2, lane);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   };
@@ -609,6 +562,429 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
       row[D + 32 + (lane & 31)] = (bf16)(dk1[r] * scale);
       row[2 * D + (lane & 31)] = (bf16)dv0[r];
       row[2 * D + 32 + (lane & 31)] = (bf16)dv1[r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- backward v3 (bf16, prescaled Q)
+// The v2 loops were issue-bound: per 64x32 wave-tile of the dK/dV kernel ~140 VALU beside 32
+// MFMAs (the element-wise bf16 packing re-shuffled by v_alignbit / v_perm, accumulator copies),
+// and every S / dP chain MFMA waited (lgkmcnt) on the LDS read issued just before it. v3 keeps
+// the same algorithm and data flow, software-pipelined over 32-row units u (half a 64-row tile):
+//   body(u) = [ A(u): S / dP chains (8 MFMA)        || E(u-1): exp2, dS = P dP, cvt_pk (VALU),
+//                                                       tr-reads for B(u-1)                  ]
+//             [ B(u-1): the products fed by P / dS   || LDS reads of A(u+1)'s fragments and
+//                       (dV/dK: 8 MFMA, dQ: 4 MFMA)       row constants                        ]
+// so no MFMA waits on a read issued in its own gap and the softmax VALU of one unit runs under
+// the matrix work of the next. 3 LDS stages: a tile's last reader (B of its second unit) runs in
+// the first body of the following tile. One barrier per tile, in the middle of its second body:
+// it publishes the next tile (DMA issued one tile ahead) and frees the stage of the tile before.
+
+// accumulator registers 8s..8s+7 -> bf16x8 operand, 4 v_cvt_pk_bf16_f32 (no re-packing)
+IVIT_DEV bf16x8 pack8(const f32x16& a, int s) {
+  const uint4 u = make_uint4(pk_bf16(a[8 * s], a[8 * s + 1]), pk_bf16(a[8 * s + 2], a[8 * s + 3]),
+                             pk_bf16(a[8 * s + 4], a[8 * s + 5]), pk_bf16(a[8 * s + 6], a[8 * s + 7]));
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+constexpr int BNS = 3;  // LDS stages of the v3 backward kernels
+
+// dK/dV: 4 waves x 32 keys (K, V fragments in registers), query tiles of 64 rows with their
+// negated row constants (-lse2, -delta; padded rows -1e30 / 0, so P = 0 there, no mask).
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __restrict__ qkv,
+                                                                 const bf16* __restrict__ dout,
+                                                                 const float* __restrict__ nlse2p,
+                                                                 const float* __restrict__ ndeltap, int N, int Npad,
+                                                                 int H, bf16* __restrict__ dqkv, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][Q|dO]
+  __shared__ __attribute__((aligned(16))) float srow[BNS][2][AK];    // [stage][-lse2|-delta]
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const bf16* Gb = dout + (long)b * N * D + h * 64;
+  const float* L = nlse2p + (long)z * Npad;
+  const float* Dl = ndeltap + (long)z * Npad;
+  const int key = bid.x * AQ + wv * 32 + (lane & 31);
+  bf16x8 kf[4], vf[4];
+  load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
+  load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
+  retire_loads(kf, vf);
+  f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  // DMA: saddr form (tile base in SGPRs, 32-bit per-lane byte offsets, k-invariant on full
+  // tiles); rows past N are clamped to row N-1: their lse2 padding makes P = 0 there
+  unsigned offq[2], offg[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    offq[i] = 2u * dma_off<4>(i, wv, lane, ld);
+    offg[i] = 2u * dma_off<4>(i, wv, lane, D);
+  }
+  auto issue = [&](int qt, int S) {
+    char* qimg = smem[S][0];
+    char* gimg = smem[S][1];
+    const char* qb = uniform_ptr(Qb + (long)qt * AK * ld);
+    const char* gb = uniform_ptr(Gb + (long)qt * AK * D);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = wv * 2 + i;
+      unsigned oq = offq[i], og = offg[i];
+      if (qt >= nfull) {
+        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128(row);
+        const int r = min(qt * AK + row, N - 1) - qt * AK;
+        oq = 2u * (unsigned)(r * ld + c * 8);
+        og = 2u * (unsigned)(r * D + c * 8);
+      }
+      glds_s<false>(oq, qb, qimg + piece * 1024);
+      glds_s<false>(og, gb, gimg + piece * 1024);
+    }
+    if (wv == 0) {
+      glds4_s(4u * lane, uniform_ptr(L + qt * AK), &srow[S][0][0]);
+      glds4_s(4u * lane, uniform_ptr(Dl + qt * AK), &srow[S][1][0]);
+    }
+  };
+
+  // pipeline registers: fragments + initial accumulators of the next A, scores of the last A,
+  // packed P / dS and transposed fragments of the pending B
+  bf16x8 qa[4], ga[4];
+  f32x16 sn, dn;   // A(u+1) chains' initial accumulators (-lse2 / -delta rows of its 32 queries)
+  f32x16 sc, dc;   // A(u) results: S' - lse2, dP - delta
+  auto read_frag = [&](const char* qimg, const char* gimg, int t, int ks) {
+    qa[ks] = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+    ga[ks] = *(const bf16x8*)(gimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+  };
+  auto read_rows = [&](const float* lr, const float* dr, int t, int part) {  // 4 of the 16 row constants
+    const float4 l4 = *(const float4*)(lr + 32 * t + 8 * part + 4 * hl);
+    const float4 d4 = *(const float4*)(dr + 32 * t + 8 * part + 4 * hl);
+    sn[4 * part] = l4.x; sn[4 * part + 1] = l4.y; sn[4 * part + 2] = l4.z; sn[4 * part + 3] = l4.w;
+    dn[4 * part] = d4.x; dn[4 * part + 1] = d4.y; dn[4 * part + 2] = d4.z; dn[4 * part + 3] = d4.w;
+  };
+  unsigned up[8], ud[8];  // packed P / dS of the pending B (words 4ss..4ss+3: 16-row half ss)
+  bf16x8 tg0[2], tg1[2], tq0[2], tq1[2];
+  // E: scores 2i, 2i+1 -> one packed word of P and of dS
+  auto e_step = [&](int i) {
+    const float p0 = fast_exp2(sc[2 * i]), p1 = fast_exp2(sc[2 * i + 1]);
+    up[i] = pk_bf16(p0, p1);
+    ud[i] = pk_bf16(p0 * dc[2 * i], p1 * dc[2 * i + 1]);
+  };
+  auto word8 = [&](const unsigned (&w)[8], int ss) {
+    return __builtin_bit_cast(bf16x8, make_uint4(w[4 * ss], w[4 * ss + 1], w[4 * ss + 2], w[4 * ss + 3]));
+  };
+  auto read_b = [&](const char* qimg, const char* gimg, int t, int ss) {
+    const int rb = 32 * t + 16 * ss;
+    tg0[ss] = tr_acc_order(gimg, rb, 0, lane);
+    tg1[ss] = tr_acc_order(gimg, rb, 32, lane);
+    tq0[ss] = tr_acc_order(qimg, rb, 0, lane);
+    tq1[ss] = tr_acc_order(qimg, rb, 32, lane);
+  };
+  // body: A(u) on (SA, tA) || E(u-1); B(u-1) on (SB, tB) || reads of A(u+1) on (SN, tN).
+  // BAR: barrier in the middle (tA == 1): tile of A(u+1) published, DMA of tile jn issued.
+  auto body = [&](auto sa, auto ta, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
+    constexpr int SA = decltype(sa)::value, TA = decltype(ta)::value, SB = decltype(sb)::value;
+    constexpr int TB = decltype(tb)::value, SN = decltype(sn_)::value, TN = decltype(tn)::value;
+    constexpr bool BAR = decltype(bar)::value;
+    f32x16 s = sn, dp = dn;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const int ks = g >> 1;
+      if ((g & 1) == 0) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[ks], kf[ks], s, 0, 0, 0);
+      else dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ks], vf[ks], dp, 0, 0, 0);
+      if ((g & 1) == 0 && ks < 3) read_frag(smem[SA][0], smem[SA][1], TA, ks + 1);  // 2-3 gaps ahead
+      e_step(g);
+      if (g == 4) read_b(smem[SB][0], smem[SB][1], TB, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (BAR) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (jn < nt) issue(jn, jn % BNS);
+    }
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const int ss = g >> 2;
+      if (g == 1) read_b(smem[SB][0], smem[SB][1], TB, 1);
+      switch (g & 3) {
+        case 0: dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(up, ss), tg0[ss], dv0, 0, 0, 0); break;
+        case 1: dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq0[ss], dk0, 0, 0, 0); break;
+        case 2: dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(up, ss), tg1[ss], dv1, 0, 0, 0); break;
+        default: dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq1[ss], dk1, 0, 0, 0); break;
+      }
+      if (more) {
+        if (g & 1) read_rows(srow[SN][0], srow[SN][1], TN, g >> 1);
+        if (g == 6) read_frag(smem[SN][0], smem[SN][1], TN, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    sc = s;
+    dc = dp;
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using F = std::false_type;
+  using T = std::true_type;
+
+  // prologue: tiles 0 (and 1) in flight, A(0)'s operands; B(-1) runs on P = dS = 0 against a
+  // zeroed stage 2 so that every body has the same shape
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  {
+    uint4* z2 = (uint4*)&smem[2][0][0];  // B(-1)'s stage: finite zeros
+    for (int i = tid; i < 2 * 8192 / 16; i += 256) z2[i] = make_uint4(0, 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int part = 0; part < 4; ++part) read_rows(srow[0][0], srow[0][1], 0, part);
+  read_frag(smem[0][0], smem[0][1], 0, 0);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    sc[r] = NEG_BIG;  // exp2 -> 0
+    dc[r] = 0.f;
+  }
+  // tile j in stage j % 3: body(2j) = A(j,0) | B(j-1,1) | next A(j,1); body(2j+1) = A(j,1) |
+  // barrier (tile j+1 landed; issue tile j+2) | B(j,0) | next A(j+1,0)
+  auto tile = [&](auto s, int j) {
+    constexpr int S = decltype(s)::value;
+    using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
+    using SNX = std::integral_constant<int, (S + 1) % BNS>;
+    using SC = std::integral_constant<int, S>;
+    body(SC{}, I0{}, SP{}, I1{}, SC{}, I1{}, F{}, 0, true);
+    body(SC{}, I1{}, SC{}, I0{}, SNX{}, I0{}, T{}, j + 2, j + 1 < nt);
+  };
+  int j = 0;
+  for (; j + 3 <= nt; j += 3) {
+    tile(I0{}, j);
+    tile(I1{}, j + 1);
+    tile(I2{}, j + 2);
+  }
+  if (j < nt) tile(I0{}, j);
+  if (j + 1 < nt) tile(I1{}, j + 1);
+  // drain: E and B of the last unit (tile nt-1, rows 32..63)
+  {
+    const int S = (nt - 1) % BNS;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e_step(i);
+    read_b(smem[S][0], smem[S][1], 1, 0);
+    read_b(smem[S][0], smem[S][1], 1, 1);
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(up, ss), tg0[ss], dv0, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq0[ss], dk0, 0, 0, 0);
+      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(up, ss), tg1[ss], dv1, 0, 0, 0);
+      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq1[ss], dk1, 0, 0, 0);
+    }
+  }
+  const int kw = bid.x * AQ + wv * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    if (kk < N) {
+      bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
+      row[D + (lane & 31)] = (bf16)(dk0[r] * scale);
+      row[D + 32 + (lane & 31)] = (bf16)(dk1[r] * scale);
+      row[2 * D + (lane & 31)] = (bf16)dv0[r];
+      row[2 * D + 32 + (lane & 31)] = (bf16)dv1[r];
+    }
+  }
+}
+
+// dQ: 4 waves x 32 queries (prescaled Q and dO fragments in registers), key tiles of 64 rows;
+// also forms the queries' row constants (as attn_bwd_dq_v2_kernel<true, true>) and writes them
+// negated for the dK/dV kernel. The pipeline runs over the full key tiles; a ragged last tile
+// (keys past N masked) goes through dq_tile afterwards.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_v3_kernel(const bf16* __restrict__ qkv,
+                                                                const bf16* __restrict__ dout,
+                                                                float* __restrict__ nlse2p,
+                                                                float* __restrict__ ndeltap, int N, int Npad, int H,
+                                                                bf16* __restrict__ dqkv, float scale,
+                                                                const bf16* __restrict__ out,
+                                                                const float* __restrict__ lse) {
+  __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int q = bid.x * AQ + wv * 32 + (lane & 31);
+  const bool qv = q < N;
+  bf16x8 qf[4], gf[4];
+  load_row_frags(Qb + (long)q * ld, qv, lane, qf);
+  load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
+  float lse2, dlt;
+  {
+    bf16x8 of[4];
+    load_row_frags(out + ((long)b * N + q) * D + h * 64, qv, lane, of);
+    float d = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf((float)of[i][e], (float)gf[i][e], d);
+    d = half_swap_sum(d);  // the other 32 of the 64 dims sit in lane ^ 32
+    lse2 = qv ? lse[(long)z * N + q] * LOG2E : 1e30f;
+    dlt = qv ? d : 0.f;
+    if (hl == 0 && q < Npad) {
+      nlse2p[(long)z * Npad + q] = -lse2;
+      ndeltap[(long)z * Npad + q] = -dlt;
+    }
+  }
+  f32x16 a0 = zero16(), a1 = zero16();
+  f32x16 nl, nd;  // S' and dP chains start from -lse2 / -delta (the query is the lane)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    nl[r] = -lse2;
+    nd[r] = -dlt;
+  }
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  unsigned off[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) off[i] = 2u * dma_off<4>(i, wv, lane, ld);
+  auto issue = [&](int kt, int S) {  // as the dK/dV kernel; keys past N are masked in dq_tile
+    char* kimg = smem[S][0];
+    char* vimg = smem[S][1];
+    const char* kb = uniform_ptr(Kb + (long)kt * AK * ld);
+    const char* vb = uniform_ptr(Vb + (long)kt * AK * ld);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = wv * 2 + i;
+      unsigned o = off[i];
+      if (kt >= nfull) {
+        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128(row);
+        o = 2u * (unsigned)((min(kt * AK + row, N - 1) - kt * AK) * ld + c * 8);
+      }
+      glds_s<false>(o, kb, kimg + piece * 1024);
+      glds_s<false>(o, vb, vimg + piece * 1024);
+    }
+  };
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  {
+    uint4* z2 = (uint4*)&smem[2][0][0];
+    for (int i = tid; i < 2 * 8192 / 16; i += 256) z2[i] = make_uint4(0, 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  if (nfull > 0) {
+    bf16x8 ka[4], va[4];
+    f32x16 sc, dc;
+    bf16x8 pdq[2];
+    bf16x8 tk0[2], tk1[2];
+    auto read_a = [&](const char* kimg, const char* vimg, int t, int ks) {
+      ka[ks] = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+      va[ks] = *(const bf16x8*)(vimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
+    };
+    auto e_step = [&](int i) {
+      const float p0 = fast_exp2(sc[2 * i]), p1 = fast_exp2(sc[2 * i + 1]);
+      uint4 u = __builtin_bit_cast(uint4, pdq[i >> 2]);
+      const unsigned w = pk_bf16(p0 * dc[2 * i], p1 * dc[2 * i + 1]);
+      switch (i & 3) {
+        case 0: u.x = w; break;
+        case 1: u.y = w; break;
+        case 2: u.z = w; break;
+        default: u.w = w; break;
+      }
+      pdq[i >> 2] = __builtin_bit_cast(bf16x8, u);
+    };
+    auto read_b = [&](const char* kimg, int t, int ss) {
+      const int rb = 32 * t + 16 * ss;
+      tk0[ss] = tr_acc_order(kimg, rb, 0, lane);
+      tk1[ss] = tr_acc_order(kimg, rb, 32, lane);
+    };
+    auto body = [&](auto sa, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
+      constexpr int SB = decltype(sb)::value, TB = decltype(tb)::value;
+      constexpr int SN = decltype(sn_)::value, TN = decltype(tn)::value;
+      constexpr bool BAR = decltype(bar)::value;
+      (void)sa;
+      f32x16 s = nl, dp = nd;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const int ks = g >> 1;
+        if ((g & 1) == 0) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[ks], qf[ks], s, 0, 0, 0);
+        else dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[ks], gf[ks], dp, 0, 0, 0);
+        e_step(g);
+        if (g == 2) read_b(smem[SB][0], TB, 0);
+        if (g == 5) read_b(smem[SB][0], TB, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (BAR) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (jn < nt) issue(jn, jn % BNS);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ss = g >> 1;
+        if ((g & 1) == 0) a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pdq[ss], tk0[ss], a0, 0, 0, 0);
+        else a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pdq[ss], tk1[ss], a1, 0, 0, 0);
+        if (more) read_a(smem[SN][0], smem[SN][1], TN, g);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      sc = s;
+      dc = dp;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using F = std::false_type;
+    using T = std::true_type;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) read_a(smem[0][0], smem[0][1], 0, ks);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sc[r] = NEG_BIG;
+      dc[r] = 0.f;
+    }
+    auto tile = [&](auto s, int j) {
+      constexpr int S = decltype(s)::value;
+      using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
+      using SNX = std::integral_constant<int, (S + 1) % BNS>;
+      using SC = std::integral_constant<int, S>;
+      body(SC{}, SP{}, I1{}, SC{}, I1{}, F{}, 0, true);
+      body(SC{}, SC{}, I0{}, SNX{}, I0{}, T{}, j + 2, j + 1 < nfull);
+    };
+    int j = 0;
+    for (; j + 3 <= nfull; j += 3) {
+      tile(I0{}, j);
+      tile(I1{}, j + 1);
+      tile(I2{}, j + 2);
+    }
+    if (j < nfull) tile(I0{}, j);
+    if (j + 1 < nfull) tile(I1{}, j + 1);
+    const int S = (nfull - 1) % BNS;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e_step(i);
+    read_b(smem[S][0], 1, 0);
+    read_b(smem[S][0], 1, 1);
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pdq[ss], tk0[ss], a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pdq[ss], tk1[ss], a1, 0, 0, 0);
+    }
+  }
+  if (nt > nfull) {  // ragged last key tile (DMA issued one tile ahead, or in the prologue)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int S = nfull % BNS;
+    dq_tile<true, true>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, nfull * AK, N, 1.0f, lane, nl);
+  }
+  const int qw = bid.x * AQ + wv * 32;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qq = qw + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    if (qq < N) {
+      bf16* row = dqkv + ((long)b * N + qq) * ld + h * 64;
+      row[lane & 31] = (bf16)(a0[r] * scale);
+      row[32 + (lane & 31)] = (bf16)(a1[r] * scale);
     }
   }
 }
@@ -722,9 +1098,9 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
     float* deltap = lse2p + B * H * Npad;
     hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad * 8, 256)), dim3(256), 0, st,
                        (const bf16*)out, (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
-    hipLaunchKernelGGL(attn_bwd_dq_v2_kernel<false>, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
+    hipLaunchKernelGGL(attn_bwd_dq_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
                        deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
-    hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel<false>, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout,
+    hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout,
                        lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
     IVIT_LAUNCH_CHECK();
     return 0;
@@ -804,11 +1180,10 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   float* lse2p = (float*)work;
   float* deltap = lse2p + B * H * Npad;
   // dQ also forms the row constants (-lse2, -delta) the dK/dV kernel reads: no rows kernel
-  hipLaunchKernelGGL((attn_bwd_dq_v2_kernel<true, true>), g, dim3(256), 0, st, (const bf16*)qkv,
-                     (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, scale,
-                     (const bf16*)out, lse);
-  hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel<true>, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
-                     deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 1.0f, 0.69314718055994531f);
+  hipLaunchKernelGGL(attn_bwd_dq_v3_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p, deltap,
+                     (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
+  hipLaunchKernelGGL(attn_bwd_dkv_v3_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p, deltap,
+                     (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -2,6 +2,7 @@
 // kernels and the f32 parity path). gfx950 only.
 #pragma once
 #include "gemm_engine.h"
+#include "panel_common.h"
 
 using namespace ivit;
 
@@ -11,6 +12,13 @@ constexpr int AQ = 128;  // queries per workgroup (4 waves x 32)
 constexpr int AK = 64;   // keys per tile
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;
+
+// LDS-DMA of 4 B per lane, saddr form: sbase + voff -> lds + 4 * lane.
+IVIT_DEV void glds4_s(unsigned voff, const char* sbase, void* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, %2" ::"v"(voff), "s"(a), "s"(sbase)
+               : "memory");
+}
 
 // tile image: 64 rows x 64 bf16 (128-B rows), chunk swizzle swz128 (see gemm_engine.h)
 IVIT_DEV int t_off(int r, int c) { return r * 128 + ((c ^ swz128(r)) << 4); }
