@@ -161,16 +161,22 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
       for (int e = 0; e < 8; ++e) qf[i][e] = (bf16)((float)qf[i][e] * c2);
   }
   const int nt = (N + AK - 1) / AK, nfull = N / AK;
-  int off[8 / W];
+  // saddr LDS-DMA (tile base in SGPRs, k-invariant 32-bit byte offsets); keys past N are clamped
+  // to row N-1 (finite V rows; their scores are masked to P = 0)
+  unsigned off[8 / W];
 #pragma unroll
-  for (int i = 0; i < 8 / W; ++i) off[i] = dma_off<W>(i, wv, lane, ld);
+  for (int i = 0; i < 8 / W; ++i) off[i] = 2u * dma_off<W>(i, wv, lane, ld);
   auto issue1 = [&](const bf16* base, int kt, char* img) {
-    if (kt < nfull) {
-      const bf16* src = base + (long)kt * AK * ld;
+    const char* sb = uniform_ptr(base + (long)kt * AK * ld);
 #pragma unroll
-      for (int i = 0; i < 8 / W; ++i) glds<16>((src + off[i]), img + (wv * (8 / W) + i) * 1024);
-    } else {
-      tile_glds_w<W>(base, ld, kt * AK, N, img, wv, lane);
+    for (int i = 0; i < 8 / W; ++i) {
+      const int piece = wv * (8 / W) + i;
+      unsigned o = off[i];
+      if (kt >= nfull) {
+        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128(row);
+        o = 2u * (unsigned)((min(kt * AK + row, N - 1) - kt * AK) * ld + c * 8);
+      }
+      glds_s<false>(o, sb, img + piece * 1024);
     }
   };
   bf16x8 ones;
@@ -209,8 +215,10 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
 #pragma unroll
         for (int r = 0; r < 16; ++r) nxt[t][r] -= d;
       m += d;
+      // in place (tied asm operands): negm keeps ONE register home across the rare branch, so
+      // the common path needs no phi copies of its 16 registers
 #pragma unroll
-      for (int r = 0; r < 16; ++r) negm[r] = -m;
+      for (int r = 0; r < 16; ++r) asm volatile("v_sub_f32 %0, %0, %1" : "+v"(negm[r]) : "v"(d));
     }
   };
   auto body = [&](auto stage, auto nxmode, int j, f32x16(&cur)[2], f32x16(&nxt)[2]) {
@@ -265,24 +273,28 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
     if (j & 1) body(I1{}, I3{}, j, sn, sc);
     else body(I0{}, I3{}, j, sc, sn);
   }
-  if (q < N) {
-    const float l = lacc[0];
-    const float inv = 1.f / l;
-    bf16* orow = out + ((long)b * N + q) * D + h * 64;
+  // epilogue: register 4g+e of o0 / o1 is dim 8g + 4hl + e (+32) of query q. One
+  // v_permlane32_swap per word pairs lane q's half-block with lane q+32's, so each lane holds
+  // 8 contiguous dims: lanes < 32 blocks g+1, lanes >= 32 blocks g (g even) — 16-B stores, 32
+  // contiguous bytes per row per instruction (8-B stores left partial lines: PMC writes 4.7x)
+  const float l = lacc[0];
+  const float inv = 1.f / l;
+  bf16* orow = out + ((long)b * N + (q < N ? q : 0)) * D + h * 64;
+  auto emit = [&](const f32x16& o, int dbase) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      Pack4 a, c;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a.h[e] = (bf16)(o0[4 * g + e] * inv);
-        c.h[e] = (bf16)(o1[4 * g + e] * inv);
-      }
-      const int d = 8 * g + 4 * hl;
-      *(uint2*)(orow + d) = a.u;
-      *(uint2*)(orow + 32 + d) = c.u;
+    for (int g = 0; g < 4; g += 2) {
+      const unsigned e0 = pk_bf16(o[4 * g] * inv, o[4 * g + 1] * inv);
+      const unsigned e1 = pk_bf16(o[4 * g + 2] * inv, o[4 * g + 3] * inv);
+      const unsigned d0 = pk_bf16(o[4 * g + 4] * inv, o[4 * g + 5] * inv);
+      const unsigned d1 = pk_bf16(o[4 * g + 6] * inv, o[4 * g + 7] * inv);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(d0, e0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(d1, e1, false, false);
+      if (q < N) *(uint4*)(orow + dbase + 8 * (hl ? g : g + 1)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
     }
-    if (hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
-  }
+  };
+  emit(o0, 0);
+  emit(o1, 32);
+  if (q < N && hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
 }
 
 // ------------------------------------------------------------------------- backward v2 (bf16)
