@@ -86,7 +86,9 @@ union Pack4 {
 // bf16 resolution); erf(x/sqrt2) and the Gaussian density share one exp(-x^2/2).
 IVIT_DEV float erf_as(float x, float e /* = exp(-x*x) */) {
   const float a = fabsf(x);
-  const float t = __frcp_rn(1.0f + 0.3275911f * a);
+  // raw v_rcp_f32 (1 ulp): __frcp_rn compiles to the 8-instruction correctly-rounded division
+  // sequence, the largest part of this epilogue function; the polynomial's own error is 1.5e-7
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * a);
   const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
   const float r = 1.0f - p * e;
   return x < 0.f ? -r : r;
