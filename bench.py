@@ -43,11 +43,11 @@ def step_flops(B, H, W, depth=12, D=384, C_l=290, C_m=9, planes=512, A=5, K=8, a
 
 
 # The dominant kernels of the bf16 step (profiles/r02_*_bench_kernel_stats.csv): the attention
-# backward pair of ivit_attn_bwd_q2 (attn_bwd_dq_v2 + attn_bwd_dkv_v2, ~30 % of GPU time), then the
-# attention forward (ivit_attn_fwd_q2, ~11 %). The roofline object reports whichever of the two has
+# backward pair of ivit_attn_bwd_q2 (attn_bwd_dq_v3 + attn_bwd_dkv_v3, ~31 % of GPU time), then the
+# attention forward (ivit_attn_fwd_q2, ~13 %). The roofline object reports whichever of the two has
 # the larger measured time per step (HIP events on the launching stream, inside the timed loop).
 ATTN = {
-    "attn_bwd": {"kernels": ["attn_bwd_dq_v2_kernel", "attn_bwd_dkv_v2_kernel"], "entry": "ivit_attn_bwd_q2",
+    "attn_bwd": {"kernels": ["attn_bwd_dq_v3_kernel", "attn_bwd_dkv_v3_kernel"], "entry": "ivit_attn_bwd_q2",
                  "flops_note": "8*B*H*N^2*64 (dQ, dK, dV, dP products; the S recompute is not counted)"},
     "attn_fwd": {"kernels": ["attn_fwd_bf16_v6_kernel"], "entry": "ivit_attn_fwd_q2",
                  "flops_note": "4*B*H*N^2*64 (QK^T, PV)"},

@@ -400,7 +400,8 @@ def test_linear_dgrad_ln_bwd_fused(M, K, xs):
 
 
 @pytest.mark.parametrize("M,N,K,mode", [(36008, 1152, 384, "qs"), (36008, 1536, 384, "gelu"), (300, 768, 128, "gelu"),
-                                        (145, 1536, 384, "dgelu"), (36008, 1536, 384, "dgelu"), (1, 384, 64, "qs")])
+                                        (145, 1536, 384, "dgelu"), (36008, 1536, 384, "dgelu"), (1, 384, 64, "qs"),
+                                        (36008, 384, 384, "dgrad"), (77, 384, 384, "dgrad")])
 def test_panel_wide(M, N, K, mode):
     """Row-panel wide GEMMs (ivit_linear_fwd_panel / ivit_linear_dgrad_gelu_panel) vs the generic
     engine on the same bf16 operands (qkv with the prescaled Q block, fc1 + GELU + pre-activation,
@@ -409,6 +410,11 @@ def test_panel_wide(M, N, K, mode):
     from _lib import ACT_GELU, BF16
     g = torch.Generator().manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    if mode == "dgrad":  # ops.panel_dgrad: the proj dgrad (ivit_linear_fwd_panel on the transposed pack)
+        w = (torch.randn(K, N, generator=g) / math.sqrt(K)).to(DEV)
+        ref = ops.linear_dgrad(x, w.to(torch.bfloat16), BF16, torch.bfloat16)
+        assert _rel(ops.panel_dgrad(x, w).float(), ref.float()) < 8e-3
+        return
     if mode == "dgelu":
         w = (torch.randn(K, N, generator=g) / math.sqrt(K)).to(DEV)
         pre = torch.randn(M, N, generator=g).to(torch.bfloat16).to(DEV)

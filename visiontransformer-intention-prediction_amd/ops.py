@@ -260,6 +260,17 @@ def panel_fwd(x, w, b, act=ACT_NONE, want_pre=False, qcols=0, qscale=1.0):
     return y, pre
 
 
+def panel_dgrad(dy, w):
+    """dy [M, K] bf16 @ w [K, N] (f32 master [out, in], packed transposed) → bf16 [M, N]: the plain
+    dgrad through the row-panel kernel (ivit_linear_fwd_panel on the transposed pack)."""
+    M, K = dy.shape
+    N = w.shape[1]
+    dx = torch.empty((M, N), dtype=torch.bfloat16, device=dy.device)
+    lib.ivit_linear_fwd_panel(ptr(dy), dy.stride(0), M, N, K, ptr(packed_weight_t(w)), None, ACT_NONE, 0, 1.0,
+                              ptr(dx), N, None, 0, stream())
+    return dx
+
+
 def panel_dgrad_gelu(dy, w, pre):
     """dy [M, K] bf16 @ w [K, N] (f32 master, packed transposed) * gelu'(pre) → bf16 [M, N]
     (ivit_linear_dgrad_gelu_panel: fc2 dgrad into fc1's pre-activation)."""
@@ -541,7 +552,7 @@ class ViTBlockFn(torch.autograd.Function):
             ctx.meta, ctx.q2 = meta, q2
             return x2, lnx, mx, rx
         ctx.save_for_backward(x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2,
-                              qkvw, f1w, f2w)
+                              qkvw, f1w, f2w, pw)
         ctx.meta = meta
         ctx.q2 = q2
         ctx.panel = panel
@@ -550,7 +561,7 @@ class ViTBlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dx2, *_unused):
         (x, ln1, qkv, o, lse, x1, ln2, h, a, m1, r1, m2, r2, n1w, n2w, wq, wp, w1, w2, s1, s2, qkvw,
-         f1w, f2w) = ctx.saved_tensors
+         f1w, f2w, pw) = ctx.saved_tensors
         B, N, H, cdt, eps = ctx.meta
         cd = tdtype(cdt)
         dx2 = torch.zeros_like(x) if dx2 is None else dx2.contiguous()
@@ -569,7 +580,7 @@ class ViTBlockFn(torch.autograd.Function):
             dx1, dx1s, dg2, dbe2 = layernorm_bwd(x1, n2w, m2, r2, dln2, dres=dx2, dx=torch.empty_like(dx2),
                                                  xs_dtype=cd, row_scale=s1, rps=N)
         g1 = _wgrad(fork, dh, ln2, cdt)
-        do = linear_dgrad(dx1s, wp, cdt, cd)
+        do = panel_dgrad(dx1s, pw) if ctx.panel else linear_dgrad(dx1s, wp, cdt, cd)
         gp = _wgrad(fork, dx1s, o, cdt)
         dqkv = attn_bwd_q2(qkv, o, do, lse, B, N, H) if ctx.q2 else attn_bwd(qkv, o, do, lse, B, N, H, cdt)
         if ctx.panel:  # qkv dgrad with norm1's backward in the epilogue
