@@ -498,6 +498,19 @@ def _wgrad(fork, dy, x, cdt):
     return linear_wgrad(dy, x, cdt) if fork is None else fork.run(linear_wgrad, dy, x, cdt)
 
 
+class GradHandoff:
+    """Backward hand-off between consecutive fused ViT blocks: block i+1's qkv-dgrad + norm1-backward
+    kernel also writes bf16(dx * s2_i) — block i's DropPath-scaled MLP-branch gradient, the fc2
+    dgrad's operand — so block i skips that separate scale-and-cast pass over dx. `scale` is set
+    by block i's forward; `g` / `ptr` by block i+1's backward; block i uses `g` only if the
+    gradient it receives is that very tensor (`ptr`), else it recomputes it."""
+    __slots__ = ("scale", "g", "ptr")
+    used = 0  # hand-offs taken (tests)
+
+    def __init__(self):
+        self.scale, self.g, self.ptr = None, None, None
+
+
 class ViTBlockFn(torch.autograd.Function):
     """timm Block: x + dp1(proj(attn(norm1 x))); x + dp2(fc2(gelu(fc1(norm2 x)))).
     x: (B*N, D) f32 residual stream; GEMM operands in the compute dtype (f32 or bf16).
@@ -511,7 +524,7 @@ class ViTBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, ln_in, m_in, r_in, n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b, nxw, nxb,
-                s1, s2, meta):
+                s1, s2, meta, hand_mine=None, hand_prev=None):
         B, N, H, cdt, eps = meta
         cd = tdtype(cdt)
         wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
@@ -556,6 +569,9 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.meta = meta
         ctx.q2 = q2
         ctx.panel = panel
+        ctx.hand_mine, ctx.hand_prev = (hand_mine, hand_prev) if panel else (None, None)
+        if ctx.hand_mine is not None:
+            ctx.hand_mine.scale, ctx.hand_mine.g, ctx.hand_mine.ptr = s2, None, None
         return x2, lnx, mx, rx
 
     @staticmethod
@@ -569,7 +585,15 @@ class ViTBlockFn(torch.autograd.Function):
         # The weight gradients are off the critical path: they run on a forked stream and
         # overlap the dgrad chain (notably the attention backward); joined before returning.
         fork = _WgradFork(dx2.device) if dx2.is_cuda and WGRAD_FORK else None
-        dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
+        hm, hp = ctx.hand_mine, ctx.hand_prev
+        dx2s = None
+        if hm is not None:
+            if hm.g is not None and hm.ptr == dx2.data_ptr():
+                dx2s = hm.g  # written by the next block's qkv-dgrad epilogue
+                GradHandoff.used += 1
+            hm.g = hm.ptr = None
+        if dx2s is None:
+            dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
         dh = panel_dgrad_gelu(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
         g2 = _wgrad(fork, dx2s, a, cdt)
         if ctx.panel:  # fc1 dgrad with norm2's backward in the epilogue
@@ -584,7 +608,12 @@ class ViTBlockFn(torch.autograd.Function):
         gp = _wgrad(fork, dx1s, o, cdt)
         dqkv = attn_bwd_q2(qkv, o, do, lse, B, N, H) if ctx.q2 else attn_bwd(qkv, o, do, lse, B, N, H, cdt)
         if ctx.panel:  # qkv dgrad with norm1's backward in the epilogue
-            dx0, _, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1)
+            if hp is not None:  # also the previous block's bf16(dx0 * s2) (GradHandoff)
+                dx0, dx0s, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1, xs_dtype=cd,
+                                                           row_scale=hp.scale, rps=N)
+                hp.g, hp.ptr = dx0s, dx0.data_ptr()
+            else:
+                dx0, _, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1)
         else:
             dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
             dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
@@ -593,7 +622,7 @@ class ViTBlockFn(torch.autograd.Function):
             fork.join((dx2s, dh, dx1s, dqkv, a, ln2, o, ln1))
         (dW2, db2), (dW1, db1), (dWp, dbp), (dWq, dbq) = g2, g1, gp, gq
         return (dx0, None, None, None, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, None, None,
-                None, None, None)
+                None, None, None, None, None)
 
 
 class NeckFn(torch.autograd.Function):

@@ -75,7 +75,7 @@ class Block(nn.Module):
         self.last_scales = (s[0].contiguous(), s[1].contiguous())
         return self.last_scales
 
-    def forward_flat(self, x, B, N, cdt, ln_in=None, next_norm=None):
+    def forward_flat(self, x, B, N, cdt, ln_in=None, next_norm=None, hand_mine=None, hand_prev=None):
         """-> (x_out, (y, mean, rstd) of the next block's norm1 or empty tensors): `ln_in` is
         this block's (y, mean, rstd) of norm1 computed by the previous block's fc2 epilogue;
         `next_norm` the next block's norm1, whose forward this block's fc2 epilogue runs
@@ -87,7 +87,8 @@ class Block(nn.Module):
         out = ops.ViTBlockFn.apply(x, li, mi, ri, self.norm1.weight, self.norm1.bias, self.attn.qkv.weight,
                                     self.attn.qkv.bias, self.attn.proj.weight, self.attn.proj.bias, self.norm2.weight,
                                     self.norm2.bias, self.mlp.fc1.weight, self.mlp.fc1.bias, self.mlp.fc2.weight,
-                                    self.mlp.fc2.bias, nxw, nxb, s1, s2, (B, N, self.attn.num_heads, cdt, 1e-6))
+                                    self.mlp.fc2.bias, nxw, nxb, s1, s2, (B, N, self.attn.num_heads, cdt, 1e-6),
+                                    hand_mine, hand_prev)
         return out[0], tuple(out[1:])
 
     def forward(self, x):
@@ -134,9 +135,13 @@ class VisionTransformer(nn.Module):
         # bf16 at D = 384: block i's fc2 epilogue also produces block i+1's norm1 (ops.ViTBlockFn)
         fuse = cdt == BF16 and self.embed_dim == 384
         ln = None
+        # ... and in the backward, block i+1 hands block i its DropPath-scaled bf16 gradient
+        hands = [ops.GradHandoff() for _ in self.blocks] if fuse and torch.is_grad_enabled() else None
         for i, blk in enumerate(self.blocks):
             nxt = self.blocks[i + 1].norm1 if fuse and i + 1 < len(self.blocks) else None
-            t, nxt_ln = blk.forward_flat(t, B, N, cdt, ln_in=ln, next_norm=nxt)
+            t, nxt_ln = blk.forward_flat(t, B, N, cdt, ln_in=ln, next_norm=nxt,
+                                         hand_mine=hands[i] if hands else None,
+                                         hand_prev=hands[i - 1] if hands and i > 0 else None)
             ln = nxt_ln if nxt is not None else None
         return t
 
