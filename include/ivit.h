@@ -69,7 +69,7 @@ int ivit_linear_dgrad_ln_bwd(const void* dY, long lddy, long M, long N, long K, 
                              long ldr, float* dX, long lddx, void* dXs, const float* scale, long rps, float* dgamma,
                              float* dbeta, int accumulate, void* work, long work_bytes, void* stream);
 /* Row-panel forms of the wide token GEMMs (bf16, N a multiple of 384, K of 64): each workgroup
- * writes 144 whole output rows, walking the N / 384 column chunks (timm Attention.qkv, Mlp.fc1).
+ * writes one 144-row x 192-column block (two workgroups per CU) (timm Attention.qkv, Mlp.fc1).
  *   act NONE: Y = (A W^T + bias), columns n < qcols times qscale (qkv with the Q block prescaled)
  *   act GELU: Ypre = A W^T + bias (if non-null), Y = gelu(Ypre)   (W packed by ivit_patch_weight_pack) */
 int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, long K, const void* wpack, const float* bias,

@@ -27,6 +27,14 @@ IVIT_DEV void wait_vm(int n) {
 }
 #undef PANEL_VM
 
+// Workgroup barrier that also publishes this wave's LDS stores: a raw s_barrier does not wait for
+// outstanding ds_write (the compiler inserts no lgkmcnt wait before it), so a partner wave could
+// read the location before the store lands.
+IVIT_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
 // Wave-uniform 64-bit address -> SGPR pair (the saddr operand of the loads below).
 IVIT_DEV const char* uniform_ptr(const void* p) {
   const unsigned long v = (unsigned long)p;

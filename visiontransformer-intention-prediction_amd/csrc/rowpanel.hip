@@ -29,15 +29,18 @@ constexpr int RP_TLD = RP_N + 4;           // epilogue row stride (floats)
 IVIT_DEV int rp_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
 
 // The streamed operand's per-lane LDS-DMA sources (row-panel-invariant): 18 pieces of 8 rows per
-// stage over 8 waves, the first two waves take three.
+// stage over W waves (W = 8: the first two waves take three, the rest two; W = 4: five / four).
+constexpr int RP_PWMAX = 5;
 struct PanelA {
   const bf16* A0;
-  unsigned voff[3];
+  unsigned voff[RP_PWMAX];
   int npc, pc0;
 };
 
+template <int W = 8>
 IVIT_DEV PanelA panel_a_setup(const bf16* A, long lda, int M, int m0, int wv, int lane) {
-  constexpr int PW = 3, PREM = RP_PIECES % 8;
+  constexpr int PW = (RP_PIECES + W - 1) / W, PREM = RP_PIECES % W;
+  static_assert(PREM != 0 && PW <= RP_PWMAX, "piece split");
   PanelA p;
   p.npc = wv < PREM ? PW : PW - 1;
   p.pc0 = wv < PREM ? wv * PW : PREM * PW + (wv - PREM) * (PW - 1);
@@ -54,13 +57,15 @@ IVIT_DEV PanelA panel_a_setup(const bf16* A, long lda, int M, int m0, int wv, in
 
 // acc[9][3] = rows m0 .. m0+143 of A (K = 64 KT) times the 48 columns of 16-column blocks
 // nb0 .. nb0+2 of a packed weight with NB16 blocks in total.
+template <int W = 8>
 IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA& pa, const u32x4* wpack, int NB16,
                              int nb0, int KT, int wv, int lane) {
+  constexpr int PW = (RP_PIECES + W - 1) / W;
   auto issue_a = [&](int kt) {
     char* st = smem + (kt % RP_NS) * RP_STAGE + pa.pc0 * 1024;
     const char* sb = uniform_ptr(pa.A0 + kt * 64);
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < PW; ++i)
       if (i < pa.npc) glds_s<false>(pa.voff[i], sb, st + i * 1024);
   };
   const unsigned vb = lane * 16;
@@ -189,7 +194,7 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         T[(4 * (lane >> 4) + i) * RP_TLD + (wv * NBW + j) * 16 + (lane & 15)] = acc[mb][j][i] + bv[j];
-    __builtin_amdgcn_s_barrier();
+    lds_barrier();
     const int m = m0 + 16 * mb + r;
     const bool ok = m < M;
     float t[12], u[12];
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
       red[(r * 2 + 0) * RP_N + c0 + e] = pg[e];
       red[(r * 2 + 1) * RP_N + c0 + e] = pb[e];
     }
-    __builtin_amdgcn_s_barrier();
+    lds_barrier();
     for (int c = tid; c < 2 * RP_N; c += 512) {
       float a = 0.f;
 #pragma unroll
@@ -296,38 +301,54 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
 }
 
 // ============================================================================= wide outputs
-// The same row panel for outputs wider than 384 columns (qkv 1152, fc1 1536, fc2's dgrad 1536):
-// the workgroup walks the N / 384 column chunks, re-streaming its 144-row A panel (from L2) for
-// each, so every output row segment is written by one workgroup as whole rows.
+// The same row panel for outputs wider than 384 columns (qkv 1152, fc1 1536, fc2's dgrad 1536)
+// and the plain proj dgrad: the A panel of 144 rows is streamed once per 192- (or 384-) column
+// chunk (from L2 for all but the first), and each chunk's row segments are written whole.
 //   EPI_QS:     Y = bf16((acc + bias[n]) * (n < qcols ? qscale : 1))        (qkv, Q block prescaled)
 //   EPI_GELU:   P = bf16(acc + bias[n]), Y = bf16(gelu(acc + bias[n]))       (fc1 + pre-activation)
 //   EPI_DGELU:  Y = bf16(acc * gelu'(P[m][n]))                                (fc2 dgrad, W packed transposed)
 constexpr int EPI_QS = 0, EPI_GELU = 1, EPI_DGELU = 2;
 
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void rowpanel_wide_kernel(const bf16* __restrict__ A, long lda, int M, int K,
-                                                               const u32x4* __restrict__ wpack, int N,
-                                                               const float* __restrict__ bias, int qcols,
-                                                               float qscale, bf16* __restrict__ Y, long ldy,
-                                                               bf16* __restrict__ P, long ldp) {
+// W = 8: one 512-thread workgroup per 144-row panel walks the N / 384 column chunks (one per CU).
+// W = 4: a 256-thread workgroup per (panel, 192-column chunk), two per CU (2 x 74 KiB LDS): the
+// epilogue of one (VALU + stores) runs beside the other's MFMA main loop instead of after it.
+template <int EPI, int W>
+__global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16* __restrict__ A, long lda, int M,
+                                                                      int K, const u32x4* __restrict__ wpack, int N,
+                                                                      const float* __restrict__ bias, int qcols,
+                                                                      float qscale, bf16* __restrict__ Y, long ldy,
+                                                                      bf16* __restrict__ P, long ldp) {
+  constexpr int CW = 48 * W, TLD = CW + 4, LPR = CW / 12;  // chunk width, T row stride, lanes per row
   __shared__ __attribute__((aligned(16))) char smem[RP_NS * RP_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * RP_MT;
-  const PanelA pa = panel_a_setup(A, lda, M, m0, wv, lane);
-  const int r = tid >> 5, c0 = (tid & 31) * 12;  // row phase: 32 lanes per row, 12 columns each
-  float* T = (float*)smem;                        // [16][RP_TLD] after the main loop
+  const int nch = N / CW;
+  int rp, nc_begin, nc_end;
+  if constexpr (W == 8) {
+    rp = xcd_remap(blockIdx.x, gridDim.x);
+    nc_begin = 0;
+    nc_end = nch;
+  } else {  // (panel, chunk) with the chunks of a panel adjacent: one XCD, the A panel in one L2
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
+    rp = id / nch;
+    nc_begin = id - rp * nch;
+    nc_end = nc_begin + 1;
+  }
+  const int m0 = rp * RP_MT;
+  const PanelA pa = panel_a_setup<W>(A, lda, M, m0, wv, lane);
+  const int r = tid / LPR, c0 = (tid % LPR) * 12;  // row phase: LPR lanes per row, 12 columns each
+  float* T = (float*)smem;                          // [16][TLD] after the main loop
 #pragma unroll 1
-  for (int nc = 0; nc < N / RP_N; ++nc) {
+  for (int nc = nc_begin; nc < nc_end; ++nc) {
     f32x4 acc[RP_MB][NBW];
-    panel_mainloop(acc, smem, pa, wpack, N / 16, nc * (RP_N / 16) + wv * NBW, K / 64, wv, lane);
+    panel_mainloop<W>(acc, smem, pa, wpack, N / 16, nc * (CW / 16) + wv * NBW, K / 64, wv, lane);
     __builtin_amdgcn_s_barrier();  // every wave is done with the A ring
-    const int n0 = nc * RP_N;
+    const int n0 = nc * CW;
     float bv[NBW];
 #pragma unroll
     for (int j = 0; j < NBW; ++j)
       bv[j] = (EPI != EPI_DGELU && bias) ? bias[n0 + (wv * NBW + j) * 16 + (lane & 15)] : 0.f;
-    const float qs = (EPI == EPI_QS && n0 < qcols) ? qscale : 1.f;  // qcols is a multiple of 384
+    const float qs = (EPI == EPI_QS && n0 < qcols) ? qscale : 1.f;  // qcols is a multiple of 384 (of CW)
     uint2 pv[3];
     auto load_pre = [&](int mb) {
       const int m = min(m0 + 16 * mb + r, M - 1);
@@ -342,13 +363,13 @@ __global__ __launch_bounds__(512, 1) void rowpanel_wide_kernel(const bf16* __res
       for (int j = 0; j < NBW; ++j)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          T[(4 * (lane >> 4) + i) * RP_TLD + (wv * NBW + j) * 16 + (lane & 15)] = acc[mb][j][i] + bv[j];
-      __builtin_amdgcn_s_barrier();
+          T[(4 * (lane >> 4) + i) * TLD + (wv * NBW + j) * 16 + (lane & 15)] = acc[mb][j][i] + bv[j];
+      lds_barrier();
       const int m = m0 + 16 * mb + r;
       float v[12];
 #pragma unroll
       for (int e = 0; e < 12; e += 4) {
-        const float4 tv = *(const float4*)(T + r * RP_TLD + c0 + e);
+        const float4 tv = *(const float4*)(T + r * TLD + c0 + e);
         v[e] = tv.x; v[e + 1] = tv.y; v[e + 2] = tv.z; v[e + 3] = tv.w;
       }
       float h[12];
@@ -458,13 +479,13 @@ extern "C" int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, lo
   IVIT_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)wpack & 15) == 0 && ((uintptr_t)Y & 7) == 0 &&
                      ((uintptr_t)Ypre & 7) == 0,
                  "ivit_linear_fwd_panel: misaligned operand");
-  const dim3 g(ivit_cdiv(M, RP_MT));
+  const dim3 g(ivit_cdiv(M, RP_MT) * (N / 192));
   hipStream_t st = ivit_stream(stream);
   if (act == IVIT_ACT_GELU)
-    hipLaunchKernelGGL(rowpanel_wide_kernel<EPI_GELU>, g, dim3(512), 0, st, (const bf16*)A, lda, (int)M, (int)K,
+    hipLaunchKernelGGL((rowpanel_wide_kernel<EPI_GELU, 4>), g, dim3(256), 0, st, (const bf16*)A, lda, (int)M, (int)K,
                        (const u32x4*)wpack, (int)N, bias, 0, 1.f, (bf16*)Y, ldy, (bf16*)Ypre, ldpre);
   else
-    hipLaunchKernelGGL(rowpanel_wide_kernel<EPI_QS>, g, dim3(512), 0, st, (const bf16*)A, lda, (int)M, (int)K,
+    hipLaunchKernelGGL((rowpanel_wide_kernel<EPI_QS, 4>), g, dim3(256), 0, st, (const bf16*)A, lda, (int)M, (int)K,
                        (const u32x4*)wpack, (int)N, bias, (int)qcols, qscale, (bf16*)Y, ldy, nullptr, 0L);
   IVIT_LAUNCH_CHECK();
   return 0;
@@ -480,7 +501,8 @@ extern "C" int ivit_linear_dgrad_gelu_panel(const void* dY, long lddy, long M, l
   IVIT_CHECK_ARG(((uintptr_t)dY & 15) == 0 && ((uintptr_t)wpack_t & 15) == 0 && ((uintptr_t)dX & 7) == 0 &&
                      ((uintptr_t)pre & 7) == 0,
                  "ivit_linear_dgrad_gelu_panel: misaligned operand");
-  hipLaunchKernelGGL(rowpanel_wide_kernel<EPI_DGELU>, dim3(ivit_cdiv(M, RP_MT)), dim3(512), 0, ivit_stream(stream),
+  hipLaunchKernelGGL((rowpanel_wide_kernel<EPI_DGELU, 4>), dim3(ivit_cdiv(M, RP_MT) * (N / 192)), dim3(256), 0,
+                     ivit_stream(stream),
                      (const bf16*)dY, lddy, (int)M, (int)K, (const u32x4*)wpack_t, (int)N, nullptr, 0, 1.f,
                      (bf16*)dX, lddx, (bf16*)pre, ldpre);
   IVIT_LAUNCH_CHECK();
