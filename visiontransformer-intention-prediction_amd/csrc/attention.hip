@@ -620,8 +620,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __r
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
   const bf16* Gb = dout + (long)b * N * D + h * 64;
-  const float* L = nlse2p + (long)z * Npad;
-  const float* Dl = ndeltap + (long)z * Npad;
+  const char* Ls = uniform_ptr(nlse2p + (long)z * Npad);
+  const char* Ds = uniform_ptr(ndeltap + (long)z * Npad);
   const int key = bid.x * AQ + wv * 32 + (lane & 31);
   bf16x8 kf[4], vf[4];
   load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
@@ -655,9 +655,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v3_kernel(const bf16* __r
       glds_s<false>(oq, qb, qimg + piece * 1024);
       glds_s<false>(og, gb, gimg + piece * 1024);
     }
-    if (wv == 0) {
-      glds4_s(4u * lane, uniform_ptr(L + qt * AK), &srow[S][0][0]);
-      glds4_s(4u * lane, uniform_ptr(Dl + qt * AK), &srow[S][1][0]);
+    if (wv == 0) {  // bases in SGPRs, the tile offset in the per-lane offset
+      glds4_s(4u * (lane + qt * AK), Ls, &srow[S][0][0]);
+      glds4_s(4u * (lane + qt * AK), Ds, &srow[S][1][0]);
     }
   };
 
