@@ -94,6 +94,27 @@ def pmc_traffic(kernel_prefix):
     return tot, os.path.relpath(files[-1], HERE)
 
 
+def isolated_attn_ms(name, B, N, H, dev, iters=20):
+    """Mean launch time of ivit_attn_fwd_q2 / ivit_attn_bwd_q2 alone at the bench shape."""
+    import ops
+    g = torch.Generator(device=dev).manual_seed(0)
+    qkv = torch.randn(B * N, 3 * H * 64, device=dev, generator=g).to(torch.bfloat16)
+    qkv[:, : H * 64] = (qkv[:, : H * 64].float() * ops.Q2_SCALE).to(torch.bfloat16)
+    dout = torch.randn(B * N, H * 64, device=dev, generator=g).to(torch.bfloat16)
+    o, lse = ops.attn_fwd_q2(qkv, B, N, H)
+    fn = (lambda: ops.attn_fwd_q2(qkv, B, N, H)) if name == "attn_fwd" else \
+        (lambda: ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H))
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
 def cpu_model_name():
     """lscpu's "Model name" (the first /proc/cpuinfo model name line)."""
     try:
@@ -302,6 +323,14 @@ def main():
                       "frac": round(fl_step / (el / args.steps) / 1e12 / peak, 4),
                       "flops_per_step_per_gpu": fl_step},
     }
+    if default_cfg and world == 1:
+        # the same kernel(s) alone on the same shape (outside the timed region): the frac without the
+        # other ViT stream's kernels sharing the CUs
+        iso = isolated_attn_ms(roof, B, N, 6, dev)
+        out["roofline"]["isolated"] = {"ms": round(iso, 4), "achieved": round(afl / (iso * 1e-3) / 1e12, 2),
+                                       "frac": round(afl / (iso * 1e-3) / 1e12 / peak, 4),
+                                       "note": "mean of 20 back-to-back launches on random bf16 inputs of the "
+                                               "bench shape (prescaled Q), HIP events, nothing else running"}
     if train:
         out["loss"] = loss_v
     else:
