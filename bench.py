@@ -45,13 +45,35 @@ def step_flops(B, H, W, depth=12, D=384, C_l=290, C_m=9, planes=512, A=5, K=8, a
 # The dominant kernels of the bf16 step (profiles/r02_*_bench_kernel_stats.csv): the attention
 # backward pair of ivit_attn_bwd_q2 (attn_bwd_dq_v3 + attn_bwd_dkv_v3, ~31 % of GPU time), then the
 # attention forward (ivit_attn_fwd_q2, ~13 %). The roofline object reports whichever of the two has
-# the larger measured time per step (HIP events on the launching stream, inside the timed loop).
+# the larger measured time per step: kernel execution time from HIP event pairs bound to the kernel
+# launches themselves (ivit_ktime_*: hipExtLaunchKernel start / stop events, the interval rocprofv3's
+# kernel trace reports), inside the timed loop. The stream-span figure (events recorded around the
+# launch on the launching stream) is reported beside it: it also counts time the kernel waited
+# behind the other ViT stream's kernels.
 ATTN = {
     "attn_bwd": {"kernels": ["attn_bwd_dq_v3_kernel", "attn_bwd_dkv_v3_kernel"], "entry": "ivit_attn_bwd_q2",
+                 "tags": (1, 2),
                  "flops_note": "8*B*H*N^2*64 (dQ, dK, dV, dP products; the S recompute is not counted)"},
-    "attn_fwd": {"kernels": ["attn_fwd_bf16_v6_kernel"], "entry": "ivit_attn_fwd_q2",
+    "attn_fwd": {"kernels": ["attn_fwd_bf16_v6_kernel"], "entry": "ivit_attn_fwd_q2", "tags": (0,),
                  "flops_note": "4*B*H*N^2*64 (QK^T, PV)"},
 }
+
+
+def kernel_exec_ms(ops, name):
+    """-> (busy ms per launch, mean kernel-sum ms per launch, launches) for one ATTN entry from its
+    kernels' recorded execution intervals (ivit_ktime_read, both ViT streams): busy = the union of
+    the intervals (time at least one of its kernels was executing) / launches — the device time per
+    launch when the two streams' launches overlap each other; the mean interval sum counts a
+    shared stretch once per launch."""
+    iv = []
+    n0 = None
+    for tag in ATTN[name]["tags"]:
+        r = ops.ktime_read(tag)
+        iv += r
+        n0 = len(r) if n0 is None else n0
+    if not n0:
+        return float("nan"), float("nan"), 0
+    return ops.busy_ms(iv) / n0, sum(b - a for a, b in iv) / n0, n0
 
 
 def attn_flops(name, B, N, H, Dh=64):
@@ -246,6 +268,7 @@ def main():
     torch.cuda.synchronize()
     ops.KernelTimer.enabled = set(ATTN)
     ops.KernelTimer.records = {}
+    ops.ktime_arm(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -256,8 +279,11 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    attn_ms = {k: ops.KernelTimer.mean_ms(k) for k in ATTN}
-    attn_n = {k: ops.KernelTimer.count(k) for k in ATTN}
+    ops.ktime_arm(False)
+    span_ms = {k: ops.KernelTimer.mean_ms(k) for k in ATTN}
+    kexec = {k: kernel_exec_ms(ops, k) for k in ATTN}
+    attn_ms = {k: kexec[k][0] for k in ATTN}
+    attn_n = {k: kexec[k][2] for k in ATTN}
     ops.KernelTimer.enabled = set()
     if world > 1:
         t = torch.tensor([el], device=dev)
@@ -306,8 +332,15 @@ def main():
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "per_launch": f"{ATTN[roof]['flops_note']} = {afl:.4g} flop (B={B}, H=6, N={N}); "
-                                   f"{attn_ms[roof]:.4f} ms avg over {attn_n[roof]} launches (HIP events on the "
-                                   f"launching stream; the other ViT stream runs concurrently)",
+                                   f"{attn_ms[roof]:.4f} ms of device time per launch = the union of the "
+                                   f"execution intervals of its kernels over {attn_n[roof]} launches (both ViT "
+                                   f"streams; hipExtLaunchKernel start/stop events bound to each kernel) / launches",
+                     "launch_ms": round(kexec[roof][1], 4),
+                     "launch_note": "mean execution interval of one launch (its kernels summed): when the two "
+                                    "streams' launches overlap, each one's interval covers the shared stretch",
+                     "stream_span_ms": round(span_ms[roof], 4),
+                     "stream_span_note": "events recorded before / after the entry point on its stream: also "
+                                         "counts the wait behind the other stream's kernels",
                      "traffic_note": (f"HBM bytes per launch from {traffic_src} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                                       f"gfx950-corrected, summed over the kernels); algorithmic bytes "
                                       f"{attn_bytes(roof, B, N, 6):.4g}")

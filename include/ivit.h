@@ -143,6 +143,19 @@ int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh, void* out
 int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* dout, const float* lse, long B, long N, long H,
                      long Dh, void* dqkv, void* work, long work_bytes, void* stream);
 
+/* ---- Kernel execution timing (bench.py's roofline figure; no reference counterpart).
+ * While armed, ivit_attn_fwd_q2 / ivit_attn_bwd_q2 launch through hipExtLaunchKernel with a
+ * start / stop event pair bound to the kernel itself: HIP stamps them at the kernel's own begin
+ * and end, not at submission, so kernels of a concurrent stream queued ahead of it do not count
+ * (the same interval rocprofv3 --kernel-trace reports). arm(1) clears the records and starts
+ * recording, arm(0) stops; read() waits for the recorded events of one tag and returns their
+ * launch count and, for the first min(count, cap), each kernel's start / stop in ms relative to
+ * the first recorded launch's start (a common origin for all tags, so intervals of kernels on
+ * concurrent streams can be merged).                                                          */
+enum { IVIT_KT_ATTN_FWD = 0, IVIT_KT_ATTN_BWD_DQ = 1, IVIT_KT_ATTN_BWD_DKV = 2, IVIT_KT_NTAGS = 3 };
+int ivit_ktime_arm(int on);
+int ivit_ktime_read(int tag, double* start_ms, double* stop_ms, long cap, long* count);
+
 /* ---- LayerNorm over the last dim D (timm norm1/norm2/norm eps 1e-6; adapters eps 1e-5).
  *      Input rows r -> (r / rpb) * rstride + roff + r % rpb (rpb = 0: identity) of X (f32).    */
 int ivit_layernorm_fwd(const float* X, long ldx, long rpb, long rstride, long roff, long M, long D,

@@ -189,6 +189,43 @@ def test_attention_q2_prescaled_path(B, N, H):
         assert _rel(d[:, i], g[:, i]) < 3e-2, ("qkv"[i], _rel(d[:, i], g[:, i]))
 
 
+def test_kernel_exec_timing_hook():
+    """ivit_ktime_*: armed launches go through hipExtLaunchKernel with kernel-bound events (one
+    record per kernel, outputs unchanged); the kernel intervals lie inside the stream's own span
+    and nothing is recorded once disarmed."""
+    import ops
+    B, N, H = 2, 1025, 2
+    qkv = torch.randn(B * N, 3 * H * 64, device=DEV).to(torch.bfloat16)
+    dod = torch.randn(B * N, H * 64, device=DEV).to(torch.bfloat16)
+    o0, l0 = ops.attn_fwd_q2(qkv, B, N, H)
+    d0 = ops.attn_bwd_q2(qkv, o0, dod, l0, B, N, H)
+    torch.cuda.synchronize()
+    ops.ktime_arm(True)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    o1, l1 = ops.attn_fwd_q2(qkv, B, N, H)
+    d1 = ops.attn_bwd_q2(qkv, o1, dod, l1, B, N, H)
+    e.record()
+    ops.ktime_arm(False)
+    ops.attn_fwd_q2(qkv, B, N, H)  # disarmed: not recorded
+    torch.cuda.synchronize()
+    assert torch.equal(o0, o1) and torch.equal(l0, l1) and torch.equal(d0, d1)
+    span = s.elapsed_time(e)
+    iv = []
+    for tag in (ops.KT_ATTN_FWD, ops.KT_ATTN_BWD_DQ, ops.KT_ATTN_BWD_DKV):
+        r = ops.ktime_read(tag)
+        assert len(r) == 1 and 0.0 < r[0][1] - r[0][0] <= span, (tag, r, span)
+        iv += r
+    # one stream: the fwd, dQ and dK/dV kernels run in order, from the common origin
+    assert iv[0][0] == 0.0 and all(a[1] <= b[0] + 1e-3 for a, b in zip(iv, iv[1:])), iv
+    assert abs(ops.busy_ms(iv) - sum(b - a for a, b in iv)) < 1e-6
+    assert iv[-1][1] <= span * 1.01, (iv, span)
+    assert ops.busy_ms([(0.0, 2.0), (1.0, 3.0), (5.0, 6.0)]) == 4.0
+    ops.ktime_arm(True)  # re-arming clears the records
+    ops.ktime_arm(False)
+    assert ops.ktime_read(ops.KT_ATTN_FWD) == []
+
+
 def test_attention_large_grid_bf16():
     """BASELINE config 5 sequence length (800x1440 grid: N = 100*180 + 1 = 18001), bf16 flash
     kernels vs an f32 torch reference on the device (scores materialised per head)."""

@@ -15,6 +15,11 @@
 //             matrix materialised in the workspace, plus row-softmax kernels.
 #include "attn_common.h"
 
+#include <hip/hip_ext.h>
+
+#include <mutex>
+#include <vector>
+
 namespace {
 
 // ------------------------------------------------------------------------- forward (bf16)
@@ -1170,6 +1175,85 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
   return 0;
 }
 
+// ------------------------------------------------------------------------- kernel timing
+// ivit_ktime_arm / _read (ivit.h): while armed, the q2 entry points launch through
+// hipExtLaunchKernel with an event pair bound to the kernel command, so the elapsed time is the
+// kernel's own execution interval. Events are pooled across arm() calls.
+namespace {
+struct KtRec {
+  int tag;
+  hipEvent_t start, stop;
+};
+std::mutex kt_mu;
+bool kt_on = false;
+std::vector<KtRec> kt_recs;
+std::vector<hipEvent_t> kt_pool;
+size_t kt_used = 0;
+
+hipEvent_t kt_event() {
+  if (kt_used == kt_pool.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    kt_pool.push_back(e);
+  }
+  return kt_pool[kt_used++];
+}
+
+// Launch through hipExtLaunchKernelGGL with a recorded event pair when armed, else plainly.
+template <typename K, typename... Args>
+void kt_launch(int tag, K kernel, dim3 g, dim3 b, hipStream_t st, Args... args) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(kt_mu);
+    if (kt_on) {
+      e0 = kt_event();
+      e1 = e0 ? kt_event() : nullptr;
+      if (e0 && e1) kt_recs.push_back({tag, e0, e1});
+    }
+  }
+  if (e0 && e1)
+    hipExtLaunchKernelGGL(kernel, g, b, 0, st, e0, e1, 0, args...);
+  else
+    hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
+}
+}  // namespace
+
+extern "C" int ivit_ktime_arm(int on) {
+  std::lock_guard<std::mutex> lk(kt_mu);
+  if (on) {
+    kt_recs.clear();
+    kt_used = 0;
+  }
+  kt_on = on != 0;
+  return 0;
+}
+
+extern "C" int ivit_ktime_read(int tag, double* start_ms, double* stop_ms, long cap, long* count) {
+  IVIT_CHECK_ARG(tag >= 0 && tag < IVIT_KT_NTAGS, "ivit_ktime_read: unknown tag %d", tag);
+  IVIT_CHECK_ARG(count && (cap == 0 || (start_ms && stop_ms)), "ivit_ktime_read: null output");
+  std::lock_guard<std::mutex> lk(kt_mu);
+  long n = 0;
+  for (const KtRec& r : kt_recs) {
+    if (r.tag != tag) continue;
+    // times relative to the first recorded launch's start event (all tags share it)
+    float t0 = 0.f, t1 = 0.f;
+    hipError_t e = hipEventSynchronize(r.stop);
+    if (e == hipSuccess) e = hipEventElapsedTime(&t0, kt_recs[0].start, r.start);
+    if (e == hipSuccess) e = hipEventElapsedTime(&t1, kt_recs[0].start, r.stop);
+    if (e != hipSuccess) {
+      ivit_set_error("ivit_ktime_read: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    if (n < cap) {
+      start_ms[n] = t0;
+      stop_ms[n] = t1;
+    }
+    ++n;
+  }
+  *count = n;
+  return 0;
+}
+
 // ------------------------------------------------------------------------- Q-prescaled bf16 path
 extern "C" int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh, void* out, float* lse, void* work,
                                 long work_bytes, void* stream) {
@@ -1178,8 +1262,8 @@ extern "C" int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh
   (void)work_bytes;
   if (B * N * H == 0) return 0;
   dim3 g(ivit_cdiv(N, 128), B * H);
-  hipLaunchKernelGGL((attn_fwd_bf16_v6_kernel<4, false>), g, dim3(256), 0, ivit_stream(stream), (const bf16*)qkv,
-                     (int)N, (int)H, (bf16*)out, lse, 1.0f);
+  kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream), (const bf16*)qkv,
+            (int)N, (int)H, (bf16*)out, lse, 1.0f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -1202,10 +1286,10 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   // independent workgroup to fill its gaps)
   constexpr int BW = 4;
   const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
-  hipLaunchKernelGGL((attn_bwd_dq_v3_kernel<BW>), gw, dim3(64 * BW), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
-                     deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
-  hipLaunchKernelGGL((attn_bwd_dkv_v3_kernel<BW>), gw, dim3(64 * BW), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
-                     deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
+  kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
+  kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

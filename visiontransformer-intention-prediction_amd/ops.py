@@ -13,7 +13,9 @@ plus single-op Functions used by the standalone module forwards.
 """
 from __future__ import annotations
 
+import ctypes
 import os
+
 import torch
 from torch.utils.weak import WeakIdKeyDictionary
 
@@ -217,6 +219,40 @@ class KernelTimer:
     @classmethod
     def count(cls, name):
         return len(cls.records.get(name, []))
+
+
+KT_ATTN_FWD, KT_ATTN_BWD_DQ, KT_ATTN_BWD_DKV = 0, 1, 2
+
+
+def ktime_arm(on):
+    """Start (clearing earlier records) / stop kernel-execution timing of the attention entry
+    points (ivit_ktime_arm: event pairs bound to the kernel commands themselves)."""
+    lib.ivit_ktime_arm(1 if on else 0)
+
+
+def ktime_read(tag):
+    """-> [(start_ms, stop_ms), ...] of every recorded kernel of one IVIT_KT_* tag since the
+    last arm, relative to the first recorded launch's start (common to all tags)."""
+    n = ctypes.c_long(0)
+    lib.ivit_ktime_read(tag, None, None, 0, ctypes.addressof(n))
+    if n.value == 0:
+        return []
+    t0, t1 = (ctypes.c_double * n.value)(), (ctypes.c_double * n.value)()
+    lib.ivit_ktime_read(tag, ctypes.addressof(t0), ctypes.addressof(t1), n.value, ctypes.addressof(n))
+    return list(zip(t0, t1))
+
+
+def busy_ms(intervals):
+    """Length of the union of [start, stop) intervals (time at least one of them was running)."""
+    tot, end = 0.0, None
+    for a, b in sorted(intervals):
+        if end is None or a > end:
+            tot += b - a
+            end = b
+        elif b > end:
+            tot += b - end
+            end = b
+    return tot
 
 
 def attn_fwd(qkv, B, N, H, cdt):
