@@ -49,10 +49,51 @@ __global__ void splitk_reduce2_kernel(const float* __restrict__ slab0, long n0, 
   out[i] = accumulate ? out[i] + s : s;
 }
 
+// The same with 16-B accesses (four consecutive outputs per thread, the splits' loads issued ahead
+// of the in-order sums): n0, n1 multiples of 4, every pointer 16-B aligned. Same summation order.
+__global__ void splitk_reduce2_v4_kernel(const float* __restrict__ slab0, long n0, float* __restrict__ out0,
+                                         const float* __restrict__ slab1, long n1, float* __restrict__ out1,
+                                         int splits, int accumulate) {
+  long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const float* sl = slab0;
+  float* out = out0;
+  long n = n0;
+  if (i >= n0) {
+    i -= n0;
+    sl = slab1;
+    out = out1;
+    n = n1;
+    if (i >= n1) return;
+  }
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+  for (int k = 0; k < splits; ++k) {
+    const float4 v = *(const float4*)(sl + (long)k * n + i);
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  if (accumulate) {
+    const float4 o = *(const float4*)(out + i);
+    s.x = o.x + s.x;
+    s.y = o.y + s.y;
+    s.z = o.z + s.z;
+    s.w = o.w + s.w;
+  }
+  *(float4*)(out + i) = s;
+}
+
 static int reduce_wgrad(hipStream_t st, const float* slab, long n, float* dW, const float* bslab, long nb, float* db,
                         int splits, int accumulate) {
-  hipLaunchKernelGGL(splitk_reduce2_kernel, dim3(ivit_cdiv(n + (bslab ? nb : 0), 256)), dim3(256), 0, st, slab, n, dW,
-                     bslab, bslab ? nb : 0, db, splits, accumulate);
+  const long n1 = bslab ? nb : 0;
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (n % 4 == 0 && n1 % 4 == 0 && al16(slab) && al16(dW) && (!n1 || (al16(bslab) && al16(db))))
+    hipLaunchKernelGGL(splitk_reduce2_v4_kernel, dim3(ivit_cdiv((n + n1) / 4, 256)), dim3(256), 0, st, slab, n, dW,
+                       bslab, n1, db, splits, accumulate);
+  else
+    hipLaunchKernelGGL(splitk_reduce2_kernel, dim3(ivit_cdiv(n + n1, 256)), dim3(256), 0, st, slab, n, dW, bslab, n1,
+                       db, splits, accumulate);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -115,6 +156,7 @@ static int splitk_choice(long tiles, long K, int bk) {
   for (int s = 1; s <= 128; ++s) {
     if (s > 1 && kt / s < 8.0) break;
     const double rounds = (double)((tiles * s + slots - 1) / slots);
+    // + 4 K steps of fixed cost per workgroup: 1 / 12 / 32 measured alike on the bench (48.65-48.83 ms)
     const double cost = rounds * (kt / s + 4.0);
     if (cost < best_cost - 1e-9) { best_cost = cost; best = s; }
   }
