@@ -109,6 +109,25 @@ int ivit_patch_embed_fwd_packed(const float* img, long B, long C, long H, long W
                                 const float* bias, const float* pos, const float* cls, long D, float* out,
                                 void* stream);
 
+/* ---- Differing patch grids (model_vit.py:64,71 with e.g. vit_small_patch16_224 for one stream,
+ *      and the bilinear re-grid of model_vit.py:139).
+ * PatchEmbed with patch P != 8 = patch matrix + ivit_linear_fwd + token assembly:
+ *   cols[b*Np + gy*Wp + gx][(c*P + ky)*P + kx] = img[b][c][gy*P + ky][gx*P + kx]  (cols_dtype)
+ *   out[b][0] = cls + pos[0];  out[b][1 + p] = Y[b*Np + p] + pos[1 + p]           (f32)
+ * tokens_bwd: dY[b*Np + p] = dtok[b][1 + p] (dy_dtype, the weight gradient's operand);
+ *   dpos (+)= sum_b dtok[b];  dcls (+)= sum_b dtok[b][0].                                    */
+int ivit_patch_im2col_p(const float* img, long B, long C, long H, long W, long P, void* cols, int cols_dtype,
+                        void* stream);
+int ivit_patch_tokens(const float* Y, long B, long Np, long D, const float* pos, const float* cls, float* out,
+                      void* stream);
+int ivit_patch_tokens_bwd(const void* dtok, int dtok_dtype, long B, long Np, long D, void* dY, int dy_dtype,
+                          float* dpos, float* dcls, int accumulate, void* stream);
+/* F.interpolate(x, size=(Ho, Wo), mode='bilinear', align_corners=False) on Z = B*C planes of
+ * Hi x Wi f32 (ATen's linear taps: src = max((o + 0.5) * in/out - 0.5, 0)), and its adjoint
+ * dX = R_h^T dY R_w as a gather (deterministic, no atomics; dX is overwritten).             */
+int ivit_bilinear_fwd(const float* X, long Z, long Hi, long Wi, float* Y, long Ho, long Wo, void* stream);
+int ivit_bilinear_bwd(const float* dY, long Z, long Hi, long Wi, long Ho, long Wo, float* dX, void* stream);
+
 /* ---- k x k stride-1 "same" convolution on NHWC maps (BasicBlock conv3x3/conv1x1,
  *      model_vit.py:12-17; DetectionHead/IntentionHead conv, heads.py:16,37; k = 5: model_cnn.py:7-9).
  *      Weights packed [Cout][k][k][Cin] (see ivit_pack_conv_weight).                           */

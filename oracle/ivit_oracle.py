@@ -143,6 +143,8 @@ def intentnet_forward(sd, lidar, map_bev, cfg, training=False, drop_path_scales=
         dl, dm = drop_path_scales
     fl = _stream(sd, "lidar", lidar, al["num_heads"], depth_l, dl, attn, checkpoint)
     fm = _stream(sd, "map", map_bev, am["num_heads"], depth_m, dm, attn, checkpoint)
+    if fm.shape[2:] != fl.shape[2:]:  # model_vit.py:139: differing patch grids
+        fm = F.interpolate(fm, size=fl.shape[2:], mode="bilinear", align_corners=False)
     feat = fusion_forward(sd, torch.cat([fl, fm], dim=1), cfg["layers"], training, cfg.get("fusion_stride", 1))
     return heads_forward(sd, feat, cfg["num_anchors"], cfg["num_classes"])
 

@@ -147,6 +147,61 @@ def gen_model_stride2():
     print("model_stride2: cls", c.shape, "loss", rec["train_loss"])
 
 
+def gen_model_regrid():
+    """The reference's OWN IntentNetViT with a patch-16 map ViT (vit_small_patch16_224 at
+    model_vit.py:71): the map grid (2 x 3 at 32x48) differs from the LiDAR grid (4 x 6), so the
+    forward re-grids the map features bilinearly (:139). Eval + train outputs, loss, gradient
+    samples; plus a standalone F.interpolate case (up and down) for the resize kernel."""
+    import loss as ref_loss
+    import model_vit as ref_model
+    import utils as ref_utils
+    cfg = model_cfg(img_size=SMALL_IMG, vit_map="vit_small_patch16_224")
+    sd = make_state_dict(cfg, seed=0)
+    lidar, mp, _ = O.synthetic_batch(2, SMALL_IMG, seed=1234)
+    gts = small_gt()
+    anchors = ref_utils.generate_anchors(SMALL_IMG[0], SMALL_IMG[1], 8)
+    m = ref_model.IntentNetViT(backbone_cfg={"img_size": SMALL_IMG, "lidar_input_channels": 290,
+                                             "map_input_channels": 9, "drop_path_rate_lidar": 0.0,
+                                             "drop_path_rate_map": 0.0,
+                                             "vit_model_name_map": "vit_small_patch16_224"})
+    assert m.backbone.map_grid_size != m.backbone.lidar_grid_size
+    m.load_state_dict(refshim.timm_to_hf_state(sd), strict=True)
+    rec = {"cfg": json.dumps(cfg), "anchors": anchors.numpy()}
+    m.eval()
+    with torch.no_grad():
+        c, b, it = m(lidar, mp)
+    rec.update(eval_cls=c.numpy(), eval_box=b.numpy(), eval_int=it.numpy())
+    m.train()
+    c, b, it = m(lidar, mp)
+    d = ref_loss.DetectionIntentionLoss(apply_intention_downsampling=False)(c, b, it, anchors, gts)
+    d["loss"].backward()
+    rec.update(train_cls=c.detach().numpy(), train_box=b.detach().numpy(), train_int=it.detach().numpy(),
+               train_loss=np.array([float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]),
+                                    float(d["intent_loss"]), float(d["num_pos_anchors"])]))
+    grads = refshim.hf_grads_to_timm({k: p.grad for k, p in m.named_parameters() if p.grad is not None})
+    names = sorted(grads)
+    samples, strides = zip(*[_sample(grads[k]) for k in names])
+    rec.update(grad_names=np.array(names), grad_abssum=np.array([float(grads[k].double().abs().sum()) for k in names]),
+               grad_samples=np.stack(samples), grad_strides=np.array(strides))
+    bn = {k: v for k, v in m.state_dict().items() if "running_" in k}
+    rec.update(bn_names=np.array(sorted(bn)), bn_values=np.stack([bn[k].numpy() for k in sorted(bn)]))
+    osd = {k: v.clone() for k, v in sd.items()}
+    with torch.no_grad():
+        oc, _, _ = O.intentnet_forward(osd, lidar, mp, cfg, training=False)
+    assert float((oc - torch.from_numpy(rec["eval_cls"])).abs().max()) < 1e-4, "oracle != reference (re-grid)"
+    # standalone resize cases: (Hi, Wi) -> (Ho, Wo), upsampling (the model's 2x) and ragged / down
+    g = torch.Generator().manual_seed(77)
+    for tag, (hi, wi, ho, wo) in {"up": (25, 45, 50, 90), "odd": (7, 5, 12, 13), "down": (9, 11, 4, 6)}.items():
+        x = torch.randn(2, 3, hi, wi, generator=g, requires_grad=True)
+        y = torch.nn.functional.interpolate(x, size=(ho, wo), mode="bilinear", align_corners=False)
+        dy = torch.randn(y.shape, generator=g)
+        y.backward(dy)
+        rec.update({f"resize_{tag}_x": x.detach().numpy(), f"resize_{tag}_y": y.detach().numpy(),
+                    f"resize_{tag}_dy": dy.numpy(), f"resize_{tag}_dx": x.grad.numpy()})
+    np.savez_compressed(os.path.join(OUT, "model_regrid.npz"), **rec)
+    print("model_regrid: cls", c.shape, "loss", rec["train_loss"])
+
+
 def gen_geometry():
     import loss as ref_loss
     import utils as ref_utils
@@ -569,3 +624,4 @@ if __name__ == "__main__":
     gen_loss_options()
     gen_map_raster()
     gen_model_stride2()
+    gen_model_regrid()

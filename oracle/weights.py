@@ -19,6 +19,8 @@ import torch
 VIT_ARCH = {
     "vit_small_patch8_224": dict(embed_dim=384, depth=12, num_heads=6, patch=8, mlp_ratio=4),
     "vit_tiny_patch8_224": dict(embed_dim=192, depth=12, num_heads=3, patch=8, mlp_ratio=4),
+    "vit_small_patch16_224": dict(embed_dim=384, depth=12, num_heads=6, patch=16, mlp_ratio=4),
+    "vit_tiny_patch16_224": dict(embed_dim=192, depth=12, num_heads=3, patch=16, mlp_ratio=4),
 }
 
 

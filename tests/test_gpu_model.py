@@ -97,6 +97,56 @@ def test_fusion_stride2_vs_golden(cd):
         np.testing.assert_allclose(bufs[str(name)].cpu().numpy(), val, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+def test_regrid_patch16_map_vs_golden(cd):
+    """A patch-16 map ViT (vit_small_patch16_224 at model_vit.py:71): generic patch embedding
+    (ivit_patch_im2col_p + linear + ivit_patch_tokens), the map features re-gridded onto the LiDAR
+    grid by ivit_bilinear_fwd (model_vit.py:139), the bilinear adjoint in backward — eval and
+    train outputs, loss, parameter gradients and BN running stats vs the reference's own model
+    (f32: 1e-3 rel; bf16: outputs within 6e-2)."""
+    import loss as L
+    import model_vit
+    import utils
+    z = golden("model_regrid.npz")
+    cfg = json.loads(str(z["cfg"]))
+    cfg["img_size"] = tuple(cfg["img_size"])
+    with pytest.warns(UserWarning, match="differ"):
+        m = model_vit.IntentNetViT(backbone_cfg={"img_size": cfg["img_size"], "drop_path_rate_lidar": 0.0,
+                                                 "drop_path_rate_map": 0.0,
+                                                 "vit_model_name_map": "vit_small_patch16_224"})
+    assert m.backbone.map_grid_size == (2, 3) and m.backbone.lidar_grid_size == (4, 6)
+    assert m.effective_head_stride == 8
+    m.load_state_dict(make_state_dict(cfg, seed=0), strict=True)
+    m = m.to(DEV).set_compute_dtype(cd)
+    lidar, mp, _ = O.synthetic_batch(2, cfg["img_size"], seed=1234)
+    tol = 1e-3 if cd == torch.float32 else 6e-2
+    m.eval()
+    with torch.no_grad():
+        c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    assert c.shape == (2, 120, 1) and b.shape == (2, 120, 6) and i.shape == (2, 120, 8)
+    assert _rel(c, z["eval_cls"]) < tol and _rel(b, z["eval_box"]) < tol and _rel(i, z["eval_int"]) < tol
+    m.train()
+    c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    assert _rel(c.detach(), z["train_cls"]) < tol
+    anchors = utils.generate_anchors(*cfg["img_size"], 8)
+    assert np.array_equal(anchors.cpu().numpy(), z["anchors"])
+    d = L.DetectionIntentionLoss(apply_intention_downsampling=False)(c, b, i, anchors, _gts(golden("model_small.npz"), 2))
+    got = [float(d["loss"]), float(d["cls_loss"]), float(d["box_loss"]), float(d["intent_loss"]),
+           float(d["num_pos_anchors"])]
+    np.testing.assert_allclose(got, z["train_loss"], rtol=1e-3 if cd == torch.float32 else 5e-2)
+    if cd != torch.float32:
+        return
+    d["loss"].backward()
+    sd = dict(m.named_parameters())
+    for name, gas, smp, st in zip(z["grad_names"], z["grad_abssum"], z["grad_samples"], z["grad_strides"]):
+        g = sd[str(name)].grad
+        assert g is not None, name
+        assert float(g.double().abs().sum()) == pytest.approx(gas, rel=1e-3, abs=1e-6), name
+    bufs = dict(m.named_buffers())
+    for name, val in zip(z["bn_names"], z["bn_values"]):
+        np.testing.assert_allclose(bufs[str(name)].cpu().numpy(), val, rtol=1e-4, atol=1e-5)
+
+
 def test_small_train_loss_grads_vs_golden(small):
     import loss as L
     import utils

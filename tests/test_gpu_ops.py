@@ -226,6 +226,52 @@ def test_kernel_exec_timing_hook():
     assert ops.ktime_read(ops.KT_ATTN_FWD) == []
 
 
+@pytest.mark.parametrize("tag", ["up", "odd", "down"])
+def test_bilinear_resize_vs_golden(tag):
+    """ivit_bilinear_fwd / _bwd vs F.interpolate(bilinear, align_corners=False) and its autograd
+    adjoint, run by the reference's torch (tests/golden/model_regrid.npz: the model's 2x
+    upsampling, a ragged upsampling and a downsampling)."""
+    import ops
+    from conftest import golden
+    z = golden("model_regrid.npz")
+    x = torch.from_numpy(z[f"resize_{tag}_x"]).to(DEV)
+    y = ops.bilinear_fwd(x, z[f"resize_{tag}_y"].shape[2:])
+    np.testing.assert_allclose(y.cpu().numpy(), z[f"resize_{tag}_y"], rtol=1e-6, atol=1e-6)
+    dx = ops.bilinear_bwd(torch.from_numpy(z[f"resize_{tag}_dy"]).to(DEV), x.shape[2:])
+    np.testing.assert_allclose(dx.cpu().numpy(), z[f"resize_{tag}_dx"], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C,H,W,D", [(2, 9, 32, 48, 384), (1, 290, 64, 96, 384), (3, 5, 16, 80, 192)])
+def test_patch_embed_patch16(cd, B, C, H, W, D):
+    """PatchEmbed with patch 16 (ivit_patch_im2col_p + linear + ivit_patch_tokens, and the
+    backward's ivit_patch_tokens_bwd + weight gradient) vs F.conv2d(k = s = 16) + CLS + pos_embed
+    in f64 (f32 path: 1e-5; bf16: vs f64 of the same bf16-rounded operands)."""
+    import ops
+    from _lib import BF16, F32
+    cdt = BF16 if cd == torch.bfloat16 else F32
+    img = torch.rand(B, C, H, W)
+    w = torch.randn(D, C, 16, 16) / math.sqrt(C * 256)
+    b, pos, cls = torch.randn(D) * 0.1, torch.randn(1, (H // 16) * (W // 16) + 1, D) * 0.1, torch.randn(1, 1, D)
+    wd = w.to(DEV).requires_grad_(True)
+    out = ops.PatchEmbedFn.apply(img.to(DEV), wd, b.to(DEV), pos.to(DEV), cls.to(DEV), cdt)
+    imr, wr = img.double(), w.double()
+    if cd == torch.bfloat16:
+        imr, wr = img.bfloat16().double(), w.bfloat16().double()
+    imr.requires_grad_(False)
+    wr.requires_grad_(True)
+    br, pr, cr = b.double().requires_grad_(True), pos.double().requires_grad_(True), cls.double().requires_grad_(True)
+    t = F.conv2d(imr, wr, br, stride=16).flatten(2).transpose(1, 2)
+    ref = (torch.cat([cr.expand(B, -1, -1), t], 1) + pr).reshape(B * t.shape[1] + B, D)
+    tol = 1e-5 if cd == torch.float32 else 2e-5
+    assert _rel(out, ref.detach()) < tol
+    g = torch.randn(out.shape)
+    out.backward(g.to(DEV))
+    gr = g.double() if cd == torch.float32 else g.bfloat16().double()
+    ref.backward(gr)
+    assert _rel(wd.grad, wr.grad) < (1e-5 if cd == torch.float32 else 1e-4)
+
+
 def test_attention_large_grid_bf16():
     """BASELINE config 5 sequence length (800x1440 grid: N = 100*180 + 1 = 18001), bf16 flash
     kernels vs an f32 torch reference on the device (scores materialised per head)."""

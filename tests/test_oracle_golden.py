@@ -259,3 +259,27 @@ def test_fusion_stride2_oracle_vs_golden():
     d = O.detection_loss(c, b, i, torch.from_numpy(z["anchors"]), _gts(golden("model_small.npz"), 2),
                          downsampling=False)
     np.testing.assert_allclose(_vec(d), z["train_loss"], rtol=1e-5)
+
+
+def test_regrid_oracle_vs_golden():
+    """Patch-16 map ViT (vit_small_patch16_224, model_vit.py:71): the map grid differs from the
+    LiDAR grid and the oracle re-grids bilinearly (:139) — vs the reference's own model; and the
+    standalone F.interpolate cases the resize kernel is tested against."""
+    z = golden("model_regrid.npz")
+    cfg = json.loads(str(z["cfg"]))
+    cfg["img_size"] = tuple(cfg["img_size"])
+    assert cfg["vit_map"] == "vit_small_patch16_224"
+    sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v.clone())
+          for k, v in make_state_dict(cfg, seed=0).items()}
+    lidar, mp, _ = O.synthetic_batch(2, cfg["img_size"], seed=1234)
+    c, b, i = O.intentnet_forward(sd, lidar, mp, cfg, training=True)
+    np.testing.assert_allclose(c.detach().numpy(), z["train_cls"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(i.detach().numpy(), z["train_int"], rtol=1e-4, atol=1e-4)
+    d = O.detection_loss(c, b, i, torch.from_numpy(z["anchors"]), _gts(golden("model_small.npz"), 2),
+                         downsampling=False)
+    np.testing.assert_allclose(_vec(d), z["train_loss"], rtol=1e-5)
+    for tag in ("up", "odd", "down"):
+        x = torch.from_numpy(z[f"resize_{tag}_x"])
+        y = torch.nn.functional.interpolate(x, size=z[f"resize_{tag}_y"].shape[2:], mode="bilinear",
+                                            align_corners=False)
+        np.testing.assert_array_equal(y.numpy(), z[f"resize_{tag}_y"])

@@ -77,11 +77,8 @@ class TwoStreamViTBackbone(nn.Module):
         self.map_num_prefix_tokens = self.vit_map.num_prefix_tokens
         self.map_grid_size = tuple(self.vit_map.patch_embed.grid_size)
         if self.lidar_grid_size != self.map_grid_size:
-            # model_vit.py:139 re-grids the map features bilinearly when the grids differ; with the
-            # patch-8 ViTs this build provides (vit.VIT_ARCH) and one img_size they never do
-            raise NotImplementedError("ivit: LiDAR and map patch grids must match (both streams use patch-8 "
-                                      "ViTs on the same img_size; the bilinear re-grid of model_vit.py:139 "
-                                      "is unreachable)")
+            # model_vit.py:76-77; forward re-grids the map features bilinearly (:139)
+            warnings.warn(f"LiDAR patch grid {self.lidar_grid_size} and Map patch grid {self.map_grid_size} differ.")
         self.feature_map_grid_h, self.feature_map_grid_w = self.lidar_grid_size
         self.adapter_lidar = nn.Sequential(LayerNorm(self.lidar_embed_dim),
                                            Linear(self.lidar_embed_dim, lidar_adapter_out_channels), GELU())
@@ -151,23 +148,33 @@ class TwoStreamViTBackbone(nn.Module):
         tm.record_stream(main)
         return tl, tm
 
+    @property
+    def generic_neck(self):
+        """The module-by-module neck (features_generic) instead of the fused NeckFn: for
+        fusion_block_stride != 1 and for differing LiDAR / map patch grids."""
+        return self.fusion_block_stride != 1 or self.lidar_grid_size != self.map_grid_size
+
     def features_generic(self, tl, tm, B):
         """model_vit.py:116-142 through the modules' own forwards (final norm, adapter LN ->
-        Linear -> GELU, token -> map, fusion BasicBlocks with their strides): the path for
-        fusion_block_stride != 1, whose strided block-0 convs run as im2col + GEMM."""
-        Hf, Wf = self.feature_map_grid_h, self.feature_map_grid_w
+        Linear -> GELU, token -> map, the map features re-gridded bilinearly onto the LiDAR grid
+        when the grids differ (:139, ops.BilinearFn), fusion BasicBlocks with their strides): the
+        path for fusion_block_stride != 1 (strided block-0 convs as im2col + GEMM) and for
+        differing patch grids."""
         maps = []
         for vitm, adapter, t in ((self.vit_lidar, self.adapter_lidar, tl), (self.vit_map, self.adapter_map, tm)):
             D = vitm.embed_dim
+            Hf, Wf = vitm.patch_embed.grid_size
             x = _LayerNormFn.apply(t, vitm.norm.weight, vitm.norm.bias, 1e-6).reshape(B, -1, D)
             y = adapter(x[:, vitm.num_prefix_tokens:])
             maps.append(y.permute(0, 2, 1).reshape(B, -1, Hf, Wf))
+        if maps[1].shape[2:] != maps[0].shape[2:]:
+            maps[1] = ops.BilinearFn.apply(maps[1], tuple(maps[0].shape[2:]))
         return self.fusion_block(torch.cat(maps, 1))
 
     def forward(self, lidar_bev, map_bev):
         """model_vit.py:134-142 → fused feature map (B, C, Hf', Wf') f32."""
         tl, tm = self.stream_tokens(lidar_bev, map_bev)
-        if self.fusion_block_stride != 1:
+        if self.generic_neck:
             return self.features_generic(tl, tm, lidar_bev.shape[0])
         names = self.neck_names()
         tens = _lookup(self, names)
@@ -246,7 +253,7 @@ class IntentNetViT(nn.Module):
         """model_vit.py:179-185 → cls (B, A*Hf*Wf, 1), box (.., 6), intent (.., K), all f32."""
         B = lidar_bev.shape[0]
         tl, tm = self.backbone.stream_tokens(lidar_bev, map_bev)
-        if self.backbone.fusion_block_stride != 1:  # strided fusion: module forwards, heads at H/s x W/s
+        if self.backbone.generic_neck:  # strided fusion / differing grids: module forwards, heads at H/s x W/s
             f = self.backbone.features_generic(tl, tm, B)
             c, b = self.det_head(f)
             it = self.intention_head(f)

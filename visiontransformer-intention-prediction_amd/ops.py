@@ -255,6 +255,41 @@ def busy_ms(intervals):
     return tot
 
 
+def bilinear_fwd(x, size):
+    """F.interpolate(x, size, mode='bilinear', align_corners=False) of an f32 (B, C, Hi, Wi) map
+    (ivit_bilinear_fwd; model_vit.py:139)."""
+    B, C, Hi, Wi = x.shape
+    Ho, Wo = size
+    x = x.contiguous()
+    y = torch.empty((B, C, Ho, Wo), dtype=torch.float32, device=x.device)
+    lib.ivit_bilinear_fwd(ptr(x), B * C, Hi, Wi, ptr(y), Ho, Wo, stream())
+    return y
+
+
+def bilinear_bwd(dy, in_size):
+    """Adjoint of bilinear_fwd (ivit_bilinear_bwd): dX (B, C, Hi, Wi) from dY (B, C, Ho, Wo)."""
+    B, C, Ho, Wo = dy.shape
+    Hi, Wi = in_size
+    dy = dy.contiguous()
+    dx = torch.empty((B, C, Hi, Wi), dtype=torch.float32, device=dy.device)
+    lib.ivit_bilinear_bwd(ptr(dy), B * C, Hi, Wi, Ho, Wo, ptr(dx), stream())
+    return dx
+
+
+class BilinearFn(torch.autograd.Function):
+    """The map features re-gridded onto the LiDAR grid when the two patch grids differ
+    (model_vit.py:139: F.interpolate(..., mode='bilinear', align_corners=False))."""
+
+    @staticmethod
+    def forward(ctx, x, size):
+        ctx.in_size = tuple(x.shape[2:])
+        return bilinear_fwd(x.float(), size)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return bilinear_bwd(dy.float(), ctx.in_size), None
+
+
 def attn_fwd(qkv, B, N, H, cdt):
     D = H * 64
     out = torch.empty((B * N, D), dtype=qkv.dtype, device=qkv.device)
@@ -447,6 +482,22 @@ class PatchEmbedFn(torch.autograd.Function):
     def forward(ctx, img, w, b, pos, cls, cdt):
         B, C, H, W = img.shape
         D = w.shape[0]
+        P = w.shape[-1]
+        if P != 8:
+            # other patch sizes (timm vit_*_patch16_224 at model_vit.py:64,71): patch matrix in the
+            # compute dtype, the linear GEMM, then the CLS / pos_embed assembly (ivit_patch_*)
+            Np = (H // P) * (W // P)
+            cols = torch.empty((B * Np, C * P * P), dtype=tdtype(cdt), device=img.device)
+            lib.ivit_patch_im2col_p(ptr(img), B, C, H, W, P, ptr(cols), cdt, stream())
+            y, _ = linear_fwd(cols, cast_weight(w, tdtype(cdt)).reshape(D, C * P * P), b, cdt,
+                              out_dtype=torch.float32)
+            out = torch.empty((B * (Np + 1), D), dtype=torch.float32, device=img.device)
+            lib.ivit_patch_tokens(ptr(y), B, Np, D, ptr(pos), ptr(cls), ptr(out), stream())
+            ctx.save_for_backward(cols)
+            ctx.meta = (B, C, H, W, D, cdt, w.shape)
+            ctx.generic = True
+            return out
+        ctx.generic = False
         Ntok = (H // 8) * (W // 8) + 1
         wc = cast_weight(w, tdtype(cdt)).reshape(D, C * 64)
         out = torch.empty((B * Ntok, D), dtype=torch.float32, device=img.device)
@@ -479,6 +530,16 @@ class PatchEmbedFn(torch.autograd.Function):
     def backward(ctx, dtok):
         (src,) = ctx.saved_tensors
         B, C, H, W, D, cdt, wshape = ctx.meta
+        if ctx.generic:
+            P = wshape[-1]
+            Np = (H // P) * (W // P)
+            dtok = dtok.contiguous()
+            dy = torch.empty((B * Np, D), dtype=tdtype(cdt), device=src.device)
+            dpos = torch.empty((1, Np + 1, D), dtype=torch.float32, device=src.device)
+            dcls = torch.empty((1, 1, D), dtype=torch.float32, device=src.device)
+            lib.ivit_patch_tokens_bwd(ptr(dtok), dt(dtok), B, Np, D, ptr(dy), cdt, ptr(dpos), ptr(dcls), 0, stream())
+            dw, db = linear_wgrad(dy, src, cdt)
+            return None, dw.reshape(wshape), db, dpos, dcls, None
         dtok = cast(dtok.contiguous(), tdtype(cdt))
         Ntok = (H // 8) * (W // 8) + 1
         dw = torch.empty(wshape, dtype=torch.float32, device=src.device)

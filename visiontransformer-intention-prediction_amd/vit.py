@@ -1,7 +1,7 @@
 """timm-compatible VisionTransformer stream (the object ``timm.create_model`` returns at
 model_vit.py:64,71): same attribute surface (``patch_embed.grid_size``, ``num_prefix_tokens``,
 ``embed_dim``, ``cls_token``, assignable ``head``, ``forward_features``) and the same
-``state_dict`` keys as timm's ``vit_{small,tiny}_patch8_224``, so reference checkpoints load.
+``state_dict`` keys as timm's ``vit_{small,tiny}_patch{8,16}_224``, so reference checkpoints load.
 Compute runs in ``ops.PatchEmbedFn`` + ``ops.ViTBlockFn`` (HIP)."""
 from __future__ import annotations
 
@@ -17,6 +17,10 @@ from layers import Conv2d, LayerNorm, Linear, _LayerNormFn
 VIT_ARCH = {
     "vit_small_patch8_224": dict(embed_dim=384, depth=12, num_heads=6, patch=8, mlp_ratio=4),
     "vit_tiny_patch8_224": dict(embed_dim=192, depth=12, num_heads=3, patch=8, mlp_ratio=4),
+    # patch-16 variants (timm registry): a stream built from one of these has a coarser grid, which
+    # model_vit.py:139 re-grids bilinearly onto the LiDAR grid (ops.BilinearFn)
+    "vit_small_patch16_224": dict(embed_dim=384, depth=12, num_heads=6, patch=16, mlp_ratio=4),
+    "vit_tiny_patch16_224": dict(embed_dim=192, depth=12, num_heads=3, patch=16, mlp_ratio=4),
 }
 
 
