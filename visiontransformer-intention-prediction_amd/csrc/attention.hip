@@ -79,9 +79,12 @@ IVIT_DEV void qk_tile_c(const char* kimg, const bf16x8 (&qf)[4], const f32x16& i
   }
 }
 
+// kbase = the next tile's first key; when it is the ragged last tile (or past the end) its keys
+// >= N are set to NEG_BIG before the row max (a uniform branch), so their P = exp2(.) is 0 in the
+// next step.
 IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], const f32x16 (&cur)[2],
                                 f32x16 (&nxt)[2], f32x16& o0, f32x16& o1, f32x16& lacc, const bf16x8& ones,
-                                const f32x16& negm, int lane) {
+                                const f32x16& negm, int lane, int kbase, int N) {
   const int hl = lane >> 5;
   auto kfrag = [&](int i) {
     return *(const bf16x8*)(kimg + t_off(32 * (i >> 2) + (lane & 31), 2 * (i & 3) + hl));
@@ -121,6 +124,15 @@ IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8
     __builtin_amdgcn_sched_barrier(0);
   }
   float a = NEG_BIG, bm = NEG_BIG;
+  if (kbase + AK > N) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        nxt[t][r] = key >= N ? NEG_BIG : nxt[t][r];
+      }
+  }
 #pragma unroll
   for (int k = 6; k < 12; ++k) {
     const int g = k / 3, which = k % 3;
@@ -226,58 +238,28 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
       for (int r = 0; r < 16; ++r) asm volatile("v_sub_f32 %0, %0, %1" : "+v"(negm[r]) : "v"(d));
     }
   };
-  auto body = [&](auto stage, auto nxmode, int j, f32x16(&cur)[2], f32x16(&nxt)[2]) {
+  // One key tile per body, all through the one fenced step; the next tile's keys past N are
+  // masked inside it (the S' of a tile past the end is computed from the stale K stage and
+  // discarded). A separate unfenced tail body (round 2) raised the kernel's register demand past
+  // 256: 68 VGPRs spilled in the prologue (PMC: ~100 MB of scratch writes per launch).
+  auto body = [&](auto stage, int j, f32x16(&cur)[2], f32x16(&nxt)[2]) {
     constexpr int S = decltype(stage)::value;  // V_j in smem[S][1], K_{j+1} in smem[S^1][0]
-    constexpr int NX = decltype(nxmode)::value;
-    const bool more = NX == 1 || j + 1 < nt;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (j + 2 < nt) issue1(Kb, j + 2, smem[S][0]);
-    if (more) issue1(Vb, j + 1, smem[S ^ 1][1]);
-    if constexpr (NX == 1) {
-      rescale(fwd_step_fenced6(smem[S ^ 1][0], smem[S][1], qf, cur, nxt, o0, o1, lacc, ones, negm, lane), nxt);
-      return;
-    }
-    if (more) qk_tile_c(smem[S ^ 1][0], qf, negm, nxt, lane);
-    bf16x8 p[4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        bf16x8 v;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (bf16)fast_exp2(cur[t][8 * ss + e]);
-        p[2 * t + ss] = v;
-      }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const int rb = 32 * t + 16 * ss;
-        const bf16x8 va0 = tr_acc_order(smem[S][1], rb, 0, lane);
-        const bf16x8 va1 = tr_acc_order(smem[S][1], rb, 32, lane);
-        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, p[2 * t + ss], o0, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, p[2 * t + ss], o1, 0, 0, 0);
-        lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[2 * t + ss], lacc, 0, 0, 0);
-      }
-    if (more) {
-      const float mt = NX == 1 || j + 1 < nfull ? tile_rowmax<false>(nxt, (j + 1) * AK, N, lane)
-                                                : tile_rowmax<true>(nxt, (j + 1) * AK, N, lane);
-      rescale(mt, nxt);
-    }
+    if (j + 1 < nt) issue1(Vb, j + 1, smem[S ^ 1][1]);
+    rescale(fwd_step_fenced6(smem[S ^ 1][0], smem[S][1], qf, cur, nxt, o0, o1, lacc, ones, negm, lane, (j + 1) * AK,
+                             N),
+            nxt);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  using I3 = std::integral_constant<int, 3>;
   int j = 0;
-  for (; j + 2 < nfull; j += 2) {
-    body(I0{}, I1{}, j, sc, sn);
-    body(I1{}, I1{}, j + 1, sn, sc);
+  for (; j + 1 < nt; j += 2) {
+    body(I0{}, j, sc, sn);
+    body(I1{}, j + 1, sn, sc);
   }
-  for (; j < nt; ++j) {
-    if (j & 1) body(I1{}, I3{}, j, sn, sc);
-    else body(I0{}, I3{}, j, sc, sn);
-  }
+  if (j < nt) body(I0{}, j, sc, sn);
   // epilogue: register 4g+e of o0 / o1 is dim 8g + 4hl + e (+32) of query q. One
   // v_permlane32_swap per word pairs lane q's half-block with lane q+32's, so each lane holds
   // 8 contiguous dims: lanes < 32 blocks g+1, lanes >= 32 blocks g (g even) — 16-B stores, 32
