@@ -305,6 +305,95 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(int mode, const void* X
   }
 }
 
+// The same partials with 8 consecutive columns per thread (16-B bf16 / 2 x 16-B f32 loads) and
+// the row loop unrolled, so several rows' loads are in flight per thread (the scalar form issued
+// one 2-B load per lane per dependent add: latency-bound). Same per-column summation order as
+// bn_partial_kernel (rows r0 + ph + 4k in sequence, then phases 0..3), so identical results.
+// C % 8 == 0; 512 columns x 4 row phases per 256-thread block.
+IVIT_DEV void ld8v(const void* p, int dt, long i, float (&x)[8]) {
+  if (dt == IVIT_BF16) load8f<bf16>((const bf16*)p + i, x, 8);
+  else load8f<float>((const float*)p + i, x, 8);
+}
+__global__ __launch_bounds__(256) void bn_partial8_kernel(int mode, const void* X, int xdt, const void* Y, int ydt,
+                                                          const void* dY, int dydt, long M, int C,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, int relu,
+                                                          float* __restrict__ part) {
+  const int lc = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int col = (blockIdx.x * 64 + lc) * 8;
+  const long r0 = (long)blockIdx.y * BN_ROWS;
+  float s[8], t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = t[e] = 0.f;
+  if (col < C) {
+    float mu[8], is[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mu[e] = mode ? mean[col + e] : 0.f;
+      is[e] = mode == 2 ? invstd[col + e] : 0.f;
+    }
+    const long rend = min(M, r0 + BN_ROWS);
+#pragma unroll 4
+    for (long r = r0 + ph; r < rend; r += 4) {
+      const long i = r * C + col;
+      float x[8];
+      ld8v(X, xdt, i, x);
+      if (mode == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += x[e];
+      } else if (mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = x[e] - mu[e];
+          s[e] += d * d;
+        }
+      } else {
+        float dz[8];
+        ld8v(dY, dydt, i, dz);
+        if (relu) {
+          float y[8];
+          ld8v(Y, ydt, i, y);
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if (y[e] <= 0.f) dz[e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s[e] += dz[e];
+          t[e] += dz[e] * (x[e] - mu[e]) * is[e];
+        }
+      }
+    }
+  }
+  __shared__ float red[2][4][512];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][ph][lc * 8 + e] = s[e];
+    red[1][ph][lc * 8 + e] = t[e];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < 512; k += 256) {
+    const int c = blockIdx.x * 512 + k;
+    if (c < C) {
+      part[((long)blockIdx.y * 2 + 0) * C + c] = red[0][0][k] + red[0][1][k] + red[0][2][k] + red[0][3][k];
+      part[((long)blockIdx.y * 2 + 1) * C + c] = red[1][0][k] + red[1][1][k] + red[1][2][k] + red[1][3][k];
+    }
+  }
+}
+
+// partial-sum launch: the 8-column form when C % 8 == 0
+static void launch_bn_partial(hipStream_t st, int mode, const void* X, int xdt, const void* Y, int ydt,
+                              const void* dY, int dydt, long M, long C, const float* mean, const float* invstd,
+                              int relu, float* part) {
+  const int nb = ivit_cdiv(M, BN_ROWS);
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(bn_partial8_kernel, dim3(ivit_cdiv(C, 512), nb), dim3(256), 0, st, mode, X, xdt, Y, ydt, dY,
+                       dydt, M, (int)C, mean, invstd, relu, part);
+  else
+    hipLaunchKernelGGL(bn_partial_kernel, dim3(ivit_cdiv(C, 64), nb), dim3(256), 0, st, mode, X, xdt, Y, ydt, dY,
+                       dydt, M, (int)C, mean, invstd, relu, part);
+}
+
 // Column sums of the per-block partials, 64 columns x 16 row phases per 1024-thread block
 // (the partial lists are hundreds of rows long: one thread per column left them latency-bound).
 IVIT_DEV float bn_colsum16(const float* __restrict__ part, int nb, long pstride, long off, int c, bool valid,
@@ -471,13 +560,10 @@ extern "C" int ivit_bn_stats(const void* X, int x_dtype, long M, long C, float* 
   IVIT_CHECK_ARG(work_bytes >= ivit_bn_workspace(M, C), "ivit_bn_stats: workspace too small");
   hipStream_t st = ivit_stream(stream);
   const int nb = ivit_cdiv(M, BN_ROWS);
-  dim3 g(ivit_cdiv(C, 64), nb);
   float* part = (float*)work;
-  hipLaunchKernelGGL(bn_partial_kernel, g, dim3(256), 0, st, 0, X, x_dtype, nullptr, 0, nullptr, 0, M, (int)C,
-                     nullptr, nullptr, 0, part);
+  launch_bn_partial(st, 0, X, x_dtype, nullptr, 0, nullptr, 0, M, C, nullptr, nullptr, 0, part);
   hipLaunchKernelGGL(bn_mean_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, M, (int)C, mean);
-  hipLaunchKernelGGL(bn_partial_kernel, g, dim3(256), 0, st, 1, X, x_dtype, nullptr, 0, nullptr, 0, M, (int)C, mean,
-                     nullptr, 0, part);
+  launch_bn_partial(st, 1, X, x_dtype, nullptr, 0, nullptr, 0, M, C, mean, nullptr, 0, part);
   hipLaunchKernelGGL(bn_var_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, M, (int)C, mean, invstd,
                      run_mean, run_var, momentum, eps);
   IVIT_LAUNCH_CHECK();
@@ -502,8 +588,7 @@ extern "C" int ivit_bn_bwd(const void* X, int x_dtype, const void* Y, int y_dtyp
   const int nb = ivit_cdiv(M, BN_ROWS);
   float* part = (float*)work;
   float* sums = part + (long)nb * 2 * C;
-  hipLaunchKernelGGL(bn_partial_kernel, dim3(ivit_cdiv(C, 64), nb), dim3(256), 0, st, 2, X, x_dtype, Y, y_dtype, dY,
-                     dy_dtype, M, (int)C, mean, invstd, relu, part);
+  launch_bn_partial(st, 2, X, x_dtype, Y, y_dtype, dY, dy_dtype, M, C, mean, invstd, relu, part);
   hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, (int)C, sums, dg, db,
                      accumulate);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ivit_cdiv(M * C, 256)), dim3(256), 0, st, X, x_dtype, Y, y_dtype, dY,
