@@ -6,6 +6,10 @@ N=1 and config 3 (DDP over RCCL) for N>1.
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
+Without torchrun's environment, ``--gpus N > 1`` starts the N ranks itself (child processes with
+RANK / LOCAL_RANK / WORLD_SIZE set, started before this process touches the GPU) and exits with
+their status; a WORLD_SIZE that disagrees with --gpus, or fewer visible GPUs than N, is an error.
+
 Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
 """
 from __future__ import annotations
@@ -149,6 +153,21 @@ def cpu_model_name():
     return "unknown"
 
 
+def granted_cpus():
+    """(threads to use, how the number was found): the cgroup CPU quota (cpu.max) when one is set
+    — the host cores this job may actually use — else the scheduler affinity mask."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        if q != "max":
+            n = max(1, int(int(q) // int(p)))
+            return min(n, aff), f"cgroup cpu.max quota {q}/{p} = {int(q) / int(p):g} CPUs"
+    except (OSError, ValueError):
+        pass
+    return aff, "sched_getaffinity (no cgroup CPU quota)"
+
+
 def cpu_baseline(steps=3):
     """The reference's CPU path restated by the oracle (timm semantics with the fused
     F.scaled_dot_product_attention, as timm's Attention.fused_attn runs it): f32 train step
@@ -157,7 +176,8 @@ def cpu_baseline(steps=3):
     sys.path.insert(0, HERE)
     from oracle import ivit_oracle as O
     from oracle.weights import make_state_dict, model_cfg
-    torch.set_num_threads(max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))))
+    threads, why = granted_cpus()
+    torch.set_num_threads(threads)
     cfg = model_cfg()
     sd = {k: (v.requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
           for k, v in make_state_dict(cfg, seed=0).items()}
@@ -180,10 +200,48 @@ def cpu_baseline(steps=3):
         ts.append(time.time() - t0)
     med = sorted(ts)[len(ts) // 2]
     return {"value": 1.0 / med, "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
-            "cpu": cpu_model_name(),
+            "cpu": cpu_model_name(), "os_cpu_count": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+            "cores_source": why,
             "sample": f"oracle f32 train step (fwd with SDPA attention + loss + bwd + AdamW), B=1, 400x720, "
                       f"median of {steps} after 1 warm-up",
             "step_s": med, "steps_s": [round(t, 3) for t in ts]}
+
+
+def launch_ranks(n):
+    """Start ranks 0..n-1 of this same command as child processes (torchrun's environment: RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1) and return the first non-zero
+    exit status (the others are stopped then), else 0. This process never initialises the GPU
+    (torch.cuda.device_count() does not, on this image)."""
+    import socket
+    import subprocess
+    have = torch.cuda.device_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} GPUs, {have} visible", file=sys.stderr, flush=True)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def main():
@@ -204,12 +262,20 @@ def main():
     ap.add_argument("--ddp", choices=["buckets", "torch"], default="buckets",
                     help="gradient exchange: ddp.GradBuckets (default) or torch DistributedDataParallel")
     args = ap.parse_args()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')} ranks were launched")
 
     sys.path.insert(0, PKG)
     from ddp import init_distributed
     rank, local, world, dev = init_distributed()
     if dev.type != "cuda":
         raise RuntimeError("bench.py needs a ROCm GPU (the HIP kernels have no CPU path)")
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    backend = dist.get_backend() if dist.is_initialized() else "none (single process)"
 
     import loss as L
     import model_vit
@@ -322,7 +388,8 @@ def main():
         metric = "BEV samples/sec inference (eval_vit.py path) IntentNetViT on MI355X"
     out = {
         "metric": metric,
-        "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": round(value, 3), "unit": "samples/s", "n_gpus": world, "backend": backend, "steps": args.steps,
+        "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.dtype, "data": "synthetic (random BEV rasters U[0,1)/Bernoulli(0.1), 20 random GT/sample; "
                                      "random-init weights)",

@@ -234,11 +234,22 @@ int ivit_adamw_shadow(long n_tensors, void* const* params, void* const* grads, v
                       void* const* exp_avg_sq, void* const* shadows, const long* sizes, long max_size, float lr,
                       float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2_sqrt,
                       void* stream);
+/* Same update with up to three bf16 outputs per tensor: outs[3t] the shadow, outs[3t+1] the
+ * row-panel pack of W [rows][cols[t]] (ivit_patch_weight_pack layout), outs[3t+2] the pack of
+ * W^T (ivit_weight_pack_t layout); any may be null. A tensor with a pack needs rows % 32 == 0
+ * and cols % 32 == 0 (it is walked in 8 x 8 tiles: max_work >= n / 64 for it, >= n otherwise).
+ * finite (device f32, may be null): 0 skips the whole update — the train_vit.py:163-165 /
+ * loss.py:190-198 non-finite-loss step without a host sync. */
+int ivit_adamw_packed(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
+                      void* const* exp_avg_sq, void* const* outs, const long* cols, const long* sizes,
+                      long max_work, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1,
+                      float bc2_sqrt, const float* finite, void* stream);
 
 /* ---- Detection / intention loss (loss.py:58-206): assignment + focal + Smooth-L1 + CE. ----- */
 /* gt: [B, Gmax, 5] f32 padded, ngt[B] int32, gint[B, Gmax] int32. keep: [B, NA] f32 0/1 (dominant
  * intent keep mask) or null. stats (f32[8]): focal_sum, box_sum, ce_sum, num_pos, keep_sum, loss,
- * cls_loss, box_loss, intent_loss (written). Per-anchor targets go to tgt (int32 [B, NA]). */
+ * cls_loss, box_loss, intent_loss (written). The workspace starts with the per-anchor targets,
+ * int32 [B, NA]: (cls target + 1) | (intent target + 1) << 2 (cls -1 = ignored, intent -1 = none). */
 long ivit_det_loss_workspace(long B, long NA, long Gmax);
 int ivit_det_loss_fwd(const float* cls, const float* box, const float* intent, const float* anchors, long B,
                       long NA, long K, const float* gt, const int* ngt, const int* gint, long Gmax,

@@ -116,3 +116,66 @@ def test_ddp_two_ranks_bf16_model_on_gpu(H, W):
         assert err < 1e-6, (rank, err)  # deterministic kernels: the same two per-rank sums
         assert same, rank
         assert moved > 0.0, rank
+
+
+def _rccl_worker(port, q):
+    """World 1 over RCCL (backend "nccl") on cuda:0: ddp.init_distributed binds the process group to
+    the device (device_id), Trainer(force_buckets=True) runs GradBuckets' backward-overlapped bucket
+    all-reduce on its comm stream and waits on the work handles — the exact multi-GPU code path,
+    with one rank. Two Trainers from the same weights and data, one plain and one through the
+    collectives, must end bitwise identical (an all-reduce over one rank is the identity)."""
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+        for p in (os.path.join(HERE, ".."), os.path.join(HERE, "..", "visiontransformer-intention-prediction_amd")):
+            sys.path.insert(0, p)
+        import ddp
+        rank, local, world, dev = ddp.init_distributed(force_group=True)
+        backend = dist.get_backend()
+        import loss as L
+        import model_vit
+        import utils
+        from optim import FusedAdamW
+        from oracle import ivit_oracle as O
+        from oracle.weights import make_state_dict, model_cfg
+        from trainer import Trainer
+        H, W = 64, 96
+        cfg = model_cfg(img_size=(H, W))
+        sd = make_state_dict(cfg, seed=0)
+        lidar, mp_, gts = O.synthetic_batch(2, (H, W), seed=5, grid_scale=H / 400.0)
+        lidar, mp_ = lidar.to(dev), mp_.to(dev)
+        anchors = utils.generate_anchors(H, W, 8, device=dev)
+        finals = []
+        for force in (False, True):
+            m = model_vit.IntentNetViT(backbone_cfg={"img_size": (H, W), "drop_path_rate_lidar": 0.0,
+                                                     "drop_path_rate_map": 0.0})
+            m.load_state_dict(sd, strict=True)
+            m = m.to(dev).set_compute_dtype(torch.bfloat16).train()
+            lf = L.DetectionIntentionLoss(apply_intention_downsampling=False)
+            tr = Trainer(m, lf, FusedAdamW(m.parameters(), lr=1e-4, weight_decay=1e-4), anchors, world=world,
+                         bucket_mb=8, check_nan=False, force_buckets=force)
+            n0 = ddp.GradBuckets.launched
+            for _ in range(2):
+                tr.step({"lidar_bev": lidar, "map_bev": mp_, "gt_list": gts})
+            torch.cuda.synchronize()
+            finals.append((torch.cat([p.detach().reshape(-1) for p in m.parameters()]).clone(),
+                           ddp.GradBuckets.launched - n0, len(tr.buckets.buckets) if tr.buckets else 0))
+        same = bool(torch.equal(finals[0][0], finals[1][0]))
+        q.put((backend, world, same, finals[1][1], finals[1][2], None))
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        q.put((None, None, None, None, None, traceback.format_exc()))
+
+
+def test_rccl_world1_bucketed_trainer():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_port(), q))
+    p.start()
+    backend, world, same, launched, nbuckets, exc = q.get(timeout=240)
+    p.join(timeout=60)
+    assert exc is None, exc
+    assert backend == "nccl" and world == 1
+    assert nbuckets > 1 and launched == 2 * nbuckets  # every bucket all-reduced on each of the 2 steps
+    assert same

@@ -28,17 +28,22 @@ import torch
 import torch.distributed as dist
 
 
-def init_distributed(backend: str | None = None):
-    """Read RANK/LOCAL_RANK/WORLD_SIZE from torchrun's env; returns (rank, local_rank, world, device)."""
+def init_distributed(backend: str | None = None, force_group: bool = False):
+    """Read RANK/LOCAL_RANK/WORLD_SIZE from torchrun's env; returns (rank, local_rank, world, device).
+    The process group (RCCL — backend "nccl" — on the GPU, bound to this rank's device; gloo on
+    the CPU) is created for world > 1, or at world 1 with ``force_group`` (tests: the collective
+    path on one GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
+        if local >= torch.cuda.device_count():
+            raise RuntimeError(f"LOCAL_RANK {local} but only {torch.cuda.device_count()} GPU(s) visible")
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_group) and not dist.is_initialized():
         be = backend or ("nccl" if dev.type == "cuda" else "gloo")
         if be == "nccl":
             dist.init_process_group(be, device_id=dev)
@@ -70,9 +75,13 @@ class GradBuckets:
         optimizer.step()
     """
 
-    def __init__(self, params, bucket_mb: float = 64.0, group=None):
+    launched = 0  # collectives issued (tests)
+
+    def __init__(self, params, bucket_mb: float = 64.0, group=None, force_collectives: bool = False):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # world 1: no exchange, unless forced (the collective path exercised on one device)
+        self.active = self.world > 1 or (force_collectives and dist.is_initialized())
         ps = [p for p in params if p.requires_grad]
         if len({id(p) for p in ps}) != len(ps):
             raise ValueError("GradBuckets: duplicate parameters")
@@ -126,7 +135,7 @@ class GradBuckets:
             raise RuntimeError("GradBuckets: a parameter's .grad was replaced outside the bucket "
                                "(use GradBuckets.zero_grad(), not optimizer.zero_grad(set_to_none=True))")
         b.ready += 1
-        if self.world == 1:
+        if not self.active:
             return
         if b.flat.is_cuda:
             # the two ViT streams produce gradients on two HIP streams (model_vit.stream_tokens):
@@ -147,6 +156,7 @@ class GradBuckets:
                 b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
         else:
             b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+        GradBuckets.launched += 1
 
     def _comm_stream(self, device):
         if getattr(self, "_comm", None) is None:
@@ -155,7 +165,7 @@ class GradBuckets:
 
     def finish(self):
         """Launch any bucket that did not fill (unused parameters), wait, and average."""
-        if self.world == 1:
+        if not self.active:
             for b in self.buckets:
                 b.ready = 0
             return
@@ -172,8 +182,9 @@ class GradBuckets:
             b.events = []
         if getattr(self, "_comm", None) is not None:
             torch.cuda.current_stream(self._comm.device).wait_stream(self._comm)
-        for b in self.buckets:
-            b.flat.mul_(inv)
+        if self.world > 1:
+            for b in self.buckets:
+                b.flat.mul_(inv)
 
     def remove(self):
         for h in self._hooks:
@@ -208,6 +219,16 @@ def any_rank(flag: bool, device, group=None) -> bool:
     t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return bool(int(t.item()))
+
+
+def min_on_device(t, group=None):
+    """Element-wise minimum over ranks of a device tensor, left on the device (no host sync): a
+    copy all-reduced with MIN on the current stream."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return t
+    out = t.detach().clone()
+    dist.all_reduce(out, op=dist.ReduceOp.MIN, group=group)
+    return out
 
 
 def max_over_ranks(value: float, device, group=None) -> float:

@@ -5,10 +5,15 @@ whole assignment + focal/Smooth-L1/CE computation is four HIP kernels with no ho
 synchronisation (the reference syncs per GT and per `.item()`); ``num_pos_anchors`` is
 therefore returned as a 0-dim device tensor (callers in train_vit.py already handle both).
 
-Intention down-sampling draws one uniform per anchor on the device (``keep_generator``)
-instead of the reference's per-class CPU-order ``torch.rand`` draws: same Bernoulli(0.15)
-law, different random stream. ``forward(..., intent_keep=mask)`` injects the mask for
-parity tests.
+Intention down-sampling (loss.py:169-182), two random streams:
+  * ``downsample_rng="device"`` (default): one uniform per anchor on the device
+    (``keep_generator``), no host sync — the same Bernoulli(keep) law as the reference, a
+    different stream;
+  * ``downsample_rng="reference"``: the reference's own draws — per dominant class in the set's
+    iteration order, ``torch.rand(k, device=device)`` over that class's positive anchors in
+    flattened (sample, anchor) order — so the same torch seed drops the same anchors. It costs an
+    assignment pass and a host sync per class (the reference's ``.item()``).
+``forward(..., intent_keep=mask)`` injects the mask for parity tests.
 """
 from __future__ import annotations
 
@@ -45,8 +50,11 @@ class DetectionIntentionLoss(nn.Module):
                  intention_class_weights=None, use_rotated_iou=False, focal_loss_alpha=0.25, focal_loss_gamma=2.0,
                  smooth_l1_beta=1.0 / 9.0, apply_intention_downsampling=True,
                  dominant_intentions=DOMINANT_CLASSES_FOR_DOWNSAMPLING,
-                 intention_downsample_ratio=INTENTION_DOWNSAMPLE_RATIO):
+                 intention_downsample_ratio=INTENTION_DOWNSAMPLE_RATIO, downsample_rng="device"):
         super().__init__()
+        if downsample_rng not in ("device", "reference"):
+            raise ValueError(f"downsample_rng must be 'device' or 'reference', got {downsample_rng!r}")
+        self.downsample_rng = downsample_rng
         self.iou_threshold, self.neg_iou_threshold = iou_threshold, neg_iou_threshold
         self.box_weight, self.cls_weight, self.intent_weight = box_weight, cls_weight, intent_weight
         self.use_rotated_iou = use_rotated_iou
@@ -60,6 +68,7 @@ class DetectionIntentionLoss(nn.Module):
         self.register_buffer("final_intention_class_weights", w)
         self.keep_generator = None
         self.last_finite = None
+        self.last_keep = None
 
     def _cfg(self, device):
         dom = 0
@@ -82,9 +91,12 @@ class DetectionIntentionLoss(nn.Module):
         if self.apply_intention_downsampling:
             if intent_keep is not None:
                 keep = intent_keep.to(dev).float().reshape(B, NA).contiguous()
+            elif self.downsample_rng == "reference":
+                keep = self._reference_keep(cls_logits, box_preds, intention_logits, anchors, gt, ng, gi)
             else:
                 u = torch.rand((B, NA), device=dev, generator=self.keep_generator)
                 keep = (u < self.intention_downsample_keep_prob).float()
+        self.last_keep = keep
         cls = cls_logits.float().reshape(B, NA)
         box = box_preds.float().reshape(B, NA, 6)
         it = intention_logits.float().reshape(B, NA, -1)
@@ -94,3 +106,33 @@ class DetectionIntentionLoss(nn.Module):
         self.last_finite = stats[9].detach()
         return {"loss": loss, "cls_loss": stats[6].detach(), "box_loss": stats[7].detach(),
                 "intent_loss": stats[8].detach(), "num_pos_anchors": stats[3].detach().round().long()}
+
+    def _reference_keep(self, cls_logits, box_preds, intention_logits, anchors, gt, ng, gi):
+        """The keep mask of the reference's draws (loss.py:170-178): the per-anchor targets from one
+        assignment pass (ivit_det_loss_fwd with no mask; its workspace starts with them), then per
+        dominant class, in ``self.dominant_intentions``' iteration order, ``torch.rand(k)`` on the
+        logits' device for its k positives in flattened order, kept where < keep probability."""
+        from _lib import lib, ptr, stream, workspace
+        B, NA = cls_logits.shape[0], anchors.shape[0]
+        dev = cls_logits.device
+        cls = cls_logits.detach().float().reshape(B, NA).contiguous()
+        box = box_preds.detach().float().reshape(B, NA, 6).contiguous()
+        it = intention_logits.detach().float().reshape(B, NA, -1).contiguous()
+        cfg = self._cfg(dev)
+        ws = workspace(lib.ivit_det_loss_workspace(B, NA, gt.shape[1]), dev)
+        stats = torch.empty((16,), dtype=torch.float32, device=dev)
+        lib.ivit_det_loss_fwd(ptr(cls), ptr(box), ptr(it), ptr(anchors), B, NA, it.shape[-1], ptr(gt), ptr(ng), ptr(gi),
+                              gt.shape[1], None, cfg["dominant_mask"], 0, None, cfg["pos_thr"], cfg["neg_thr"],
+                              cfg["alpha"], cfg["gamma"], cfg["beta"], cfg["w_cls"], cfg["w_box"], cfg["w_int"],
+                              int(cfg["rotated"]), ptr(stats), ptr(ws), ws.numel(), stream())
+        tgt = ws[:B * NA * 4].view(torch.int32)
+        pos_idx = torch.nonzero((tgt & 3) == 2).squeeze(1)  # cls target 1, in flattened order
+        it_pos = (tgt[pos_idx] >> 2) - 1
+        keep = torch.ones((B * NA,), dtype=torch.float32, device=dev)
+        for d in self.dominant_intentions:
+            m = it_pos == d
+            k = int(m.sum().item())
+            if k:
+                r = torch.rand(k, device=dev)
+                keep[pos_idx[m]] = (r < self.intention_downsample_keep_prob).float()
+        return keep.reshape(B, NA)

@@ -154,28 +154,65 @@ class TwoStreamViTBackbone(nn.Module):
         fusion_block_stride != 1 and for differing LiDAR / map patch grids."""
         return self.fusion_block_stride != 1 or self.lidar_grid_size != self.map_grid_size
 
-    def features_generic(self, tl, tm, B):
-        """model_vit.py:116-142 through the modules' own forwards (final norm, adapter LN ->
-        Linear -> GELU, token -> map, the map features re-gridded bilinearly onto the LiDAR grid
-        when the grids differ (:139, ops.BilinearFn), fusion BasicBlocks with their strides): the
-        path for fusion_block_stride != 1 (strided block-0 convs as im2col + GEMM) and for
-        differing patch grids."""
-        maps = []
-        for vitm, adapter, t in ((self.vit_lidar, self.adapter_lidar, tl), (self.vit_map, self.adapter_map, tm)):
-            D = vitm.embed_dim
-            Hf, Wf = vitm.patch_embed.grid_size
-            x = _LayerNormFn.apply(t, vitm.norm.weight, vitm.norm.bias, 1e-6).reshape(B, -1, D)
-            y = adapter(x[:, vitm.num_prefix_tokens:])
-            maps.append(y.permute(0, 2, 1).reshape(B, -1, Hf, Wf))
-        if maps[1].shape[2:] != maps[0].shape[2:]:
-            maps[1] = ops.BilinearFn.apply(maps[1], tuple(maps[0].shape[2:]))
-        return self.fusion_block(torch.cat(maps, 1))
+    def _process_stream(self, x, vit_stream, num_prefix_tokens, grid_size, adapter, stream_name):
+        """model_vit.py:116-122: the stream ViT's features (final norm included), prefix tokens
+        dropped, adapter (LayerNorm -> Linear -> GELU), tokens -> (B, C, Hf, Wf) feature map with
+        token n at (n // Wf, n % Wf); None (after the reference's message) when the token count
+        does not match the patch grid."""
+        tokens_all = vit_stream.forward_features(x)
+        adapted = adapter(tokens_all[:, num_prefix_tokens:])
+        B, N, C = adapted.shape
+        if grid_size and N == grid_size[0] * grid_size[1]:
+            Hf, Wf = grid_size
+            return adapted.permute(0, 2, 1).contiguous().view(B, C, Hf, Wf)
+        print(f"ERROR ({stream_name}): Token count {N} or grid_size {grid_size} issue.")
+        return None
+
+    def _process_streams(self, lidar_bev, map_bev):
+        """The two _process_stream calls (model_vit.py:135,137), on the two side streams when the
+        inputs are on the GPU (as stream_tokens)."""
+        args_l = (lidar_bev, self.vit_lidar, self.lidar_num_prefix_tokens, self.lidar_grid_size, self.adapter_lidar,
+                  "LiDAR")
+        args_m = (map_bev, self.vit_map, self.map_num_prefix_tokens, self.map_grid_size, self.adapter_map, "Map")
+        if not (self.concurrent_streams and lidar_bev.is_cuda):
+            return self._process_stream(*args_l), self._process_stream(*args_m)
+        main = torch.cuda.current_stream(lidar_bev.device)
+        s1, s2 = _side_streams(lidar_bev.device)
+        s1.wait_stream(main)
+        s2.wait_stream(main)
+        with torch.cuda.stream(s1):
+            fl = self._process_stream(*args_l)
+        with torch.cuda.stream(s2):
+            fm = self._process_stream(*args_m)
+        main.wait_stream(s1)
+        main.wait_stream(s2)
+        lidar_bev.record_stream(s1)
+        map_bev.record_stream(s2)
+        for f in (fl, fm):
+            if f is not None:
+                f.record_stream(main)
+        return fl, fm
+
+    def features_generic(self, lidar_bev, map_bev):
+        """model_vit.py:134-142 through the modules' own forwards: _process_stream per stream (a
+        None there gives the reference's zero feature map), the map features re-gridded bilinearly
+        onto the LiDAR grid when the grids differ (:139, ops.BilinearFn), fusion BasicBlocks with
+        their strides — the path for fusion_block_stride != 1 (strided block-0 convs as im2col +
+        GEMM) and for differing patch grids."""
+        fl, fm = self._process_streams(lidar_bev, map_bev)
+        for f, x in ((fl, lidar_bev), (fm, map_bev)):
+            if f is None:
+                return torch.zeros(x.shape[0], self.final_feature_channels, self.feature_map_grid_h or 1,
+                                   self.feature_map_grid_w or 1, device=x.device)
+        if fl.shape[2:] != fm.shape[2:]:
+            fm = ops.BilinearFn.apply(fm, tuple(fl.shape[2:]))
+        return self.fusion_block(torch.cat([fl, fm], 1))
 
     def forward(self, lidar_bev, map_bev):
         """model_vit.py:134-142 → fused feature map (B, C, Hf', Wf') f32."""
-        tl, tm = self.stream_tokens(lidar_bev, map_bev)
         if self.generic_neck:
-            return self.features_generic(tl, tm, lidar_bev.shape[0])
+            return self.features_generic(lidar_bev, map_bev)
+        tl, tm = self.stream_tokens(lidar_bev, map_bev)
         names = self.neck_names()
         tens = _lookup(self, names)
         B = lidar_bev.shape[0]
@@ -252,12 +289,12 @@ class IntentNetViT(nn.Module):
     def forward(self, lidar_bev, map_bev):
         """model_vit.py:179-185 → cls (B, A*Hf*Wf, 1), box (.., 6), intent (.., K), all f32."""
         B = lidar_bev.shape[0]
-        tl, tm = self.backbone.stream_tokens(lidar_bev, map_bev)
         if self.backbone.generic_neck:  # strided fusion / differing grids: module forwards, heads at H/s x W/s
-            f = self.backbone.features_generic(tl, tm, B)
+            f = self.backbone(lidar_bev, map_bev)
             c, b = self.det_head(f)
             it = self.intention_head(f)
             return c.reshape(B, -1, 1), b.reshape(B, -1, 6), it.reshape(B, -1, NUM_INTENTION_CLASSES)
+        tl, tm = self.backbone.stream_tokens(lidar_bev, map_bev)
         meta, names = self._neck_meta(B)
         bb = dict(self.backbone.named_parameters())
         bb.update(dict(self.backbone.named_buffers()))

@@ -93,6 +93,16 @@ def shadow_of(p):
     return e[1]
 
 
+def packs_of(p):
+    """(pack, transposed pack) of parameter p that are live (built at its current version), or
+    None each. FusedAdamW rewrites them in its update launch (ivit_adamw_packed): its pointer-table
+    update does not move the version counter, so without that the packs would stay at the
+    weights they were built from."""
+    e, et = _PACKED.get(p), _PACKED_T.get(p)
+    return (e[1] if e is not None and e[0] == p._version else None,
+            et[1] if et is not None and et[0] == p._version else None)
+
+
 # ------------------------------------------------------------------------------ primitives
 def linear_fwd(x, w, b, cdt, act=ACT_NONE, out_dtype=None, want_pre=False, resid=None, row_scale=None, rps=1,
                out=None, pre=None):
@@ -599,13 +609,19 @@ class GradHandoff:
     """Backward hand-off between consecutive fused ViT blocks: block i+1's qkv-dgrad + norm1-backward
     kernel also writes bf16(dx * s2_i) — block i's DropPath-scaled MLP-branch gradient, the fc2
     dgrad's operand — so block i skips that separate scale-and-cast pass over dx. `scale` is set
-    by block i's forward; `g` / `ptr` by block i+1's backward; block i uses `g` only if the
-    gradient it receives is that very tensor (`ptr`), else it recomputes it."""
-    __slots__ = ("scale", "g", "ptr")
+    by block i's forward; `g` / `key` by block i+1's backward; block i uses `g` only if the
+    gradient it receives is that very tensor, unmodified — same TensorImpl, data pointer and
+    version counter (a hook that edits it in place bumps the version; a different tensor at a
+    reused address has another TensorImpl) — else it recomputes it."""
+    __slots__ = ("scale", "g", "key")
     used = 0  # hand-offs taken (tests)
 
     def __init__(self):
-        self.scale, self.g, self.ptr = None, None, None
+        self.scale, self.g, self.key = None, None, None
+
+    @staticmethod
+    def ident(t):
+        return (t._cdata, t.data_ptr(), t._version)
 
 
 class ViTBlockFn(torch.autograd.Function):
@@ -624,13 +640,17 @@ class ViTBlockFn(torch.autograd.Function):
                 s1, s2, meta, hand_mine=None, hand_prev=None):
         B, N, H, cdt, eps = meta
         cd = tdtype(cdt)
-        wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
+        q2 = cdt == BF16
+        panel = q2 and x.shape[1] == 384
+        if panel:  # row-panel kernels read the packed weights; only the last fc2 runs the engine GEMM
+            wq = wp = w1 = None
+            w2 = cast_weight(f2w, cd) if nxw is None else None
+        else:
+            wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
         if ln_in is None:
             ln1, m1, r1 = layernorm_fwd(x, n1w, n1b, eps, cd)
         else:
             ln1, m1, r1 = ln_in, m_in, r_in
-        q2 = cdt == BF16
-        panel = q2 and x.shape[1] == 384
         if panel:
             qkv, _ = panel_fwd(ln1, qkvw, qkvb, qcols=H * 64, qscale=Q2_SCALE)
             o, lse = attn_fwd_q2(qkv, B, N, H)
@@ -668,7 +688,7 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.panel = panel
         ctx.hand_mine, ctx.hand_prev = (hand_mine, hand_prev) if panel else (None, None)
         if ctx.hand_mine is not None:
-            ctx.hand_mine.scale, ctx.hand_mine.g, ctx.hand_mine.ptr = s2, None, None
+            ctx.hand_mine.scale, ctx.hand_mine.g, ctx.hand_mine.key = s2, None, None
         return x2, lnx, mx, rx
 
     @staticmethod
@@ -685,10 +705,10 @@ class ViTBlockFn(torch.autograd.Function):
         hm, hp = ctx.hand_mine, ctx.hand_prev
         dx2s = None
         if hm is not None:
-            if hm.g is not None and hm.ptr == dx2.data_ptr():
+            if hm.g is not None and dx2 is not None and hm.key == GradHandoff.ident(dx2):
                 dx2s = hm.g  # written by the next block's qkv-dgrad epilogue
                 GradHandoff.used += 1
-            hm.g = hm.ptr = None
+            hm.g = hm.key = None
         if dx2s is None:
             dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
         dh = panel_dgrad_gelu(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
@@ -708,7 +728,7 @@ class ViTBlockFn(torch.autograd.Function):
             if hp is not None:  # also the previous block's bf16(dx0 * s2) (GradHandoff)
                 dx0, dx0s, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1, xs_dtype=cd,
                                                            row_scale=hp.scale, rps=N)
-                hp.g, hp.ptr = dx0s, dx0.data_ptr()
+                hp.g, hp.key = dx0s, GradHandoff.ident(dx0)
             else:
                 dx0, _, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1)
         else:

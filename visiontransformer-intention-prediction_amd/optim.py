@@ -29,7 +29,10 @@ class FusedAdamW(torch.optim.Optimizer):
         return tab
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, finite=None):
+        """One AdamW update. ``finite``: optional device scalar (f32); when it holds 0 the launch
+        updates nothing — the guard of loss.py:190-198 without a host sync (trainer.Trainer passes
+        the loss's flag when it does not sync). The host-side step counters still advance then."""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -60,17 +63,24 @@ class FusedAdamW(torch.optim.Optimizer):
                 sizes = self._table_sizes(ps, dev)
                 bc1 = 1.0 - b1 ** step
                 bc2s = math.sqrt(1.0 - b2 ** step)
-                # live bf16 compute copies (ops.cast_weight) are refreshed in the same launch
-                shadows = [ops.shadow_of(p) for p in ps]
-                if any(s is not None for s in shadows):
-                    tsh = self._table_ptrs([s.data_ptr() if s is not None else 0 for s in shadows], dev)
-                    lib.ivit_adamw_shadow(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(tsh), ptr(sizes),
-                                          max(p.numel() for p in ps), group["lr"], b1, b2, group["eps"],
-                                          group["weight_decay"], bc1, bc2s, stream())
-                else:
-                    lib.ivit_adamw(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(sizes),
-                                   max(p.numel() for p in ps), group["lr"], b1, b2, group["eps"],
-                                   group["weight_decay"], bc1, bc2s, stream())
+                # live bf16 compute copies (ops.cast_weight) and row-panel weight packs
+                # (ops.packed_weight / packed_weight_t) are rewritten in the same launch
+                outs, cols, work = [], [], 0
+                for p in ps:
+                    sh = ops.shadow_of(p)
+                    pk, pkt = ops.packs_of(p)
+                    c = p.numel() // p.shape[0] if p.dim() > 0 else 1
+                    tiled = pk is not None or pkt is not None
+                    if tiled and (p.shape[0] % 32 or c % 32):
+                        raise ValueError(f"FusedAdamW: packed weight of shape {tuple(p.shape)} not 32-aligned")
+                    outs += [t.data_ptr() if t is not None else 0 for t in (sh, pk, pkt)]
+                    cols.append(c)
+                    work = max(work, p.numel() // 64 if tiled else p.numel())
+                to = self._table_ptrs(outs, dev)
+                tc = self._table_ptrs(cols, dev)
+                lib.ivit_adamw_packed(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(to), ptr(tc), ptr(sizes),
+                                      work, group["lr"], b1, b2, group["eps"], group["weight_decay"], bc1, bc2s,
+                                      ptr(finite), stream())
         return loss
 
     def _table_ptrs(self, ptrs, device):

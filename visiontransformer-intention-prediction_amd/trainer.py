@@ -15,25 +15,31 @@ zero_grad → forward → (NaN skip) → DetectionIntentionLoss → (non-finite-
 Both checks are taken collectively across ranks (ddp.any_rank) so every rank stays on the same
 step; under DDP one rank's non-finite loss therefore skips the update on every rank (the
 replicas stay identical). They cost one host sync each, as the reference's ``torch.isnan``
-checks do; the benchmark turns them off (``check_nan=False``) — nothing else is skipped.
+checks do; the benchmark turns them off (``check_nan=False``) — nothing else is skipped. Without
+the host checks a non-finite loss still zeroes the update: backward runs (exact-zero gradients
+from the loss kernel) and FusedAdamW's launch reads the loss's device finite flag (min over ranks
+under DDP) and leaves weights and moments untouched; only its host step counters advance.
 """
 from __future__ import annotations
 
 import torch
 
-from ddp import GradBuckets, any_rank, broadcast_state
+from ddp import GradBuckets, any_rank, broadcast_state, min_on_device
+from optim import FusedAdamW
 
 
 class Trainer:
     def __init__(self, model, loss_fn, optimizer, anchors, world: int = 1, bucket_mb: float = 64.0,
-                 check_nan: bool = True):
+                 check_nan: bool = True, force_buckets: bool = False):
         self.model, self.loss_fn, self.optimizer, self.anchors = model, loss_fn, optimizer, anchors
         self.world = world
         self.check_nan = check_nan
         if world > 1:
             # identical replicas from the first step, whatever each rank's RNG did
             broadcast_state(model)
-        self.buckets = GradBuckets(model.parameters(), bucket_mb) if world > 1 else None
+        # force_buckets: the bucketed all-reduce path even at world 1 (tests on one GPU over RCCL)
+        self.buckets = GradBuckets(model.parameters(), bucket_mb, force_collectives=force_buckets) \
+            if world > 1 or force_buckets else None
         self.skipped = 0
         self.nonfinite = 0
 
@@ -67,5 +73,13 @@ class Trainer:
         d["loss"].backward()
         if self.buckets is not None:
             self.buckets.finish()
-        self.optimizer.step()
+        fin = getattr(self.loss_fn, "last_finite", None)
+        if not self.check_nan and fin is not None and isinstance(self.optimizer, FusedAdamW):
+            # no host sync: the update launch itself reads the loss's finite flag and does nothing
+            # on 0 (weights and moments unchanged, as with the reference's disconnected zero loss)
+            if self.buckets is not None and self.world > 1:
+                fin = min_on_device(fin)  # every rank skips together (replicas stay identical)
+            self.optimizer.step(finite=fin)
+        else:
+            self.optimizer.step()
         return d
