@@ -78,6 +78,16 @@ int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, long K, const
  * transposed by ivit_weight_pack_t), bf16. */
 int ivit_linear_dgrad_gelu_panel(const void* dY, long lddy, long M, long N, long K, const void* wpack_t,
                                  const void* pre, long ldpre, void* dX, long lddx, void* stream);
+/* The weight and bias gradients of one timm Block's four linears (Mlp.fc2, Mlp.fc1, Attention.proj,
+ * Attention.qkv; model_vit.py:64,71 -> timm Block backward) in one grouped launch + one reduce:
+ *   dW_g = dY_g^T X_g (f32 [N][K]), db_g = colsum(dY_g) (f32 [N], may be null), bf16 token-major
+ *   operands [M][*], for (dY, X) = (dy2 [M][D], a [M][Hd]), (dh [M][Hd], x2 [M][D]),
+ *   (dyp [M][D], o [M][D]), (dyq [M][3D], x1 [M][D]). D = 384, Hd % 384 == 0, operands 16-B aligned. */
+long ivit_vit_block_wgrad_workspace(long M, long D, long Hd);
+int ivit_vit_block_wgrad(long M, long D, long Hd, const void* dy2, const void* a, const void* dh, const void* x2,
+                         const void* dyp, const void* o, const void* dyq, const void* x1, float* dw2, float* db2,
+                         float* dw1, float* db1, float* dwp, float* dbp, float* dwq, float* dbq, void* work,
+                         long work_bytes, void* stream);
 /* W [K][N] f32 -> the row-panel packed bf16 layout of W^T (ivit_patch_weight_pack_bytes(N, K / 64) bytes). */
 int ivit_weight_pack_t(const float* w, long K, long N, void* wpack, void* stream);
 /* ---- timm PatchEmbed (Conv2d k=s=8) + CLS concat + pos_embed (model_vit.py:64,71 → timm). */

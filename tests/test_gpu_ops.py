@@ -594,6 +594,56 @@ def test_adamw_refreshes_bf16_weight_shadows():
     assert torch.equal(ops.cast_weight(ps[0], torch.bfloat16), ps[0].detach().to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("M", [1, 33, 194, 4501, 36008])
+def test_vit_block_wgrad_grouped(M):
+    """ivit_vit_block_wgrad (the four weight + bias gradients of a bf16 timm Block in one grouped
+    launch + reduce) vs f64 of the same bf16 operands: dW = dY^T X, db = colsum(dY), for
+    M tokens incl. ragged last K steps and fewer tokens than splits; deterministic (two runs equal)."""
+    import ops
+    D, Hd = 384, 1536
+    g = torch.Generator(device=DEV).manual_seed(M)
+    mk = lambda c: torch.randn(M, c, device=DEV, generator=g).to(torch.bfloat16)
+    ops_ = [mk(D), mk(Hd), mk(Hd), mk(D), mk(D), mk(D), mk(3 * D), mk(D)]
+    got = ops.vit_block_wgrad(*ops_)
+    again = ops.vit_block_wgrad(*ops_)
+    for (dw, db), (dw2, db2) in zip(got, again):
+        assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    for q, (dw, db) in enumerate(got):
+        dy, x = ops_[2 * q].double(), ops_[2 * q + 1].double()
+        rw, rb = dy.T @ x, dy.sum(0)
+        assert dw.shape == rw.shape and db.shape == rb.shape
+        ew = float((dw.double() - rw).norm() / rw.norm())
+        eb = float((db.double() - rb).norm() / rb.norm())
+        assert ew < 1e-5 and eb < 1e-5, (q, ew, eb)
+
+
+def test_adamw_packs_unaligned_grads():
+    """ivit_adamw_packed on a packed weight whose gradient is a view at a 4-B (not 16-B) offset (a
+    DDP bucket view): the scalar-access path gives the same update as torch.optim.AdamW and packs
+    equal to freshly built ones."""
+    import ops
+    from optim import FusedAdamW
+    p = torch.randn(384, 1536, device=DEV, requires_grad=True)
+    ref = p.detach().clone().requires_grad_(True)
+    flat = torch.zeros(p.numel() + 1, device=DEV)
+    p.grad = flat[1:].view_as(p)
+    ops.packed_weight(p)
+    ops.packed_weight_t(p)
+    opt, topt = FusedAdamW([p], lr=1e-2, weight_decay=1e-2), torch.optim.AdamW([ref], lr=1e-2, weight_decay=1e-2)
+    for _ in range(2):
+        gr = torch.randn_like(p)
+        p.grad.copy_(gr)
+        ref.grad = gr.clone()
+        opt.step()
+        topt.step()
+    assert (p.detach() - ref.detach()).abs().max().item() < 1e-5
+    pk, pkt = ops.packs_of(p)
+    fresh, fresh_t = torch.empty_like(pk), torch.empty_like(pkt)
+    ops.lib.ivit_patch_weight_pack(ops.ptr(p.detach()), 384, 1536 // 64, ops.ptr(fresh), ops.stream())
+    ops.lib.ivit_weight_pack_t(ops.ptr(p.detach()), 384, 1536, ops.ptr(fresh_t), ops.stream())
+    assert torch.equal(pk, fresh) and torch.equal(pkt, fresh_t)
+
+
 def test_geometry_golden():
     from conftest import golden
     import utils

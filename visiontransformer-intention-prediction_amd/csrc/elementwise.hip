@@ -134,7 +134,7 @@ struct Adam {
   }
 };
 
-__global__ void adamw_packed_kernel(void* const* params, void* const* grads, void* const* ms, void* const* vs,
+__global__ __launch_bounds__(256) void adamw_packed_kernel(void* const* params, void* const* grads, void* const* ms, void* const* vs,
                                     void* const* outs, const long* cols, const long* sizes, Adam a,
                                     const float* finite) {
   if (finite != nullptr && !(*finite != 0.f)) return;
@@ -163,7 +163,8 @@ __global__ void adamw_packed_kernel(void* const* params, void* const* grads, voi
   // streams are aligned (uniform per tensor)
   const bool vec = ((((unsigned long)p) | ((unsigned long)g) | ((unsigned long)m) | ((unsigned long)v)) & 15) == 0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < ntile; i += (long)gridDim.x * blockDim.x) {
-    const long r0 = (i / tc) * 8, c0 = (i - (i / tc) * tc) * 8;
+    const unsigned tr = (unsigned)i / (unsigned)tc;  // ntile < 2^31: 32-bit division
+    const long r0 = (long)tr * 8, c0 = (i - (long)tr * tc) * 8;
     unsigned tw[8][4];  // transposed pack: column e of the tile, rows 2j, 2j+1
     float prev[8];      // the even row's values until the odd row pairs them
 #pragma unroll

@@ -144,6 +144,23 @@ def linear_wgrad(dy, x, cdt, want_bias=True):
     return dw, db
 
 
+def vit_block_wgrad(dy2, a, dh, x2, dyp, o, dyq, x1):
+    """The four weight + bias gradients of one bf16 timm Block (fc2, fc1, proj, qkv) in one grouped
+    launch + one reduce (ivit_vit_block_wgrad): dW = dY^T X, db = colsum(dY) for
+    (dY, X) = (dx2s, a), (dh, ln2), (dx1s, o), (dqkv, ln1). -> [(dW, db)] * 4."""
+    M, D = dy2.shape
+    Hd = a.shape[1]
+    dev = dy2.device
+    shapes = ((D, Hd), (Hd, D), (D, D), (3 * D, D))
+    dws = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in shapes]
+    dbs = [torch.empty((sh[0],), dtype=torch.float32, device=dev) for sh in shapes]
+    ws = workspace(lib.ivit_vit_block_wgrad_workspace(M, D, Hd), dev)
+    lib.ivit_vit_block_wgrad(M, D, Hd, ptr(dy2), ptr(a), ptr(dh), ptr(x2), ptr(dyp), ptr(o), ptr(dyq), ptr(x1),
+                             ptr(dws[0]), ptr(dbs[0]), ptr(dws[1]), ptr(dbs[1]), ptr(dws[2]), ptr(dbs[2]), ptr(dws[3]),
+                             ptr(dbs[3]), ptr(ws), ws.numel(), stream())
+    return list(zip(dws, dbs))
+
+
 def layernorm_fwd(x, g, b, eps, out_dtype, rowmap=(0, 0, 0), M=None):
     D = x.shape[-1]
     M = x.shape[0] if M is None else M
@@ -569,6 +586,9 @@ class PatchEmbedFn(torch.autograd.Function):
 # Off by default: measured on MI355X with the two ViT streams already concurrent, the extra
 # fork costs 7 % (65.0 -> 69.5 ms/step, bench.py A/B in one call). IVIT_WGRAD_FORK=1 enables it.
 WGRAD_FORK = os.environ.get("IVIT_WGRAD_FORK", "0") == "1"
+# bf16 row-panel ViT blocks: the four weight gradients as one grouped launch (ivit_vit_block_wgrad)
+# instead of four split-K engine GEMMs; IVIT_GROUP_WGRAD=0 selects the per-GEMM path (A/B runs).
+GROUP_WGRAD = os.environ.get("IVIT_GROUP_WGRAD", "1") == "1"
 _FORK_STREAMS = {}
 
 
@@ -712,7 +732,9 @@ class ViTBlockFn(torch.autograd.Function):
         if dx2s is None:
             dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
         dh = panel_dgrad_gelu(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
-        g2 = _wgrad(fork, dx2s, a, cdt)
+        # bf16 row-panel blocks: the four weight gradients in one grouped launch after the dgrads
+        group = ctx.panel and GROUP_WGRAD and fork is None
+        g2 = None if group else _wgrad(fork, dx2s, a, cdt)
         if ctx.panel:  # fc1 dgrad with norm2's backward in the epilogue
             dx1, dx1s, dg2, dbe2 = linear_dgrad_ln_bwd(dh, f1w, x1, n2w, m2, r2, dres=dx2, dx=torch.empty_like(dx2),
                                                        xs_dtype=cd, row_scale=s1, rps=N)
@@ -720,9 +742,9 @@ class ViTBlockFn(torch.autograd.Function):
             dln2 = linear_dgrad(dh, w1, cdt, torch.float32)
             dx1, dx1s, dg2, dbe2 = layernorm_bwd(x1, n2w, m2, r2, dln2, dres=dx2, dx=torch.empty_like(dx2),
                                                  xs_dtype=cd, row_scale=s1, rps=N)
-        g1 = _wgrad(fork, dh, ln2, cdt)
+        g1 = None if group else _wgrad(fork, dh, ln2, cdt)
         do = panel_dgrad(dx1s, pw) if ctx.panel else linear_dgrad(dx1s, wp, cdt, cd)
-        gp = _wgrad(fork, dx1s, o, cdt)
+        gp = None if group else _wgrad(fork, dx1s, o, cdt)
         dqkv = attn_bwd_q2(qkv, o, do, lse, B, N, H) if ctx.q2 else attn_bwd(qkv, o, do, lse, B, N, H, cdt)
         if ctx.panel:  # qkv dgrad with norm1's backward in the epilogue
             if hp is not None:  # also the previous block's bf16(dx0 * s2) (GradHandoff)
@@ -734,7 +756,10 @@ class ViTBlockFn(torch.autograd.Function):
         else:
             dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
             dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
-        gq = _wgrad(fork, dqkv, ln1, cdt)
+        if group:
+            g2, g1, gp, gq = vit_block_wgrad(dx2s, a, dh, ln2, dx1s, o, dqkv, ln1)
+        else:
+            gq = _wgrad(fork, dqkv, ln1, cdt)
         if fork is not None:
             fork.join((dx2s, dh, dx1s, dqkv, a, ln2, o, ln1))
         (dW2, db2), (dW1, db1), (dWp, dbp), (dWq, dbq) = g2, g1, gp, gq
