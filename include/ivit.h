@@ -90,6 +90,10 @@ int ivit_vit_block_wgrad(long M, long D, long Hd, const void* dy2, const void* a
                          long work_bytes, void* stream);
 /* W [K][N] f32 -> the row-panel packed bf16 layout of W^T (ivit_patch_weight_pack_bytes(N, K / 64) bytes). */
 int ivit_weight_pack_t(const float* w, long K, long N, void* wpack, void* stream);
+/* Many packs in one launch: jobs = device array of n records {const float* w; void* wpack; long rows;
+ * long cols; int transposed (+4 pad)} (40 B each); transposed 0 = ivit_patch_weight_pack(w, rows,
+ * cols / 64), 1 = ivit_weight_pack_t(w, rows, cols); max_rows_cols >= every rows * cols. */
+int ivit_weight_pack_multi(long n, const void* jobs, long max_rows_cols, void* stream);
 /* ---- timm PatchEmbed (Conv2d k=s=8) + CLS concat + pos_embed (model_vit.py:64,71 → timm). */
 int ivit_patch_embed_fwd(int dtype, const float* img, long B, long C, long H, long W, const void* Wt,
                          const float* bias, const float* pos, const float* cls, long D, float* out, void* stream);
@@ -249,11 +253,12 @@ int ivit_adamw_shadow(long n_tensors, void* const* params, void* const* grads, v
  * W^T (ivit_weight_pack_t layout); any may be null. A tensor with a pack needs rows % 32 == 0
  * and cols % 32 == 0 (it is walked in 8 x 8 tiles: max_work >= n / 64 for it, >= n otherwise).
  * finite (device f32, may be null): 0 skips the whole update — the train_vit.py:163-165 /
- * loss.py:190-198 non-finite-loss step without a host sync. */
+ * loss.py:190-198 non-finite-loss step without a host sync. tiled = 0: no tensor of the set has a
+ * pack (outs[3t+1], outs[3t+2] ignored; a light streaming kernel), 1: some may. */
 int ivit_adamw_packed(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
                       void* const* exp_avg_sq, void* const* outs, const long* cols, const long* sizes,
                       long max_work, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1,
-                      float bc2_sqrt, const float* finite, void* stream);
+                      float bc2_sqrt, const float* finite, int tiled, void* stream);
 
 /* ---- Detection / intention loss (loss.py:58-206): assignment + focal + Smooth-L1 + CE. ----- */
 /* gt: [B, Gmax, 5] f32 padded, ngt[B] int32, gint[B, Gmax] int32. keep: [B, NA] f32 0/1 (dominant

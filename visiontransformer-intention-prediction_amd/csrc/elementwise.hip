@@ -89,16 +89,19 @@ __global__ void merge_heads_kernel(const float* dcls, const float* dbox, const f
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // shadows (optional): per tensor a bf16 copy of the updated parameter (nullptr: none) — the
 // compute-dtype weights the next forward reads, refreshed here instead of by per-step casts.
-__global__ void adamw_kernel(void* const* params, void* const* grads, void* const* ms, void* const* vs,
-                             const long* sizes, float lr, float b1, float b2, float eps, float wd, float bc1,
-                             float bc2s, void* const* shadows) {
+// (shadows: stride sstride entries per tensor; finite: as adamw_packed_kernel below)
+__global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* const* grads, void* const* ms,
+                                                    void* const* vs, const long* sizes, float lr, float b1, float b2,
+                                                    float eps, float wd, float bc1, float bc2s, void* const* shadows,
+                                                    int sstride, const float* finite) {
+  if (finite != nullptr && !(*finite != 0.f)) return;
   const int t = blockIdx.y;
   const long n = sizes[t];
   float* p = (float*)params[t];
   const float* g = (const float*)grads[t];
   float* m = (float*)ms[t];
   float* v = (float*)vs[t];
-  bf16* sh = shadows ? (bf16*)shadows[t] : nullptr;
+  bf16* sh = shadows ? (bf16*)shadows[(long)sstride * t] : nullptr;
   const float step = lr / bc1;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float gi = g[i];
@@ -279,7 +282,8 @@ extern "C" int ivit_adamw(long n_tensors, void* const* params, void* const* grad
   int gx = ivit_cdiv(max_size, 256);
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
-                     exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, (void* const*)nullptr);
+                     exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, (void* const*)nullptr, 1,
+                     (const float*)nullptr);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -294,7 +298,8 @@ extern "C" int ivit_adamw_shadow(long n_tensors, void* const* params, void* cons
   int gx = ivit_cdiv(max_size, 256);
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
-                     exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, shadows);
+                     exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, shadows, 1,
+                     (const float*)nullptr);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -302,12 +307,18 @@ extern "C" int ivit_adamw_shadow(long n_tensors, void* const* params, void* cons
 extern "C" int ivit_adamw_packed(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
                                  void* const* exp_avg_sq, void* const* outs, const long* cols, const long* sizes,
                                  long max_work, float lr, float beta1, float beta2, float eps, float weight_decay,
-                                 float bc1, float bc2_sqrt, const float* finite, void* stream) {
+                                 float bc1, float bc2_sqrt, const float* finite, int tiled, void* stream) {
   if (n_tensors <= 0) return 0;
   IVIT_CHECK_ARG(n_tensors < 65536, "ivit_adamw_packed: too many tensors");
   IVIT_CHECK_ARG(outs != nullptr && cols != nullptr, "ivit_adamw_packed: null outs / cols table");
   int gx = ivit_cdiv(max_work, 256);
   if (gx > 1024) gx = 1024;
+  if (!tiled) {  // no packs: the light streaming kernel (the tile kernel's registers cap occupancy)
+    hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
+                       exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, outs, 3, finite);
+    IVIT_LAUNCH_CHECK();
+    return 0;
+  }
   const Adam a{lr, beta1, beta2, eps, weight_decay, lr / bc1, bc2_sqrt};
   hipLaunchKernelGGL(adamw_packed_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads,
                      exp_avg, exp_avg_sq, outs, cols, sizes, a, finite);

@@ -236,6 +236,36 @@ __global__ __launch_bounds__(256) void pack_t_kernel(const float* __restrict__ w
   wp[i] = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
 }
 
+// Every pack of a list in one launch (FusedAdamW's refresh after the update): blockIdx.y = pack;
+// tr = 0: W [rows][cols] -> the patch_pack_kernel layout, 1: W [rows = K][cols = N] -> the
+// pack_t_kernel layout of W^T.
+struct PackJob {
+  const float* w;
+  uint4* wp;
+  long rows, cols;
+  int tr;
+};
+__global__ __launch_bounds__(256) void multi_pack_kernel(const PackJob* __restrict__ jobs) {
+  const PackJob j = jobs[blockIdx.y];
+  const long total = j.rows * j.cols / 8;  // uint4 outputs
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int lane = (int)(i & 63);
+    const long snb = i >> 6;
+    if (!j.tr) {  // D = rows, K = cols
+      const long NB16 = j.rows / 16, s = snb / NB16, nb = snb - s * NB16;
+      const float* q = j.w + (nb * 16 + (lane & 15)) * j.cols + s * 32 + 8 * (lane >> 4);
+      j.wp[i] = f32x8_to_bf16x8(*(const float4*)q, *(const float4*)(q + 4));
+    } else {  // K = rows, N = cols
+      const long NB16 = j.cols / 16, s = snb / NB16, nb = snb - s * NB16;
+      const long n = nb * 16 + (lane & 15), k0 = s * 32 + 8 * (lane >> 4);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = j.w[(k0 + e) * j.cols + n];
+      j.wp[i] = make_uint4(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]), pk_bf16(v[4], v[5]), pk_bf16(v[6], v[7]));
+    }
+  }
+}
+
 __global__ void patch_cls_kernel(float* out, long B, long Ntok, long D, const float* cls, const float* pos) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B * D) return;
@@ -255,6 +285,16 @@ extern "C" int ivit_patch_weight_pack(const float* w, long D, long C, void* wpac
   const long K = C * 64, n = (K / 32) * (D / 16) * 64;
   hipLaunchKernelGGL(patch_pack_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), w, D, K,
                      (uint4*)wpack);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_weight_pack_multi(long n, const void* jobs, long max_rows_cols, void* stream) {
+  if (n <= 0) return 0;
+  IVIT_CHECK_ARG(n < 65536 && jobs != nullptr, "ivit_weight_pack_multi: bad job table");
+  int gx = ivit_cdiv(max_rows_cols / 8, 256);
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(multi_pack_kernel, dim3(gx, n), dim3(256), 0, ivit_stream(stream), (const PackJob*)jobs);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -53,7 +53,14 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] += 1
                 by_step.setdefault(st["step"], []).append(p)
-            for step, ps in by_step.items():
+            for step, ps_all in by_step.items():
+                bc1 = 1.0 - b1 ** step
+                bc2s = math.sqrt(1.0 - b2 ** step)
+                # the update through the light streaming kernel (live bf16 compute copies, ops.cast_weight,
+                # rewritten in it), then every live row-panel weight pack (ops.packed_weight /
+                # packed_weight_t) rebuilt from the updated f32 weights in ONE launch: the pointer-table
+                # update moves no version counter, so without it the packs would stay at the old weights
+                ps = ps_all
                 dev = ps[0].device
                 st = [self.state[p] for p in ps]
                 tp = self._table(ps, dev)
@@ -61,26 +68,22 @@ class FusedAdamW(torch.optim.Optimizer):
                 tm = self._table([s["exp_avg"] for s in st], dev)
                 tv = self._table([s["exp_avg_sq"] for s in st], dev)
                 sizes = self._table_sizes(ps, dev)
-                bc1 = 1.0 - b1 ** step
-                bc2s = math.sqrt(1.0 - b2 ** step)
-                # live bf16 compute copies (ops.cast_weight) and row-panel weight packs
-                # (ops.packed_weight / packed_weight_t) are rewritten in the same launch
-                outs, cols, work = [], [], 0
+                outs, jobs, big = [], [], 0
                 for p in ps:
                     sh = ops.shadow_of(p)
+                    outs += [sh.data_ptr() if sh is not None else 0, 0, 0]
                     pk, pkt = ops.packs_of(p)
-                    c = p.numel() // p.shape[0] if p.dim() > 0 else 1
-                    tiled = pk is not None or pkt is not None
-                    if tiled and (p.shape[0] % 32 or c % 32):
-                        raise ValueError(f"FusedAdamW: packed weight of shape {tuple(p.shape)} not 32-aligned")
-                    outs += [t.data_ptr() if t is not None else 0 for t in (sh, pk, pkt)]
-                    cols.append(c)
-                    work = max(work, p.numel() // 64 if tiled else p.numel())
+                    rows, cols = p.shape[0], p.numel() // p.shape[0]
+                    for pack, tr in ((pk, 0), (pkt, 1)):
+                        if pack is not None:
+                            jobs.append((p.data_ptr(), pack.data_ptr(), rows, cols, tr))
+                            big = max(big, rows * cols)
                 to = self._table_ptrs(outs, dev)
-                tc = self._table_ptrs(cols, dev)
-                lib.ivit_adamw_packed(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(to), ptr(tc), ptr(sizes),
-                                      work, group["lr"], b1, b2, group["eps"], group["weight_decay"], bc1, bc2s,
-                                      ptr(finite), stream())
+                lib.ivit_adamw_packed(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(to), ptr(to), ptr(sizes),
+                                      max(p.numel() for p in ps), group["lr"], b1, b2, group["eps"],
+                                      group["weight_decay"], bc1, bc2s, ptr(finite), 0, stream())
+                if jobs:
+                    lib.ivit_weight_pack_multi(len(jobs), ptr(self._pack_jobs(jobs, dev)), big, stream())
         return loss
 
     def _table_ptrs(self, ptrs, device):
@@ -88,6 +91,20 @@ class FusedAdamW(torch.optim.Optimizer):
         tab = self._tables.get(key)
         if tab is None:
             tab = torch.tensor(ptrs, dtype=torch.int64).pin_memory().to(device, non_blocking=True)
+            if len(self._tables) > 64:
+                self._tables.clear()
+            self._tables[key] = tab
+        return tab
+
+    def _pack_jobs(self, jobs, device):
+        """Device table of ivit_weight_pack_multi records (w, wpack, rows, cols, transposed), 40 B each."""
+        key = ("packs",) + tuple(jobs)
+        tab = self._tables.get(key)
+        if tab is None:
+            rec = []
+            for w, wp, rows, cols, tr in jobs:
+                rec += [w, wp, rows, cols, tr]
+            tab = torch.tensor(rec, dtype=torch.int64).pin_memory().to(device, non_blocking=True)
             if len(self._tables) > 64:
                 self._tables.clear()
             self._tables[key] = tab
