@@ -82,3 +82,17 @@ for name, fn, by, fl in rows:
     tot_floor += floor
     print(f"{name:32s} {ms * 1e3:8.1f} {fl / ms / 1e9:7.1f} {by / ms / 1e6:7.0f} {hb:9.1f} {mf:10.1f}  {ms * 1e3 / floor:5.2f}")
 print(f"{'block total':32s} {tot:8.1f} us   floor {tot_floor:.1f} us  ({tot / tot_floor:.2f}x)")
+
+# library reference points (torch.matmul -> hipBLASLt): the same GEMMs without the fused epilogues
+if os.environ.get("BLAS_REF", "1") == "1":
+    wq16, w116, w216 = wqkv.to(torch.bfloat16), w1.to(torch.bfloat16), w2.to(torch.bfloat16)
+    refs = [("blas qkv  ln @ Wqkv^T", lambda: ln @ wq16.t(), M * D * B2 + M * 3 * D * B2, 2.0 * M * 3 * D * D),
+            ("blas fc1  ln @ W1^T", lambda: ln @ w116.t(), M * D * B2 + M * F * B2, 2.0 * M * F * D),
+            ("blas fc2  a @ W2^T", lambda: a @ w216.t(), M * F * B2 + M * D * B2, 2.0 * M * D * F),
+            ("blas fc2 dgrad dy @ W2", lambda: dy @ w216, M * D * B2 + M * F * B2, 2.0 * M * D * F),
+            ("blas qkv dgrad dqkv @ Wqkv", lambda: dqkv @ wq16, M * 3 * D * B2 + M * D * B2, 2.0 * M * 3 * D * D)]
+    for name, fn, by, fl in refs:
+        ms = timeit(fn)
+        hb, mf = by / 6.3e12 * 1e6, fl / 2516.6e12 * 1e6
+        print(f"{name:32s} {ms * 1e3:8.1f} {fl / ms / 1e9:7.1f} {by / ms / 1e6:7.0f} {hb:9.1f} {mf:10.1f}  "
+              f"{ms * 1e3 / max(hb, mf):5.2f}")

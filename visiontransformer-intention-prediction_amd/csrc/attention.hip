@@ -595,14 +595,19 @@ constexpr int BNS = 3;  // LDS stages of the v3 backward kernels
 // negated row constants (-lse2, -delta; padded rows -1e30 / 0, so P = 0 there, no mask).
 // (W = 8, one 512-thread workgroup per CU sharing each Q / dO tile, halves the L2 -> LDS bytes
 // but measured slower; the product uses W = 4.)
-template <int W>
+// XR: the row constants arrive as exact bf16 triples (split3_bf16, written by the dQ kernel) and
+// enter each S / dP chain through one extra MFMA, [hi mid lo 0 ..] x [1 1 1 0 ..]^T, from a zero
+// accumulator: per 32-query unit two ds_read_b64 instead of eight ds_read_b128 of f32 row
+// vectors (a third of the unit's LDS-array cycles), for two more MFMAs.
+template <int W, bool XR = false>
 __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ nlse2p,
                                                                  const float* __restrict__ ndeltap, int N, int Npad,
                                                                  int H, bf16* __restrict__ dqkv, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][Q|dO]
-  __shared__ __attribute__((aligned(16))) float srow[BNS][2][AK];    // [stage][-lse2|-delta]
+  constexpr int RW = XR ? 2 : 1;  // words per row constant
+  __shared__ __attribute__((aligned(16))) float srow[BNS][2][RW * AK];  // [stage][-lse2|-delta]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int2 bid = attn_block_id();
@@ -613,8 +618,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
   const bf16* Gb = dout + (long)b * N * D + h * 64;
-  const char* Ls = uniform_ptr(nlse2p + (long)z * Npad);
-  const char* Ds = uniform_ptr(ndeltap + (long)z * Npad);
+  const char* Ls = uniform_ptr(nlse2p + (long)RW * z * Npad);
+  const char* Ds = uniform_ptr(ndeltap + (long)RW * z * Npad);
   constexpr int PW = 8 / W;  // DMA pieces per wave per 8-KiB tile image
   const int key = bid.x * (32 * W) + wv * 32 + (lane & 31);
   bf16x8 kf[4], vf[4];
@@ -650,8 +655,11 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
       glds_s<false>(og, gb, gimg + piece * 1024);
     }
     if (wv == 0) {  // bases in SGPRs, the tile offset in the per-lane offset
-      glds4_s(4u * (lane + qt * AK), Ls, &srow[S][0][0]);
-      glds4_s(4u * (lane + qt * AK), Ds, &srow[S][1][0]);
+#pragma unroll
+      for (int i = 0; i < RW; ++i) {
+        glds4_s(4u * (lane + (RW * qt + i) * AK), Ls, &srow[S][0][i * AK]);
+        glds4_s(4u * (lane + (RW * qt + i) * AK), Ds, &srow[S][1][i * AK]);
+      }
     }
   };
 
@@ -669,6 +677,15 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
     const float4 d4 = *(const float4*)(dr + 32 * t + 8 * part + 4 * hl);
     sn[4 * part] = l4.x; sn[4 * part + 1] = l4.y; sn[4 * part + 2] = l4.z; sn[4 * part + 3] = l4.w;
     dn[4 * part] = d4.x; dn[4 * part + 1] = d4.y; dn[4 * part + 2] = d4.z; dn[4 * part + 3] = d4.w;
+  };
+  // XR operands: A = this lane's query row pair in k 0..1 (lanes >= 32 hold k 8..15, multiplied by
+  // B's zero rows), B = (1, 1) in k 0..1 of every key column
+  uint2 xl = make_uint2(0, 0), xd = make_uint2(0, 0);
+  const bf16x8 xb =
+      __builtin_bit_cast(bf16x8, make_uint4(hl ? 0u : pk_bf16(1.f, 1.f), hl ? 0u : pk_bf16(1.f, 0.f), 0u, 0u));
+  auto read_xrows = [&](const float* lr, const float* dr, int t) {
+    xl = *(const uint2*)(lr + 2 * (32 * t + (lane & 31)));
+    xd = *(const uint2*)(dr + 2 * (32 * t + (lane & 31)));
   };
   unsigned up[8], ud[8];  // packed P / dS of the pending B (words 4ss..4ss+3: 16-row half ss)
   bf16x8 tg0[2], tg1[2], tq0[2], tq1[2];
@@ -694,7 +711,16 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
     constexpr int SA = decltype(sa)::value, TA = decltype(ta)::value, SB = decltype(sb)::value;
     constexpr int TB = decltype(tb)::value, SN = decltype(sn_)::value, TN = decltype(tn)::value;
     constexpr bool BAR = decltype(bar)::value;
-    f32x16 s = sn, dp = dn;
+    f32x16 s, dp;
+    if constexpr (XR) {
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, make_uint4(xl.x, xl.y, 0u, 0u)), xb,
+                                                  zero16(), 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, make_uint4(xd.x, xd.y, 0u, 0u)), xb,
+                                                   zero16(), 0, 0, 0);
+    } else {
+      s = sn;
+      dp = dn;
+    }
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       const int ks = g >> 1;
@@ -721,7 +747,11 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
         default: dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq1[ss], dk1, 0, 0, 0); break;
       }
       if (more) {
-        if (g & 1) read_rows(srow[SN][0], srow[SN][1], TN, g >> 1);
+        if constexpr (XR) {
+          if (g == 3) read_xrows(srow[SN][0], srow[SN][1], TN);
+        } else if (g & 1) {
+          read_rows(srow[SN][0], srow[SN][1], TN, g >> 1);
+        }
         if (g == 6) read_frag(smem[SN][0], smem[SN][1], TN, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -745,8 +775,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  if constexpr (XR) {
+    read_xrows(srow[0][0], srow[0][1], 0);
+  } else {
 #pragma unroll
-  for (int part = 0; part < 4; ++part) read_rows(srow[0][0], srow[0][1], 0, part);
+    for (int part = 0; part < 4; ++part) read_rows(srow[0][0], srow[0][1], 0, part);
+  }
   read_frag(smem[0][0], smem[0][1], 0, 0);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -1067,7 +1101,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v3_kernel(const bf1
                                                                 float* __restrict__ ndeltap, int N, int Npad, int H,
                                                                 bf16* __restrict__ dqkv, float scale,
                                                                 const bf16* __restrict__ out,
-                                                                const float* __restrict__ lse) {
+                                                                const float* __restrict__ lse,
+                                                                unsigned* __restrict__ xpair, long xstride) {
   __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1099,6 +1134,10 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v3_kernel(const bf1
     if (hl == 0 && q < Npad) {
       nlse2p[(long)z * Npad + q] = -lse2;
       ndeltap[(long)z * Npad + q] = -dlt;
+      if (xpair) {  // the same as bf16 triples, for the dK/dV kernel's extra chain MFMA
+        ((uint2*)xpair)[(long)z * Npad + q] = split3_bf16(-lse2);
+        ((uint2*)(xpair + xstride))[(long)z * Npad + q] = split3_bf16(-dlt);
+      }
     }
   }
   f32x16 a0 = zero16(), a1 = zero16();
@@ -1309,7 +1348,8 @@ long ld_scores(long N) { return (N + 7) / 8 * 8; }
 }  // namespace
 
 extern "C" long ivit_attn_workspace(int dtype, long B, long N, long H, long Dh, int backward) {
-  if (dtype == IVIT_BF16) return backward ? 2 * B * H * ((N + AK - 1) / AK * AK) * 4 : 0;
+  // bf16 backward: -lse2 and -delta rows (f32) and the same as bf16 triples (2 words each)
+  if (dtype == IVIT_BF16) return backward ? 6 * B * H * ((N + AK - 1) / AK * AK) * 4 : 0;
   const long one = B * H * N * ld_scores(N) * 4;
   return backward ? 2 * one : one;
 }
@@ -1530,6 +1570,13 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   const long Npad = (N + AK - 1) / AK * AK;
   float* lse2p = (float*)work;
   float* deltap = lse2p + B * H * Npad;
+  unsigned* xpair = (unsigned*)(deltap + B * H * Npad);
+  // IVIT_ATTN_XR=1: dK/dV with the row constants through the extra chain MFMA (correct, measured
+  // 0.825 vs 0.812 ms per pair: the two MFMAs cost more than the LDS reads they remove)
+  static const bool xr = [] {
+    const char* e = getenv("IVIT_ATTN_XR");
+    return e && atoi(e) != 0;
+  }();
   // dQ also forms the row constants (-lse2, -delta) the dK/dV kernel reads: no rows kernel.
   // 4 waves per workgroup, two workgroups per CU: 8-wave workgroups (half the L2 -> LDS bytes,
   // one per CU) measured 0.875 vs 0.814 ms per pair (the 8-wave tile barrier, no second
@@ -1537,7 +1584,8 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   constexpr int BW = 4;
   const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
   kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
+            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse,
+            xpair, 2 * B * H * Npad);
   const char* v4e = getenv("IVIT_ATTN_DKV_V4");
   if (v4e && atoi(v4e) == 1) {  // 64 keys per wave, one wave per SIMD (attn_bwd_dkv_v4_kernel)
     const dim3 g4(ivit_cdiv(N, 64 * BW), B * H);
@@ -1547,6 +1595,10 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
     const dim3 g4(ivit_cdiv(N, 128), B * H);
     kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<2>, g4, dim3(128), st, (const bf16*)qkv,
               (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
+  } else if (xr) {  // row constants through one extra MFMA per chain (bf16 pairs)
+    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW, true>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+              (const bf16*)dout, (const float*)xpair, (const float*)(xpair + 2 * B * H * Npad), (int)N, (int)Npad, (int)H,
+              (bf16*)dqkv, 0.69314718055994531f);
   } else {
     kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
               (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
