@@ -77,3 +77,21 @@ def test_map_raster_dense_and_edge_geometry():
     ref = O.rasterize_map_np(m, pose)
     assert ref.sum() > 1000
     assert np.array_equal(got, ref), np.argwhere(got != ref)[:8]
+
+
+def test_map_fill_odd_slopes_hand_derived():
+    """The fill kernel on the hand-derived odd-slope triangle of tests/test_oracle_golden.py
+    (truncated 16.16 slopes, floor spans, half-open edge rows — OpenCV drawing.cpp semantics):
+    a crosswalk polygon at pixel offset (100, 50) must give exactly that pixel set in channel 3
+    and nothing elsewhere (parity unpinned at the OpenCV level; the convention is pinned here)."""
+    import utils
+    from test_oracle_golden import ODD_SLOPE_TRIANGLE, odd_slope_expected
+    T = lambda px, py: {"x": (300.0 - py) * 0.2, "y": (px - 360.0) * 0.2}  # pose at the origin, yaw 0
+    pose = {"tx_m": 0.0, "ty_m": 0.0, "qx": 0.0, "qy": 0.0, "qz": 0.0, "qw": 1.0}
+    ox, oy = 100, 50
+    m = {"lane_segments": {}, "pedestrian_crossings": {"c": {"polygon": [T(ox + x, oy + y)
+                                                                         for x, y in ODD_SLOPE_TRIANGLE]}}}
+    got = utils.rasterize_map_ego_centric(m, pose).cpu().numpy()
+    exp = odd_slope_expected(400, 720, ox, oy).astype(np.float32)
+    assert np.array_equal(got[3], exp), np.argwhere(got[3] != exp)[:8]
+    assert got.sum() == exp.sum()

@@ -244,6 +244,43 @@ def test_cv_raster_primitives():
     assert img.sum() == 6 and img[2].all()
 
 
+# Triangle A(0,0) B(7,3) C(2,5), edges C->A, A->B, B->C, derived by hand from OpenCV's
+# drawing.cpp semantics (LINE_8, shift 0) — not from the restatement:
+#  CollectPolyEdges: x = x_top << 16, dx = (X_b - X_a) / (y_b - y_a) in C integer division
+#    (truncates toward 0): C->A dx = 131072 / 5 = 26214 (not 26214.4), A->B dx = 458752 / 3 =
+#    152917, B->C dx = -327680 / 2 = -163840; an edge is active on y0 <= y < y1.
+#  FillEdgeCollection (delta = 0 for LINE_8): span [x_l >> 16, x_r >> 16] (floor, no rounding):
+#    y0: [0, 0]; y1: [0, 26214 >> 16 = 0 .. 152917 >> 16 = 2]; y2: [0, 305834 >> 16 = 4]
+#    (4.67 -> 4); y3: A->B retired, [78642 >> 16 = 1, 458752 >> 16 = 7];
+#    y4: [104856 >> 16 = 1, 294912 >> 16 = 4] (4.5 -> 4); y5 = y_max: no span.
+#  Line (LineIterator, 8-connected, left to right, err = major - 2 minor) for each edge:
+#    C->A (0,0)(0,1)(1,2)(1,3)(2,4)(2,5); A->B (0,0)(1,0)(2,1)(3,1)(4,2)(5,2)(6,3)(7,3);
+#    B->C (2,5)(3,5)(4,4)(5,4)(6,3)(7,3).
+ODD_SLOPE_TRIANGLE = [(0, 0), (7, 3), (2, 5)]
+ODD_SLOPE_ROWS = {0: (0, 1), 1: (0, 3), 2: (0, 5), 3: (1, 7), 4: (1, 5), 5: (2, 3)}  # row: (x_first, x_last)
+
+
+def odd_slope_expected(H=10, W=10, ox=0, oy=0):
+    img = np.zeros((H, W), np.uint8)
+    for y, (a, b) in ODD_SLOPE_ROWS.items():
+        img[oy + y, ox + a:ox + b + 1] = 1
+    return img
+
+
+def test_cv_fill_poly_odd_slopes_hand_derived():
+    """fillPoly's fixed-point conventions asserted explicitly on odd slopes (truncated dx, floor
+    spans, half-open edge rows): the restatement reproduces the hand-derived pixel set. The map
+    rasteriser's outputs remain parity unpinned at the OpenCV level (cv2 absent here); this pins
+    the convention, tests/test_gpu_map.py checks the kernel on the same triangle."""
+    img = np.zeros((10, 10), np.uint8)
+    O.cv_fill_poly(img, ODD_SLOPE_TRIANGLE)
+    assert np.array_equal(img, odd_slope_expected()), np.argwhere(img != odd_slope_expected())
+    for rot in (1, 2):  # vertex order does not matter
+        img = np.zeros((10, 10), np.uint8)
+        O.cv_fill_poly(img, ODD_SLOPE_TRIANGLE[rot:] + ODD_SLOPE_TRIANGLE[:rot])
+        assert np.array_equal(img, odd_slope_expected())
+
+
 def test_fusion_stride2_oracle_vs_golden():
     """fusion_block_stride=2 (model_vit.py:55,125-128): the oracle's strided fusion block vs the
     reference's own model."""
