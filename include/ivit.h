@@ -189,6 +189,14 @@ enum { IVIT_KT_ATTN_FWD = 0, IVIT_KT_ATTN_BWD_DQ = 1, IVIT_KT_ATTN_BWD_DKV = 2, 
 int ivit_ktime_arm(int on);
 int ivit_ktime_read(int tag, double* start_ms, double* stop_ms, long cap, long* count);
 
+/* ---- Diagnostic per-workgroup stamps (no reference counterpart; tools/panel_stamps.py).
+ * buf (device, 8 x u64 per workgroup, cap u64 in all) non-null: the row-panel kernels
+ * (ivit_linear_fwd_panel, ivit_linear_dgrad_gelu_panel, ivit_linear_resid_ln_fwd,
+ * ivit_linear_dgrad_ln_bwd) launch their stamping builds and write, per workgroup b at
+ * buf[8 b ..]: shader clock at entry, at the first K stage's data ready, after the main loop,
+ * at exit; 100-MHz real time at entry and exit; HW_ID | XCC_ID << 32; 0. Null: off (default).  */
+int ivit_debug_stamps(void* buf, long cap);
+
 /* ---- LayerNorm over the last dim D (timm norm1/norm2/norm eps 1e-6; adapters eps 1e-5).
  *      Input rows r -> (r / rpb) * rstride + roff + r % rpb (rpb = 0: identity) of X (f32).    */
 int ivit_layernorm_fwd(const float* X, long ldx, long rpb, long rstride, long roff, long M, long D,

@@ -8,6 +8,15 @@
 using namespace ivit;
 
 static thread_local char g_err[512];
+static u64* g_stamp_buf = nullptr;
+static long g_stamp_cap = 0;
+u64* ivit_stamp_buffer(long blocks) { return g_stamp_buf && 8 * blocks <= g_stamp_cap ? g_stamp_buf : nullptr; }
+extern "C" int ivit_debug_stamps(void* buf, long cap) {
+  g_stamp_buf = (u64*)buf;
+  g_stamp_cap = buf ? cap : 0;
+  return 0;
+}
+
 void ivit_set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);

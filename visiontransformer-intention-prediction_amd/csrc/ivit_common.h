@@ -108,6 +108,30 @@ template <typename O> IVIT_DEV float gelu_grad_t(float x) {
 
 IVIT_DEV bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// ---------------------------------------------------------------- diagnostic stamps
+// (ivit_debug_stamps) Kernels built with a stamping flag record clocks per workgroup; lane 0 of
+// wave 0 writes them with an ordinary vector store into a buffer no other code reads.
+typedef unsigned long long u64;
+IVIT_DEV u64 clk_now() { return __builtin_amdgcn_s_memtime(); }
+IVIT_DEV u64 rclk_now() { return __builtin_amdgcn_s_memrealtime(); }
+IVIT_DEV u64 hw_ids() {
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID, 32 bits
+  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+  return (u64)hw | ((u64)xcc << 32);
+}
+struct Stamps {
+  u64 t0, t1, t2, r0;
+  IVIT_DEV void begin() { t0 = clk_now(); r0 = rclk_now(); t1 = t2 = 0; }
+  IVIT_DEV void end(u64* buf) {
+    const u64 t3 = clk_now(), r3 = rclk_now();
+    if (threadIdx.x == 0) {
+      u64* o = buf + 8L * blockIdx.x;
+      o[0] = t0; o[1] = t1; o[2] = t2; o[3] = t3; o[4] = r0; o[5] = r3; o[6] = hw_ids(); o[7] = 0;
+    }
+  }
+};
+u64* ivit_stamp_buffer(long blocks);  // host: the armed buffer if it holds `blocks` records, else null
+
 // store 8 consecutive values (vectorised when aligned and complete)
 template <typename O>
 IVIT_DEV void store8(O* p, const float (&x)[8], int nv) {

@@ -22,6 +22,7 @@ IVIT_DEV void wait_vm(int n) {
     PANEL_VM(1) PANEL_VM(2) PANEL_VM(3) PANEL_VM(4) PANEL_VM(5) PANEL_VM(6) PANEL_VM(7) PANEL_VM(8) PANEL_VM(9)
     PANEL_VM(10) PANEL_VM(11) PANEL_VM(12) PANEL_VM(13) PANEL_VM(14) PANEL_VM(15) PANEL_VM(16) PANEL_VM(17)
     PANEL_VM(18) PANEL_VM(19) PANEL_VM(20) PANEL_VM(21) PANEL_VM(22) PANEL_VM(23) PANEL_VM(24)
+    PANEL_VM(25) PANEL_VM(26) PANEL_VM(27) PANEL_VM(28) PANEL_VM(29) PANEL_VM(30) PANEL_VM(31) PANEL_VM(32)
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }

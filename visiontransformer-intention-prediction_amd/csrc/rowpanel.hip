@@ -57,9 +57,11 @@ IVIT_DEV PanelA panel_a_setup(const bf16* A, long lda, int M, int m0, int wv, in
 
 // acc[9][3] = rows m0 .. m0+143 of A (K = 64 KT) times the 48 columns of 16-column blocks
 // nb0 .. nb0+2 of a packed weight with NB16 blocks in total.
-template <int W = 8>
+// TR: the MFMA operands swapped (weights as A, the panel as B), so acc holds the output
+// transposed: lane l has columns 4 (l >> 4) + i, i < 4, of row l & 15 of each 16 x 16 block.
+template <int W = 8, bool TR = false>
 IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA& pa, const u32x4* wpack, int NB16,
-                             int nb0, int KT, int wv, int lane) {
+                             int nb0, int KT, int wv, int lane, u64* t_first = nullptr) {
   constexpr int PW = (RP_PIECES + W - 1) / W;
   auto issue_a = [&](int kt) {
     char* st = smem + (kt % RP_NS) * RP_STAGE + pa.pc0 * 1024;
@@ -86,6 +88,7 @@ IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA&
     wait_vm((kt + 1 < KT ? npc + 2 * NBW : 0) + (kt + 2 < KT ? npc : 0));
     tie(cur);
     __builtin_amdgcn_s_barrier();  // every wave's pieces of A(kt); stage (kt-1) % 4 free
+    if (t_first && kt == 0) *t_first = clk_now();
     if (kt + 2 < KT) issue_b(kt + 2, nb2);
     if (kt + 3 < KT) issue_a(kt + 3);
     const char* ia = smem + (kt % RP_NS) * RP_STAGE;
@@ -107,7 +110,10 @@ IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA&
       for (int j = 0; j < NBW; ++j) {
         union { u32x4 u; bf16x8 v; } bw;
         bw.u = cur[t * NBW + j];
-        acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[f % 4], bw.v, acc[mb][j], 0, 0, 0);
+        if constexpr (TR)
+          acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw.v, fr[f % 4], acc[mb][j], 0, 0, 0);
+        else
+          acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr[f % 4], bw.v, acc[mb][j], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -132,20 +138,24 @@ IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA&
 //   dXs = bf16(dX * scale[m / rps]) (optional), per-workgroup partial column sums of dY xh / dY.
 // Pointer roles in BWD: R = dres (nullable), X = X (read), Y = dXs, mean / rstd read, bias unused,
 // part = [gridDim.x][2][384] partials (reduced by colreduce_kernel).
-template <bool BWD>
+template <bool BWD, bool ST = false>
 __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
     const bf16* __restrict__ A, long lda, int M, int K, const u32x4* __restrict__ wpack,
     const float* __restrict__ bias, const float* R, long ldr, const float* __restrict__ scale, int rps,
     const float* __restrict__ gamma, const float* __restrict__ beta, float eps, float* X, long ldx,
-    bf16* __restrict__ Y, long ldy, float* mean, float* rstd, float* dX, long lddx, float* __restrict__ part) {
+    bf16* __restrict__ Y, long ldy, float* mean, float* rstd, float* dX, long lddx, float* __restrict__ part,
+    u64* stamps) {
   __shared__ __attribute__((aligned(16))) char smem[RP_NS * RP_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * RP_MT;
+  Stamps stp;
+  if constexpr (ST) stp.begin();
 
   PanelA pa = panel_a_setup(A, lda, M, m0, wv, lane);
   f32x4 acc[RP_MB][NBW];
-  panel_mainloop(acc, smem, pa, wpack, RP_N / 16, wv * NBW, K / 64, wv, lane);
+  panel_mainloop(acc, smem, pa, wpack, RP_N / 16, wv * NBW, K / 64, wv, lane, ST ? &stp.t1 : nullptr);
+  if constexpr (ST) stp.t2 = clk_now();
 
   // ---- epilogue, one 16-row block at a time through LDS
   __builtin_amdgcn_s_barrier();  // every wave is done with the A ring
@@ -298,6 +308,7 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
       part[(long)blockIdx.x * 2 * RP_N + c] = a;
     }
   }
+  if constexpr (ST) stp.end(stamps);
 }
 
 // ============================================================================= wide outputs
@@ -309,15 +320,114 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
 //   EPI_DGELU:  Y = bf16(acc * gelu'(P[m][n]))                                (fc2 dgrad, W packed transposed)
 constexpr int EPI_QS = 0, EPI_GELU = 1, EPI_DGELU = 2;
 
+// Transposed-accumulator epilogue of the wide kernels (EV = 1): acc[mb][j][i] is column
+// nw + 16 j + 4 (lane >> 4) + i of row m0 + 16 mb + (lane & 15).
+template <int EPI>
+IVIT_DEV void wide_epilogue_tr(const f32x4 (&acc)[RP_MB][NBW], int nw, int m0, int M, const float* __restrict__ bias,
+                               int qcols, float qscale, bf16* __restrict__ Y, long ldy, bf16* __restrict__ P,
+                               long ldp, int lane) {
+  const int g = lane >> 4, tl = lane & 15;
+  const bool odd = g & 1;
+  const int cb = nw + 4 * g;  // + 16 j: this lane's first column in block j
+  float bv[NBW][4];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[j][i] = (EPI != EPI_DGELU && bias) ? bias[cb + 16 * j + i] : 0.f;
+  const float qs = (EPI == EPI_QS && nw < qcols) ? qscale : 1.f;  // qcols is a multiple of 384 (of the chunk)
+  // packed Y (and P) words of block (mb, j); DGELU: h = the 4 pre-activations
+  auto compute = [&](int mb, int j, uint2 h, uint2& y, uint2& p) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = acc[mb][j][i] + bv[j][i];
+    if constexpr (EPI == EPI_QS) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] *= qs;
+    } else if constexpr (EPI == EPI_GELU) {
+      p = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = gelu_t<bf16>(v[i]);
+    } else {
+      Pack4 q;
+      q.u = h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] *= gelu_grad_t<bf16>((float)q.h[i]);
+    }
+    y = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+  };
+  auto load_h = [&](int mb, uint2 (&h)[NBW]) {
+    const bf16* pr = P + (long)min(m0 + 16 * mb + tl, M - 1) * ldp + cb;
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) h[j] = *(const uint2*)(pr + 16 * j);
+  };
+  uint2 h0[NBW], h1[NBW];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) h0[j] = h1[j] = make_uint2(0, 0);
+#pragma unroll
+  for (int q = 0; q < RP_MB / 2; ++q) {
+    const int mb0 = 2 * q, mb1 = 2 * q + 1;
+    if constexpr (EPI == EPI_DGELU) {
+      load_h(mb0, h0);
+      load_h(mb1, h1);
+    }
+    const int m = m0 + 16 * (odd ? mb1 : mb0) + tl;
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      uint2 y0, y1, p0, p1;
+      compute(mb0, j, h0[j], y0, p0);
+      compute(mb1, j, h1[j], y1, p1);
+      // odd rows of (block mb0's words) <-> even rows of (block mb1's words)
+      const auto s0 = __builtin_amdgcn_permlane16_swap(y0.x, y1.x, false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(y0.y, y1.y, false, false);
+      const uint4 out = odd ? make_uint4(s0[0], s1[0], y1.x, y1.y) : make_uint4(y0.x, y0.y, s0[1], s1[1]);
+      const int c = cb + 16 * j - (odd ? 4 : 0);
+      if (m < M) *(uint4*)(Y + (long)m * ldy + c) = out;
+      if constexpr (EPI == EPI_GELU) {
+        if (P) {
+          const auto t0 = __builtin_amdgcn_permlane16_swap(p0.x, p1.x, false, false);
+          const auto t1 = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
+          const uint4 po = odd ? make_uint4(t0[0], t1[0], p1.x, p1.y) : make_uint4(p0.x, p0.y, t0[1], t1[1]);
+          if (m < M) *(uint4*)(P + (long)m * ldp + c) = po;
+        }
+      }
+    }
+  }
+  if constexpr (RP_MB % 2 == 1) {  // the last block alone: 8-B stores
+    constexpr int mb = RP_MB - 1;
+    if constexpr (EPI == EPI_DGELU) load_h(mb, h0);
+    const int m = m0 + 16 * mb + tl;
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      uint2 y, p;
+      compute(mb, j, h0[j], y, p);
+      if (m < M) {
+        *(uint2*)(Y + (long)m * ldy + cb + 16 * j) = y;
+        if constexpr (EPI == EPI_GELU) {
+          if (P) *(uint2*)(P + (long)m * ldp + cb + 16 * j) = p;
+        }
+      }
+    }
+  }
+}
+
 // W = 8: one 512-thread workgroup per 144-row panel walks the N / 384 column chunks (one per CU).
 // W = 4: a 256-thread workgroup per (panel, 192-column chunk), two per CU (2 x 74 KiB LDS): the
 // epilogue of one (VALU + stores) runs beside the other's MFMA main loop instead of after it.
-template <int EPI, int W>
+// EV = 1 (Y, and P when written, 16-B aligned with ldy, ldp multiples of 8): the transposed
+// accumulators (panel_mainloop<W, true>) go out straight from registers — each lane holds 4
+// consecutive columns of one row per block; one v_permlane16_swap per word pairs lane l's row
+// of block mb with lane l ^ 16's of block mb + 1, so every lane stores 8 consecutive columns
+// (16 B, 32 contiguous bytes per row per instruction): no LDS round trip, no barriers. The
+// round-2 form (EV = 0: through an f32 LDS tile, 8-B stores, two barriers per 16-row block)
+// measured 4.2 us of a 12.5-us workgroup on the qkv projection (tools/panel_stamps.py).
+template <int EPI, int W, bool ST = false, int EV = 0>
 __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16* __restrict__ A, long lda, int M,
                                                                       int K, const u32x4* __restrict__ wpack, int N,
                                                                       const float* __restrict__ bias, int qcols,
                                                                       float qscale, bf16* __restrict__ Y, long ldy,
-                                                                      bf16* __restrict__ P, long ldp) {
+                                                                      bf16* __restrict__ P, long ldp, u64* stamps) {
+  Stamps stp;
+  if constexpr (ST) stp.begin();
   constexpr int CW = 48 * W, TLD = CW + 4, LPR = CW / 12;  // chunk width, T row stride, lanes per row
   __shared__ __attribute__((aligned(16))) char smem[RP_NS * RP_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -341,7 +451,14 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
 #pragma unroll 1
   for (int nc = nc_begin; nc < nc_end; ++nc) {
     f32x4 acc[RP_MB][NBW];
-    panel_mainloop<W>(acc, smem, pa, wpack, N / 16, nc * (CW / 16) + wv * NBW, K / 64, wv, lane);
+    panel_mainloop<W, EV == 1>(acc, smem, pa, wpack, N / 16, nc * (CW / 16) + wv * NBW, K / 64, wv, lane,
+                               ST && nc == nc_begin ? &stp.t1 : nullptr);
+    if constexpr (ST) stp.t2 = clk_now();
+    if constexpr (EV == 1) {
+      if (nc + 1 < nc_end) __builtin_amdgcn_s_barrier();  // the next chunk's prologue rewrites the A ring
+      wide_epilogue_tr<EPI>(acc, nc * CW + wv * NBW * 16, m0, M, bias, qcols, qscale, Y, ldy, P, ldp, lane);
+      continue;
+    }
     __builtin_amdgcn_s_barrier();  // every wave is done with the A ring
     const int n0 = nc * CW;
     float bv[NBW];
@@ -412,12 +529,36 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
       __builtin_amdgcn_s_barrier();  // T is rewritten by the next block (or the next chunk's ring)
     }
   }
+  if constexpr (ST) stp.end(stamps);
 }
 
 }  // namespace
 }  // namespace ivit
 
 using namespace ivit;
+
+namespace {
+template <bool BWD>
+auto ln_kernel(bool st) {
+  return st ? rowpanel_ln_kernel<BWD, true> : rowpanel_ln_kernel<BWD, false>;
+}
+// The wide kernel build for (EPI, stamps, epilogue form): EV = 1 needs 16-B aligned rows of Y
+// (and of P when the kernel writes it); IVIT_WIDE_EPI=0 forces the LDS-tile epilogue (A/B).
+template <int EPI>
+void launch_wide(dim3 g, hipStream_t st, bool ev1, u64* sb, const bf16* A, long lda, int M, int K, const u32x4* wp,
+                 int N, const float* bias, int qcols, float qscale, bf16* Y, long ldy, bf16* P, long ldp) {
+  static const bool off = [] {
+    const char* e = getenv("IVIT_WIDE_EPI");
+    return e && atoi(e) == 0;
+  }();
+  ev1 = ev1 && !off && EPI == EPI_QS;  // GELU / DGELU: the LDS-tile form measured faster (VALU-bound epilogue;
+                                       // the transposed DGELU's 8-B pre-activation loads cost more)
+  auto k = ev1 ? (sb ? rowpanel_wide_kernel<EPI, 4, true, 1> : rowpanel_wide_kernel<EPI, 4, false, 1>)
+               : (sb ? rowpanel_wide_kernel<EPI, 4, true, 0> : rowpanel_wide_kernel<EPI, 4, false, 0>);
+  hipLaunchKernelGGL(k, g, dim3(256), 0, st, A, lda, M, K, wp, N, bias, qcols, qscale, Y, ldy, P, ldp, sb);
+}
+bool al16_rows(const void* p, long ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && ld % 8 == 0); }
+}  // namespace
 
 extern "C" int ivit_linear_resid_ln_fwd(const void* A, long lda, long M, long N, long K, const void* wpack,
                                         const float* bias, const float* R, long ldr, const float* scale, long rps,
@@ -432,9 +573,11 @@ extern "C" int ivit_linear_resid_ln_fwd(const void* A, long lda, long M, long N,
   IVIT_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)wpack & 15) == 0 && ((uintptr_t)R & 15) == 0 &&
                      ((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 7) == 0,
                  "ivit_linear_resid_ln_fwd: misaligned operand");
-  hipLaunchKernelGGL(rowpanel_ln_kernel<false>, dim3(ivit_cdiv(M, RP_MT)), dim3(512), 0, ivit_stream(stream),
-                     (const bf16*)A, lda, (int)M, (int)K, (const u32x4*)wpack, bias, R, ldr, scale, (int)rps, gamma,
-                     beta, eps, X, ldx, (bf16*)Y, ldy, mean, rstd, nullptr, 0L, nullptr);
+  u64* sb = ivit_stamp_buffer(ivit_cdiv(M, RP_MT));
+  hipLaunchKernelGGL(ln_kernel<false>(sb != nullptr), dim3(ivit_cdiv(M, RP_MT)),
+                     dim3(512), 0, ivit_stream(stream), (const bf16*)A, lda, (int)M, (int)K, (const u32x4*)wpack,
+                     bias, R, ldr, scale, (int)rps, gamma, beta, eps, X, ldx, (bf16*)Y, ldy, mean, rstd, nullptr, 0L,
+                     nullptr, sb);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -458,9 +601,11 @@ extern "C" int ivit_linear_dgrad_ln_bwd(const void* dY, long lddy, long M, long 
                  "ivit_linear_dgrad_ln_bwd: misaligned operand");
   hipStream_t st = ivit_stream(stream);
   const int nb = ivit_cdiv(M, RP_MT);
-  hipLaunchKernelGGL(rowpanel_ln_kernel<true>, dim3(nb), dim3(512), 0, st, (const bf16*)dY, lddy, (int)M, (int)K,
-                     (const u32x4*)wpack_t, nullptr, dres, ldr, scale, (int)rps, gamma, nullptr, 0.f,
-                     (float*)X, ldx, (bf16*)dXs, (long)RP_N, (float*)mean, (float*)rstd, dX, lddx, (float*)work);
+  u64* sb = ivit_stamp_buffer(nb);
+  hipLaunchKernelGGL(ln_kernel<true>(sb != nullptr), dim3(nb), dim3(512), 0, st,
+                     (const bf16*)dY, lddy, (int)M, (int)K, (const u32x4*)wpack_t, nullptr, dres, ldr, scale,
+                     (int)rps, gamma, nullptr, 0.f, (float*)X, ldx, (bf16*)dXs, (long)RP_N, (float*)mean,
+                     (float*)rstd, dX, lddx, (float*)work, sb);
   IVIT_LAUNCH_CHECK();
   launch_colreduce(st, (const float*)work, nb, 2 * N, (int)(2 * N), dgamma, (int)N, dbeta, accumulate);
   IVIT_LAUNCH_CHECK();
@@ -481,12 +626,13 @@ extern "C" int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, lo
                  "ivit_linear_fwd_panel: misaligned operand");
   const dim3 g(ivit_cdiv(M, RP_MT) * (N / 192));
   hipStream_t st = ivit_stream(stream);
+  u64* sb = ivit_stamp_buffer(g.x);
   if (act == IVIT_ACT_GELU)
-    hipLaunchKernelGGL((rowpanel_wide_kernel<EPI_GELU, 4>), g, dim3(256), 0, st, (const bf16*)A, lda, (int)M, (int)K,
-                       (const u32x4*)wpack, (int)N, bias, 0, 1.f, (bf16*)Y, ldy, (bf16*)Ypre, ldpre);
+    launch_wide<EPI_GELU>(g, st, al16_rows(Y, ldy) && al16_rows(Ypre, ldpre), sb, (const bf16*)A, lda, (int)M,
+                          (int)K, (const u32x4*)wpack, (int)N, bias, 0, 1.f, (bf16*)Y, ldy, (bf16*)Ypre, ldpre);
   else
-    hipLaunchKernelGGL((rowpanel_wide_kernel<EPI_QS, 4>), g, dim3(256), 0, st, (const bf16*)A, lda, (int)M, (int)K,
-                       (const u32x4*)wpack, (int)N, bias, (int)qcols, qscale, (bf16*)Y, ldy, nullptr, 0L);
+    launch_wide<EPI_QS>(g, st, al16_rows(Y, ldy), sb, (const bf16*)A, lda, (int)M, (int)K, (const u32x4*)wpack,
+                        (int)N, bias, (int)qcols, qscale, (bf16*)Y, ldy, nullptr, 0L);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -501,10 +647,10 @@ extern "C" int ivit_linear_dgrad_gelu_panel(const void* dY, long lddy, long M, l
   IVIT_CHECK_ARG(((uintptr_t)dY & 15) == 0 && ((uintptr_t)wpack_t & 15) == 0 && ((uintptr_t)dX & 7) == 0 &&
                      ((uintptr_t)pre & 7) == 0,
                  "ivit_linear_dgrad_gelu_panel: misaligned operand");
-  hipLaunchKernelGGL((rowpanel_wide_kernel<EPI_DGELU, 4>), dim3(ivit_cdiv(M, RP_MT) * (N / 192)), dim3(256), 0,
-                     ivit_stream(stream),
-                     (const bf16*)dY, lddy, (int)M, (int)K, (const u32x4*)wpack_t, (int)N, nullptr, 0, 1.f,
-                     (bf16*)dX, lddx, (bf16*)pre, ldpre);
+  const dim3 g(ivit_cdiv(M, RP_MT) * (N / 192));
+  u64* sb = ivit_stamp_buffer(g.x);
+  launch_wide<EPI_DGELU>(g, ivit_stream(stream), al16_rows(dX, lddx), sb, (const bf16*)dY, lddy, (int)M, (int)K,
+                         (const u32x4*)wpack_t, (int)N, nullptr, 0, 1.f, (bf16*)dX, lddx, (bf16*)pre, ldpre);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
