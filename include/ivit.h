@@ -26,6 +26,7 @@ extern "C" {
 #define IVIT_ACT_NONE 0
 #define IVIT_ACT_GELU 1
 #define IVIT_ACT_RELU 2
+#define IVIT_ACT_GELU_D 3 /* ivit_linear_fwd_panel only: GELU, second output = GELU'(pre-activation) */
 
 const char* ivit_version(void);
 const char* ivit_last_error(void);
@@ -74,10 +75,16 @@ int ivit_linear_dgrad_ln_bwd(const void* dY, long lddy, long M, long N, long K, 
  *   act GELU: Ypre = A W^T + bias (if non-null), Y = gelu(Ypre)   (W packed by ivit_patch_weight_pack) */
 int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, long K, const void* wpack, const float* bias,
                           int act, long qcols, float qscale, void* Y, long ldy, void* Ypre, long ldpre, void* stream);
-/* dX[M,N] = (dY[M,K] W[K,N]) * gelu'(pre[M,N])  (Mlp.fc2 dgrad into fc1's pre-activation; W packed
+/*   act GELU_D: Ypre = gelu'(A W^T + bias) (if non-null), Y = gelu(A W^T + bias): the derivative
+ *   the backward needs, from the f32 pre-activation, instead of the pre-activation itself.
+ * dX[M,N] = (dY[M,K] W[K,N]) * gelu'(pre[M,N])  (Mlp.fc2 dgrad into fc1's pre-activation; W packed
  * transposed by ivit_weight_pack_t), bf16. */
 int ivit_linear_dgrad_gelu_panel(const void* dY, long lddy, long M, long N, long K, const void* wpack_t,
                                  const void* pre, long ldpre, void* dX, long lddx, void* stream);
+/* dX[M,N] = (dY[M,K] W[K,N]) * G[M,N]  (bf16; G = the GELU' that ivit_linear_fwd_panel wrote with
+ * act GELU_D: the same fc2 dgrad with no GELU' evaluation in its epilogue). */
+int ivit_linear_dgrad_mul_panel(const void* dY, long lddy, long M, long N, long K, const void* wpack_t, const void* G,
+                                long ldg, void* dX, long lddx, void* stream);
 /* The weight and bias gradients of one timm Block's four linears (Mlp.fc2, Mlp.fc1, Attention.proj,
  * Attention.qkv; model_vit.py:64,71 -> timm Block backward) in one grouped launch + one reduce:
  *   dW_g = dY_g^T X_g (f32 [N][K]), db_g = colsum(dY_g) (f32 [N], may be null), bf16 token-major

@@ -518,6 +518,32 @@ def test_panel_wide(M, N, K, mode):
         assert _rel(pre.float(), rpre.float()) < 8e-3 and _rel(got.float(), ref.float()) < 8e-3
 
 
+@pytest.mark.parametrize("M,N,K", [(36008, 1536, 384), (300, 768, 128), (145, 1536, 384), (1, 384, 64)])
+def test_panel_gelu_derivative_pair(M, N, K):
+    """fc1 with GELU' as its second output (act GELU_D: y = gelu(z), g = gelu'(z) from the f32 z =
+    x W^T + b) and the fc2 dgrad that multiplies by it (ivit_linear_dgrad_mul_panel), vs torch on
+    the same bf16 operands: z in f64, exact-erf GELU / GELU' (bf16-output tolerance)."""
+    import ops
+    from _lib import ACT_GELU_D, BF16
+    g = torch.Generator().manual_seed(7 * M + N + K)
+    x = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(N, K, generator=g) / math.sqrt(K)).to(DEV)
+    b = (0.1 * torch.randn(N, generator=g)).to(DEV)
+    y, gp = ops.panel_fwd(x, w, b, act=ACT_GELU_D, want_pre=True)
+    z = x.double().cpu() @ w.to(torch.bfloat16).double().cpu().t() + b.double().cpu()
+    phi = torch.exp(-0.5 * z * z) / math.sqrt(2 * math.pi)
+    cdf = 0.5 * (1 + torch.erf(z / math.sqrt(2)))
+    assert _rel(y.float().cpu(), z * cdf) < 8e-3
+    assert _rel(gp.float().cpu(), cdf + z * phi) < 8e-3
+    # the dgrad side: dx = (dy @ W2) * g
+    dy = torch.randn(M, K, generator=g).to(torch.bfloat16).to(DEV)
+    w2 = (torch.randn(K, N, generator=g) / math.sqrt(K)).to(DEV)
+    dx = ops.panel_dgrad_mul(dy, w2, gp)
+    ref = (dy.double().cpu() @ w2.to(torch.bfloat16).double().cpu()) * gp.double().cpu()
+    assert _rel(dx.float().cpu(), ref) < 8e-3
+    assert dx.shape == (M, N) and dx.dtype == torch.bfloat16
+
+
 def test_patch_im2col_bitexact():
     """bf16 patch matrix (the throughput path's GEMM operand) is exactly the rearranged, rounded raster."""
     from _lib import lib, ptr, stream

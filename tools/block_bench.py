@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch  # noqa: E402
 
 import ops  # noqa: E402
-from _lib import ACT_GELU, BF16  # noqa: E402
+from _lib import ACT_GELU, ACT_GELU_D, BF16  # noqa: E402
 
 torch.manual_seed(0)
 M, D, F = 8 * 4501, 384, 1536
@@ -61,6 +61,9 @@ rows = [
     ("fwd fc2 + resid + LN1'", lambda: ops.linear_resid_ln_fwd(a, w2, b2, x32, scale, 4501, g, beta, 1e-6),
      M * F * B2 + M * D * (F4 + F4 + B2) + 8 * M, 2.0 * M * D * F),
     ("bwd fc2 dgrad x GELU'", lambda: ops.panel_dgrad_gelu(dy, w2, h), M * D * B2 + 2 * M * F * B2, 2.0 * M * D * F),
+    ("fwd fc1 + GELU (+GELU') [train]", lambda: ops.panel_fwd(ln, w1, b1, act=ACT_GELU_D, want_pre=True),
+     M * D * B2 + 2 * M * F * B2, 2.0 * M * F * D),
+    ("bwd fc2 dgrad x G [train]", lambda: ops.panel_dgrad_mul(dy, w2, h), M * D * B2 + 2 * M * F * B2, 2.0 * M * D * F),
     ("bwd fc2 wgrad", lambda: ops.linear_wgrad(dy, a, BF16), M * (D + F) * B2, 2.0 * M * D * F),
     ("bwd fc1 dgrad + LN2 bwd", lambda: ops.linear_dgrad_ln_bwd(dh, w1, x32, g, mean, rstd, dres=x32.clone(),
                                                                 xs_dtype=torch.bfloat16, row_scale=scale, rps=4501),

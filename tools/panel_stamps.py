@@ -12,7 +12,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import ops  # noqa: E402
-from _lib import ACT_GELU, lib  # noqa: E402
+from _lib import ACT_GELU, ACT_GELU_D, lib  # noqa: E402
 
 torch.manual_seed(0)
 M, D, F = 8 * 4501, 384, 1536
@@ -27,6 +27,8 @@ mean, rstd = torch.zeros(M, device=dev), torch.ones(M, device=dev)
 cases = [("qkv fwd (wide QS)", lambda: ops.panel_fwd(ln, wqkv, b3, qcols=D, qscale=ops.Q2_SCALE)),
          ("fc1 fwd (wide GELU+pre)", lambda: ops.panel_fwd(ln, w1, b1, act=ACT_GELU, want_pre=True)),
          ("fc2 dgrad (wide DGELU)", lambda: ops.panel_dgrad_gelu(dy, w2, h)),
+         ("fc1 fwd (wide GELU+GELU')", lambda: ops.panel_fwd(ln, w1, b1, act=ACT_GELU_D, want_pre=True)),
+         ("fc2 dgrad (wide x GELU')", lambda: ops.panel_dgrad_mul(dy, w2, h)),
          ("fc2 fwd + LN (ln<false>)", lambda: ops.linear_resid_ln_fwd(a, w2, bD, x32, scale, 4501, g, beta, 1e-6)),
          ("fc1 dgrad + LN bwd (ln<true>)", lambda: ops.linear_dgrad_ln_bwd(dh, w1, x32, g, mean, rstd, dres=x32.clone(),
                                                                           xs_dtype=torch.bfloat16, row_scale=scale,

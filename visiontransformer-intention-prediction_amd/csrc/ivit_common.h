@@ -101,6 +101,13 @@ IVIT_DEV float gelu_grad_fast(float x) {
   const float e = __expf(-0.5f * x * x);
   return 0.5f * (1.0f + erf_as(x * 0.70710678118654752f, e)) + x * 0.39894228040143268f * e;
 }
+// gelu(x) and gelu'(x) together (one exp, one erf): y = x c, dy = c + x phi(x), c = Phi(x)
+IVIT_DEV void gelu_fast2(float x, float& y, float& dy) {
+  const float e = __expf(-0.5f * x * x);
+  const float c = 0.5f * (1.0f + erf_as(x * 0.70710678118654752f, e));
+  y = x * c;
+  dy = c + x * 0.39894228040143268f * e;
+}
 template <typename O> IVIT_DEV float gelu_t(float x) { return sizeof(O) == 2 ? gelu_fast(x) : gelu_erf(x); }
 template <typename O> IVIT_DEV float gelu_grad_t(float x) {
   return sizeof(O) == 2 ? gelu_grad_fast(x) : gelu_erf_grad(x);

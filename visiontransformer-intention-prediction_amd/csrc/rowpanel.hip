@@ -318,7 +318,11 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
 //   EPI_QS:     Y = bf16((acc + bias[n]) * (n < qcols ? qscale : 1))        (qkv, Q block prescaled)
 //   EPI_GELU:   P = bf16(acc + bias[n]), Y = bf16(gelu(acc + bias[n]))       (fc1 + pre-activation)
 //   EPI_DGELU:  Y = bf16(acc * gelu'(P[m][n]))                                (fc2 dgrad, W packed transposed)
-constexpr int EPI_QS = 0, EPI_GELU = 1, EPI_DGELU = 2;
+//   EPI_GELUD:  P = bf16(gelu'(acc + bias[n])), Y = bf16(gelu(acc + bias[n]))    (fc1, training)
+//   EPI_DMUL:   Y = bf16(acc * P[m][n])   (fc2 dgrad, P = the GELU' EPI_GELUD wrote)
+constexpr int EPI_QS = 0, EPI_GELU = 1, EPI_DGELU = 2, EPI_GELUD = 3, EPI_DMUL = 4;
+constexpr bool epi_reads_p(int e) { return e == EPI_DGELU || e == EPI_DMUL; }
+constexpr bool epi_writes_p(int e) { return e == EPI_GELU || e == EPI_GELUD; }
 
 // Transposed-accumulator epilogue of the wide kernels (EV = 1): acc[mb][j][i] is column
 // nw + 16 j + 4 (lane >> 4) + i of row m0 + 16 mb + (lane & 15).
@@ -333,7 +337,7 @@ IVIT_DEV void wide_epilogue_tr(const f32x4 (&acc)[RP_MB][NBW], int nw, int m0, i
 #pragma unroll
   for (int j = 0; j < NBW; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bv[j][i] = (EPI != EPI_DGELU && bias) ? bias[cb + 16 * j + i] : 0.f;
+    for (int i = 0; i < 4; ++i) bv[j][i] = (!epi_reads_p(EPI) && bias) ? bias[cb + 16 * j + i] : 0.f;
   const float qs = (EPI == EPI_QS && nw < qcols) ? qscale : 1.f;  // qcols is a multiple of 384 (of the chunk)
   // packed Y (and P) words of block (mb, j); DGELU: h = the 4 pre-activations
   auto compute = [&](int mb, int j, uint2 h, uint2& y, uint2& p) {
@@ -347,11 +351,16 @@ IVIT_DEV void wide_epilogue_tr(const f32x4 (&acc)[RP_MB][NBW], int nw, int m0, i
       p = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = gelu_t<bf16>(v[i]);
+    } else if constexpr (EPI == EPI_GELUD) {
+      float d[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gelu_fast2(v[i], v[i], d[i]);
+      p = make_uint2(pk_bf16(d[0], d[1]), pk_bf16(d[2], d[3]));
     } else {
       Pack4 q;
       q.u = h;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] *= gelu_grad_t<bf16>((float)q.h[i]);
+      for (int i = 0; i < 4; ++i) v[i] *= EPI == EPI_DMUL ? (float)q.h[i] : gelu_grad_t<bf16>((float)q.h[i]);
     }
     y = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
   };
@@ -366,7 +375,7 @@ IVIT_DEV void wide_epilogue_tr(const f32x4 (&acc)[RP_MB][NBW], int nw, int m0, i
 #pragma unroll
   for (int q = 0; q < RP_MB / 2; ++q) {
     const int mb0 = 2 * q, mb1 = 2 * q + 1;
-    if constexpr (EPI == EPI_DGELU) {
+    if constexpr (epi_reads_p(EPI)) {
       load_h(mb0, h0);
       load_h(mb1, h1);
     }
@@ -382,7 +391,7 @@ IVIT_DEV void wide_epilogue_tr(const f32x4 (&acc)[RP_MB][NBW], int nw, int m0, i
       const uint4 out = odd ? make_uint4(s0[0], s1[0], y1.x, y1.y) : make_uint4(y0.x, y0.y, s0[1], s1[1]);
       const int c = cb + 16 * j - (odd ? 4 : 0);
       if (m < M) *(uint4*)(Y + (long)m * ldy + c) = out;
-      if constexpr (EPI == EPI_GELU) {
+      if constexpr (epi_writes_p(EPI)) {
         if (P) {
           const auto t0 = __builtin_amdgcn_permlane16_swap(p0.x, p1.x, false, false);
           const auto t1 = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
@@ -394,7 +403,7 @@ IVIT_DEV void wide_epilogue_tr(const f32x4 (&acc)[RP_MB][NBW], int nw, int m0, i
   }
   if constexpr (RP_MB % 2 == 1) {  // the last block alone: 8-B stores
     constexpr int mb = RP_MB - 1;
-    if constexpr (EPI == EPI_DGELU) load_h(mb, h0);
+    if constexpr (epi_reads_p(EPI)) load_h(mb, h0);
     const int m = m0 + 16 * mb + tl;
 #pragma unroll
     for (int j = 0; j < NBW; ++j) {
@@ -402,7 +411,7 @@ IVIT_DEV void wide_epilogue_tr(const f32x4 (&acc)[RP_MB][NBW], int nw, int m0, i
       compute(mb, j, h0[j], y, p);
       if (m < M) {
         *(uint2*)(Y + (long)m * ldy + cb + 16 * j) = y;
-        if constexpr (EPI == EPI_GELU) {
+        if constexpr (epi_writes_p(EPI)) {
           if (P) *(uint2*)(P + (long)m * ldp + cb + 16 * j) = p;
         }
       }
@@ -464,7 +473,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
     float bv[NBW];
 #pragma unroll
     for (int j = 0; j < NBW; ++j)
-      bv[j] = (EPI != EPI_DGELU && bias) ? bias[n0 + (wv * NBW + j) * 16 + (lane & 15)] : 0.f;
+      bv[j] = (!epi_reads_p(EPI) && bias) ? bias[n0 + (wv * NBW + j) * 16 + (lane & 15)] : 0.f;
     const float qs = (EPI == EPI_QS && n0 < qcols) ? qscale : 1.f;  // qcols is a multiple of 384 (of CW)
     uint2 pv[3];
     auto load_pre = [&](int mb) {
@@ -473,7 +482,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
 #pragma unroll
       for (int e = 0; e < 3; ++e) pv[e] = *(const uint2*)(prow + 4 * e);
     };
-    if constexpr (EPI == EPI_DGELU) load_pre(0);
+    if constexpr (epi_reads_p(EPI)) load_pre(0);
 #pragma unroll
     for (int mb = 0; mb < RP_MB; ++mb) {
 #pragma unroll
@@ -490,7 +499,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
         v[e] = tv.x; v[e + 1] = tv.y; v[e + 2] = tv.z; v[e + 3] = tv.w;
       }
       float h[12];
-      if constexpr (EPI == EPI_DGELU) {
+      if constexpr (epi_reads_p(EPI)) {
 #pragma unroll
         for (int e = 0; e < 3; ++e) {
           Pack4 q;
@@ -510,6 +519,13 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
           } else if constexpr (EPI == EPI_GELU) {
             p[e / 2] = pk_bf16(a, b);
             a = gelu_t<bf16>(a); b = gelu_t<bf16>(b);
+          } else if constexpr (EPI == EPI_GELUD) {
+            float da, db;
+            gelu_fast2(a, a, da);
+            gelu_fast2(b, b, db);
+            p[e / 2] = pk_bf16(da, db);
+          } else if constexpr (EPI == EPI_DMUL) {
+            a *= h[e]; b *= h[e + 1];
           } else {
             a *= gelu_grad_t<bf16>(h[e]); b *= gelu_grad_t<bf16>(h[e + 1]);
           }
@@ -518,7 +534,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
         bf16* yrow = Y + (long)m * ldy + n0 + c0;
 #pragma unroll
         for (int e = 0; e < 3; ++e) *(uint2*)(yrow + 4 * e) = make_uint2(y[2 * e], y[2 * e + 1]);
-        if constexpr (EPI == EPI_GELU) {
+        if constexpr (epi_writes_p(EPI)) {
           if (P) {
             bf16* prow = P + (long)m * ldp + n0 + c0;
 #pragma unroll
@@ -551,8 +567,14 @@ void launch_wide(dim3 g, hipStream_t st, bool ev1, u64* sb, const bf16* A, long 
     const char* e = getenv("IVIT_WIDE_EPI");
     return e && atoi(e) == 0;
   }();
-  ev1 = ev1 && !off && EPI == EPI_QS;  // GELU / DGELU: the LDS-tile form measured faster (VALU-bound epilogue;
-                                       // the transposed DGELU's 8-B pre-activation loads cost more)
+  static const int mode = [] {
+    const char* e = getenv("IVIT_WIDE_EPI");
+    return e ? atoi(e) : 1;
+  }();
+  // QS and GELUD: the transposed form (GELUD 89.5 -> 85.8 us); GELU / DGELU / DMUL: the LDS-tile form
+  // measured faster (the transposed forms' 8-B loads of P cost more: DMUL 76.2 vs 83.6 us);
+  // IVIT_WIDE_EPI=2: transposed for all
+  ev1 = ev1 && !off && (EPI == EPI_QS || EPI == EPI_GELUD || mode == 2);
   auto k = ev1 ? (sb ? rowpanel_wide_kernel<EPI, 4, true, 1> : rowpanel_wide_kernel<EPI, 4, false, 1>)
                : (sb ? rowpanel_wide_kernel<EPI, 4, true, 0> : rowpanel_wide_kernel<EPI, 4, false, 0>);
   hipLaunchKernelGGL(k, g, dim3(256), 0, st, A, lda, M, K, wp, N, bias, qcols, qscale, Y, ldy, P, ldp, sb);
@@ -617,7 +639,8 @@ extern "C" int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, lo
                                      void* Ypre, long ldpre, void* stream) {
   IVIT_CHECK_ARG(M > 0 && N > 0 && N % RP_N == 0 && K > 0 && K % 64 == 0 && qcols % RP_N == 0,
                  "ivit_linear_fwd_panel: N and qcols must be multiples of %d, K of 64", RP_N);
-  IVIT_CHECK_ARG(act == IVIT_ACT_NONE || (act == IVIT_ACT_GELU && qcols == 0), "ivit_linear_fwd_panel: bad act");
+  IVIT_CHECK_ARG(act == IVIT_ACT_NONE || ((act == IVIT_ACT_GELU || act == IVIT_ACT_GELU_D) && qcols == 0),
+                 "ivit_linear_fwd_panel: bad act");
   IVIT_CHECK_ARG(lda >= K && lda % 8 == 0 && ldy >= N && ldy % 4 == 0 && (!Ypre || (ldpre >= N && ldpre % 4 == 0)),
                  "ivit_linear_fwd_panel: bad leading dimensions");
   IVIT_CHECK_ARG(RP_MT * lda * 2 < (1L << 32) && M < (1L << 31), "ivit_linear_fwd_panel: too large");
@@ -627,7 +650,10 @@ extern "C" int ivit_linear_fwd_panel(const void* A, long lda, long M, long N, lo
   const dim3 g(ivit_cdiv(M, RP_MT) * (N / 192));
   hipStream_t st = ivit_stream(stream);
   u64* sb = ivit_stamp_buffer(g.x);
-  if (act == IVIT_ACT_GELU)
+  if (act == IVIT_ACT_GELU_D)
+    launch_wide<EPI_GELUD>(g, st, al16_rows(Y, ldy) && al16_rows(Ypre, ldpre), sb, (const bf16*)A, lda, (int)M,
+                           (int)K, (const u32x4*)wpack, (int)N, bias, 0, 1.f, (bf16*)Y, ldy, (bf16*)Ypre, ldpre);
+  else if (act == IVIT_ACT_GELU)
     launch_wide<EPI_GELU>(g, st, al16_rows(Y, ldy) && al16_rows(Ypre, ldpre), sb, (const bf16*)A, lda, (int)M,
                           (int)K, (const u32x4*)wpack, (int)N, bias, 0, 1.f, (bf16*)Y, ldy, (bf16*)Ypre, ldpre);
   else
@@ -651,6 +677,24 @@ extern "C" int ivit_linear_dgrad_gelu_panel(const void* dY, long lddy, long M, l
   u64* sb = ivit_stamp_buffer(g.x);
   launch_wide<EPI_DGELU>(g, ivit_stream(stream), al16_rows(dX, lddx), sb, (const bf16*)dY, lddy, (int)M, (int)K,
                          (const u32x4*)wpack_t, (int)N, nullptr, 0, 1.f, (bf16*)dX, lddx, (bf16*)pre, ldpre);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_linear_dgrad_mul_panel(const void* dY, long lddy, long M, long N, long K, const void* wpack_t,
+                                           const void* G, long ldg, void* dX, long lddx, void* stream) {
+  IVIT_CHECK_ARG(M > 0 && N > 0 && N % RP_N == 0 && K > 0 && K % 64 == 0,
+                 "ivit_linear_dgrad_mul_panel: N must be a multiple of %d, K of 64", RP_N);
+  IVIT_CHECK_ARG(lddy >= K && lddy % 8 == 0 && lddx >= N && lddx % 4 == 0 && ldg >= N && ldg % 4 == 0,
+                 "ivit_linear_dgrad_mul_panel: bad leading dimensions");
+  IVIT_CHECK_ARG(RP_MT * lddy * 2 < (1L << 32) && M < (1L << 31), "ivit_linear_dgrad_mul_panel: too large");
+  IVIT_CHECK_ARG(((uintptr_t)dY & 15) == 0 && ((uintptr_t)wpack_t & 15) == 0 && ((uintptr_t)dX & 7) == 0 &&
+                     ((uintptr_t)G & 7) == 0,
+                 "ivit_linear_dgrad_mul_panel: misaligned operand");
+  const dim3 g(ivit_cdiv(M, RP_MT) * (N / 192));
+  u64* sb = ivit_stamp_buffer(g.x);
+  launch_wide<EPI_DMUL>(g, ivit_stream(stream), al16_rows(dX, lddx), sb, (const bf16*)dY, lddy, (int)M, (int)K,
+                        (const u32x4*)wpack_t, (int)N, nullptr, 0, 1.f, (bf16*)dX, lddx, (bf16*)G, ldg);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

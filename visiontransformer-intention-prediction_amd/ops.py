@@ -19,7 +19,7 @@ import os
 import torch
 from torch.utils.weak import WeakIdKeyDictionary
 
-from _lib import ACT_GELU, ACT_NONE, BF16, F32, dt, lib, ptr, stream, tdtype, workspace
+from _lib import ACT_GELU, ACT_GELU_D, ACT_NONE, BF16, F32, dt, lib, ptr, stream, tdtype, workspace
 
 
 def _code(dtype):
@@ -348,7 +348,8 @@ def qkv_fwd_q2(x, w, b, D):
 
 def panel_fwd(x, w, b, act=ACT_NONE, want_pre=False, qcols=0, qscale=1.0):
     """Row-panel form of a wide bf16 token GEMM (ivit_linear_fwd_panel): x [M, K] bf16 @ w [N, K]
-    (f32 master, packed) + b; act GELU with the pre-activation copy, or columns < qcols scaled."""
+    (f32 master, packed) + b; act GELU with the pre-activation copy (act GELU_D: with GELU' of the
+    pre-activation instead, what the backward needs), or columns < qcols scaled."""
     M, K = x.shape
     N = w.shape[0]
     y = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
@@ -366,6 +367,18 @@ def panel_dgrad(dy, w):
     dx = torch.empty((M, N), dtype=torch.bfloat16, device=dy.device)
     lib.ivit_linear_fwd_panel(ptr(dy), dy.stride(0), M, N, K, ptr(packed_weight_t(w)), None, ACT_NONE, 0, 1.0,
                               ptr(dx), N, None, 0, stream())
+    return dx
+
+
+def panel_dgrad_mul(dy, w, g):
+    """dy [M, K] bf16 @ w [K, N] (f32 master, packed transposed) * g → bf16 [M, N], g = the GELU'
+    panel_fwd(act=ACT_GELU_D) wrote (ivit_linear_dgrad_mul_panel: fc2 dgrad into fc1's pre-activation
+    with no GELU' evaluation)."""
+    M, K = dy.shape
+    N = w.shape[1]
+    dx = torch.empty((M, N), dtype=torch.bfloat16, device=dy.device)
+    lib.ivit_linear_dgrad_mul_panel(ptr(dy), dy.stride(0), M, N, K, ptr(packed_weight_t(w)), ptr(g), g.stride(0),
+                                    ptr(dx), N, stream())
     return dx
 
 
@@ -688,7 +701,9 @@ class ViTBlockFn(torch.autograd.Function):
         # inference (torch.inference_mode): nothing is saved, and fc1 skips its pre-activation copy
         infer = torch.is_inference_mode_enabled()
         if panel:
-            a, h = panel_fwd(ln2, f1w, f1b, act=ACT_GELU, want_pre=not infer)
+            # training: h = GELU'(fc1 pre-activation) for the fc2 dgrad (panel_dgrad_mul), computed
+            # beside GELU from the f32 pre-activation instead of re-evaluated in the backward
+            a, h = panel_fwd(ln2, f1w, f1b, act=ACT_GELU if infer else ACT_GELU_D, want_pre=not infer)
         else:
             a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=not infer)
         if nxw is not None and panel:
@@ -731,7 +746,7 @@ class ViTBlockFn(torch.autograd.Function):
             hm.g = hm.key = None
         if dx2s is None:
             dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
-        dh = panel_dgrad_gelu(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
+        dh = panel_dgrad_mul(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
         # bf16 row-panel blocks: the four weight gradients in one grouped launch after the dgrads
         group = ctx.panel and GROUP_WGRAD and fork is None
         g2 = None if group else _wgrad(fork, dx2s, a, cdt)
