@@ -332,9 +332,10 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ops.KernelTimer.enabled = set(ATTN)
+    timing = os.environ.get("IVIT_BENCH_KTIME", "1") != "0"  # 0: no attention timing in the loop (A/B of its cost)
+    ops.KernelTimer.enabled = set(ATTN) if timing else set()
     ops.KernelTimer.records = {}
-    ops.ktime_arm(True)
+    ops.ktime_arm(timing)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

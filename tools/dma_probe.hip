@@ -25,6 +25,40 @@ __global__ __launch_bounds__(1024, 1) void dma_probe_kernel(const char* __restri
   if (threadIdx.x == 0 && iters < 0) sink[0] = smem[0];
 }
 
+// The same stream into VGPRs (global_load_dwordx4, 16 B per lane, DEPTH loads in flight per wave):
+// the path the row-panel kernels' weight fragments take. The loaded words are folded into one
+// value so the loads stay live.
+template <int DEPTH>
+__global__ __launch_bounds__(1024, 1) void vgpr_probe_kernel(const char* __restrict__ src, long span, int iters,
+                                                            int* sink) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  long off = ((long)blockIdx.x * nw + wv) * 65536;
+  unsigned acc = 0;
+  for (int it = 0; it < iters; ++it) {
+    uint4 r[DEPTH];
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) r[d] = *(const uint4*)(src + (off + (long)d * 1024) % span + lane * 16);
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) acc ^= r[d].x ^ r[d].w;
+    off += (long)DEPTH * 1024 * 257;
+  }
+  if (acc == 0x12345678u && iters < 0) sink[0] = (int)acc;
+}
+
+extern "C" int vgpr_probe(const void* src, long span, int wgs, int waves, int depth, int iters, int* sink,
+                          void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g(wgs), b(64 * waves);
+  switch (depth) {
+    case 2: hipLaunchKernelGGL(vgpr_probe_kernel<2>, g, b, 0, st, (const char*)src, span, iters, sink); break;
+    case 4: hipLaunchKernelGGL(vgpr_probe_kernel<4>, g, b, 0, st, (const char*)src, span, iters, sink); break;
+    case 8: hipLaunchKernelGGL(vgpr_probe_kernel<8>, g, b, 0, st, (const char*)src, span, iters, sink); break;
+    case 16: hipLaunchKernelGGL(vgpr_probe_kernel<16>, g, b, 0, st, (const char*)src, span, iters, sink); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int dma_probe(const void* src, long span, int wgs, int waves, int depth, int iters, int* sink, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   dim3 g(wgs), b(64 * waves);

@@ -228,8 +228,18 @@ __global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
   float s = 0.f;
   if (c < C) {
-#pragma unroll 4
-    for (int b = ph; b < nb; b += 16) s += part[(long)b * pstride + c];
+    // the first 16 rows of this phase loaded at once (16 loads in flight per lane: the reduce is
+    // latency-bound on a dozen workgroups), summed in the same order as the sequential loop
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int b = ph + 16 * i;
+      v[i] = b < nb ? part[(long)b * pstride + c] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (ph + 16 * i < nb) s += v[i];
+    for (int b = ph + 256; b < nb; b += 16) s += part[(long)b * pstride + c];
   }
   __shared__ float red[16][64];
   red[ph][threadIdx.x & 63] = s;
