@@ -160,6 +160,13 @@ long ivit_conv_wgrad_workspace(long B, long H, long W, long Cin, long Cout, long
 int ivit_conv_wgrad(int dtype, const void* dY, long lddy, const void* X, long B, long H, long W, long Cin,
                     long Cout, long ks, float* dWp, float* dbias, int accumulate, void* work, long work_bytes,
                     void* stream);
+/* Data gradient on the transposed, tap-flipped pack of ivit_pack_conv_weight_t (bf16; the 288 x 256
+ * panel kernel: Cout % 64 == 0, Cin % 8 == 0, B*H*W >= 288); same sums as ivit_conv_dgrad. */
+int ivit_conv_dgrad_t(int dtype, const void* dY, long lddy, long B, long H, long W, long Cout, const void* WpT,
+                      long Cin, long ks, void* dX, int dx_dtype, void* stream);
+/* torch [Cout][Cin][k][k] f32  ->  [Cin][k][k][Cout] (dtype) with the taps flipped: the K-contiguous
+ * weight of the data gradient, WpT[ci][ky][kx][co] = w[co][ci][k-1-ky][k-1-kx]. */
+int ivit_pack_conv_weight_t(int dtype, const float* w, long Cout, long Cin, long ks, void* out, void* stream);
 /* torch [Cout][Cin][k][k] f32  ->  packed [Cout_pad][k][k][Cin] (dtype), rows >= Cout zeroed. */
 int ivit_pack_conv_weight(int dtype, const float* w, long Cout, long Cin, long ks, long Cout_pad, void* out,
                           void* stream);

@@ -324,6 +324,61 @@ def test_conv_nhwc(k, Cin, cd):
     assert _rel(db, dyh.float().cpu().double().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,ybf", [(2, 13, 29, 128, 256, 3, False),   # ragged last pixel panel
+                                                   (1, 17, 23, 64, 384, 1, True),     # ragged channel tile
+                                                   (1, 19, 21, 64, 136, 5, False),    # partial 16-channel block
+                                                   (1, 24, 12, 192, 512, 3, True)])
+def test_conv_panel(B, H, W, Cin, Cout, k, ybf):
+    """288 x 256 panel kernel (conv_panel.hip): forward through ivit_conv_fwd and the data gradient
+    on the tap-flipped transposed pack (ivit_conv_dgrad_t) vs f64 of the same bf16 operands (the
+    fusion block convs, model_vit.py:12-43)."""
+    import ops
+    from _lib import BF16
+    torch.manual_seed(7)
+    x = torch.randn(B, Cin, H, W)
+    w = torch.randn(Cout, Cin, k, k) / math.sqrt(Cin * k * k)
+    bias = torch.randn(Cout) * 0.1
+    xh = ops.cast(x.permute(0, 2, 3, 1).reshape(-1, Cin).contiguous().to(DEV), torch.bfloat16)
+    wd = w.to(DEV)
+    wp = ops.pack_conv(wd, BF16)
+    od = torch.bfloat16 if ybf else torch.float32
+    y = ops.conv_fwd(xh, B, H, W, wp, bias.to(DEV), BF16, od)
+    xr = xh.float().cpu().reshape(B, H, W, Cin).permute(0, 3, 1, 2).double().requires_grad_(True)
+    wr = wp.float().cpu().reshape(Cout, k, k, Cin).permute(0, 3, 1, 2).double().requires_grad_(True)
+    ref = F.conv2d(xr, wr, bias.double(), padding=k // 2)
+    tol = 1e-2 if ybf else 1e-5
+    assert _rel(y.float().reshape(B, H, W, Cout).permute(0, 3, 1, 2), ref.detach()) < tol
+    dy = torch.randn(B, Cout, H, W)
+    dyh = ops.cast(dy.permute(0, 2, 3, 1).reshape(-1, Cout).contiguous().to(DEV), torch.bfloat16)
+    ref.backward(dyh.float().cpu().reshape(B, H, W, Cout).permute(0, 3, 1, 2).double())
+    # reference gradient against the bf16-rounded weight the transposed pack holds
+    wt = ops.pack_conv_t(wd, BF16)
+    assert torch.equal(wt.float().cpu(), w.bfloat16().float().permute(1, 2, 3, 0).flip(1, 2))
+    dx = ops.conv_dgrad(dyh, B, H, W, wp, BF16, torch.float32, w=wd)
+    if Cout % 64 == 0:
+        assert _rel(dx.reshape(B, H, W, Cin).permute(0, 3, 1, 2), xr.grad) < 1e-5
+    dx0 = ops.conv_dgrad(dyh, B, H, W, wp, BF16, torch.float32)  # 128 x 128 engine
+    assert _rel(dx, dx0) < 1e-5
+
+
+def test_conv_panel_fusion_shape_vs_engine(monkeypatch):
+    """Full fusion-block shape (B = 8, 50 x 90, 512 -> 512, k = 3): panel kernel vs the 128 x 128
+    engine (IVIT_CONV_PANEL=0), forward and data gradient — same bf16 products, f32 sums."""
+    import ops
+    from _lib import BF16
+    torch.manual_seed(3)
+    B, H, W, C = 8, 50, 90, 512
+    xh = (torch.randn(B * H * W, C, device=DEV) * 0.5).bfloat16()
+    w = torch.randn(C, C, 3, 3, device=DEV) / math.sqrt(C * 9)
+    wp = ops.pack_conv(w, BF16)
+    y1 = ops.conv_fwd(xh, B, H, W, wp, None, BF16, torch.float32)
+    d1 = ops.conv_dgrad(xh, B, H, W, wp, BF16, torch.float32, w=w)
+    monkeypatch.setenv("IVIT_CONV_PANEL", "0")
+    y0 = ops.conv_fwd(xh, B, H, W, wp, None, BF16, torch.float32)
+    d0 = ops.conv_dgrad(xh, B, H, W, wp, BF16, torch.float32, w=w)
+    assert _rel(y1, y0) < 1e-5 and _rel(d1, d0) < 1e-5
+
+
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("D", [64, 384])
 def test_patch_embed(cd, D):

@@ -1,0 +1,52 @@
+"""Fusion-block convolution timings (B = 8, 50 x 90 map): forward and data gradient through the
+288 x 256 panel kernel (conv_panel.hip) and the 128 x 128 engine (IVIT_CONV_PANEL=0), alternating
+in one process; HIP events around 20 back-to-back launches.
+
+    python tools/conv_bench.py
+"""
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "visiontransformer-intention-prediction_amd"))
+
+
+def timed(fn, reps=20):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3  # us
+
+
+def main():
+    import ops
+    from _lib import BF16
+    dev = torch.device("cuda", 0)
+    B, H, W = 8, 50, 90
+    M = B * H * W
+    for (cin, cout, k) in ((384, 512, 3), (512, 512, 3), (384, 512, 1)):
+        x = (torch.randn(M, cin, device=dev) * 0.5).bfloat16()
+        dy = (torch.randn(M, cout, device=dev) * 0.5).bfloat16()
+        w = torch.randn(cout, cin, k, k, device=dev) / (cin * k * k) ** 0.5
+        wp = ops.pack_conv(w, BF16)
+        fl = 2.0 * M * cout * cin * k * k
+        for rep in range(2):
+            for mode in ("1", "0"):
+                os.environ["IVIT_CONV_PANEL"] = mode
+                tf = timed(lambda: ops.conv_fwd(x, B, H, W, wp, None, BF16, torch.float32))
+                td = timed(lambda: ops.conv_dgrad(dy, B, H, W, wp, BF16, torch.float32, w=w))
+                name = "panel " if mode == "1" else "engine"
+                print(f"{cin}->{cout} k{k} {name}: fwd {tf:7.1f} us ({fl / tf / 1e6:6.1f} TF/s)  "
+                      f"dgrad(+pack) {td:7.1f} us ({fl / td / 1e6:6.1f} TF/s)", flush=True)
+    os.environ["IVIT_CONV_PANEL"] = "1"
+
+
+if __name__ == "__main__":
+    main()

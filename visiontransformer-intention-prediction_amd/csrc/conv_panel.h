@@ -1,0 +1,18 @@
+// Panel implicit-GEMM convolution (conv_panel.hip): the fusion-block 3x3 / 1x1 convolutions' forward
+// and data gradient (model_vit.py:12-43 BasicBlock, reached from model_vit.py:141).
+#pragma once
+#include "ivit_common.h"
+
+namespace ivit {
+
+// C[m][n] = bias[n] + sum_{tap, c} A[pixel m shifted by tap][c] * Bk[n][tap * Cin + c]
+//   A: NHWC bf16 map, pixel stride lda elements, Cin channels (Cin % 64 == 0), k x k "same" taps;
+//   Bk: bf16 [N][ks * ks * Cin] (K-contiguous packed weights); C: f32 or bf16, row stride ldy.
+// Returns false (nothing launched) when the shape is not one the kernel takes.
+bool conv_panel_ok(long M, long N, long Cin, long lda, long ks);
+int conv_panel_launch(const bf16* A, long lda, int Bn, int H, int W, int Cin, int ks, const bf16* Bk, int N,
+                      const float* bias, void* Y, long ldy, bool y_bf16, hipStream_t st);
+// IVIT_CONV_PANEL=0 turns the panel kernel off (A/B against the 128x128 engine); default on.
+bool conv_panel_enabled();
+
+}  // namespace ivit

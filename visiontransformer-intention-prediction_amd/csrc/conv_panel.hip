@@ -1,0 +1,250 @@
+// Panel implicit-GEMM convolution for the fusion block (BasicBlock conv3x3 / conv1x1, model_vit.py:12-43,
+// reached from model_vit.py:141): forward Y = conv(X, W) and the data gradient dX = conv(dY, flip(W)^T).
+//
+// The 128 x 128 engine tile (gemm_engine.h) streams one LDS fragment read per MFMA and, at two
+// workgroups per CU, keeps the LDS array as busy as the matrix pipe; and 36 000 output pixels of a
+// B = 8 fusion map cut into 282 x 4 such tiles fill the 512 workgroup slots 2.2 times (the third
+// round a fifth full). Here a workgroup of 8 waves owns 288 pixels x 256 output channels:
+//   * 36 000 = 125 x 288, so a 512-channel convolution is 250 tiles, one round over the 256 CUs;
+//   * each wave computes 144 pixels x 64 channels with v_mfma_f32_16x16x32_bf16 (9 x 4 blocks),
+//     13 fragment reads per 36 MFMAs (a third of the engine's LDS read traffic per flop);
+//   * both operands stream by LDS-DMA into a double-buffered [rows][64 k] image (68 KiB per
+//     stage): the map through per-lane tap addresses (a padding tap reads a zero page), the packed
+//     weights [N][k*k*Cin] by the saddr form;
+//   * the weights are the MFMA's A operand, so each lane's accumulators are 4 consecutive output
+//     channels of one pixel and the epilogue stores 16 B (f32) / 8 B (bf16) per lane directly.
+// Same sums as the engine (f32 accumulation of bf16 products), K in the same tap-major order.
+#include "conv_panel.h"
+
+#include <stdlib.h>
+
+#include "panel_common.h"
+
+namespace ivit {
+namespace {
+
+constexpr int CP_BM = 288, CP_BN = 256, CP_W = 8;
+constexpr int CP_WM = 144, CP_WN = 64;                      // wave tile: 2 (M) x 4 (N) waves
+constexpr int CP_MB = CP_WM / 16, CP_NB = CP_WN / 16;       // 9 x 4 MFMA blocks per wave
+constexpr int CP_SA = CP_BM * 128, CP_SB = CP_BN * 128;     // [rows][64 k] bf16 images
+constexpr int CP_STAGE = CP_SA + CP_SB;                     // 68 KiB
+constexpr int CP_PA = CP_BM / 8, CP_PB = CP_BN / 8;         // 1-KiB DMA pieces (8 rows) per image
+constexpr int CP_PAW = (CP_PA + CP_W - 1) / CP_W;           // 5: waves 0-3 take 5 A pieces, 4-7 four
+constexpr int CP_PAX = CP_PA - (CP_PAW - 1) * CP_W;         // waves with CP_PAW pieces
+constexpr int CP_PBW = CP_PB / CP_W;                        // 4 B pieces per wave
+static_assert(CP_PB % CP_W == 0 && CP_PAX > 0, "piece split");
+
+__device__ __attribute__((aligned(16))) uint4 cp_zero16[4];
+
+// 128-B image rows (64 k), 16-B chunk c of row r at chunk c ^ ((r >> 1) & 7): the 16x16x32 operand
+// reads (rows r0 .. r0+15, chunks 4t .. 4t+3) hit 16 distinct bank quads per ds_read_b128 lane group.
+IVIT_DEV int cp_off(int r, int c) { return r * 128 + ((c ^ ((r >> 1) & 7)) << 4); }
+
+struct CpArgs {
+  const bf16* A;
+  long lda;
+  int H, W, Cin, ks, M;
+  const bf16* Bk;
+  int N, K;
+  const float* bias;
+  void* Y;
+  long ldy;
+  int tilesN;
+};
+
+template <typename O>
+__global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * CP_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 2, wn = wv & 3;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // the N tiles of one pixel panel share an XCD
+  const int tm = lin / p.tilesN, tn = lin - tm * p.tilesN;
+  const int m0 = tm * CP_BM, n0 = tn * CP_BN;
+  const int pad = p.ks >> 1;
+  const int npa = wv < CP_PAX ? CP_PAW : CP_PAW - 1;
+
+  // per-lane DMA state (k-invariant): the map pixel (flat offset + y, x) of each A piece row, the
+  // weight row offset of each B piece row; rows past M / N are clamped (computed, never stored)
+  int abase[CP_PAW], ayx[CP_PAW];
+#pragma unroll
+  for (int i = 0; i < CP_PAW; ++i) {
+    const int piece = min(wv + CP_W * i, CP_PA - 1);
+    const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+    const int m = min(m0 + row, p.M - 1);
+    const int x = m % p.W, y = (m / p.W) % p.H;
+    abase[i] = m * (int)p.lda + c * 8;
+    ayx[i] = (y << 16) | x;
+  }
+  unsigned boff[CP_PBW];
+#pragma unroll
+  for (int i = 0; i < CP_PBW; ++i) {
+    const int row = (wv + CP_W * i) * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+    const int n = min(n0 + row, p.N - 1);
+    boff[i] = 2u * (unsigned)(n * p.K + c * 8);
+  }
+  auto issue = [&](int kt, int s) {
+    char* sa = smem + s * CP_STAGE;
+    char* sb = sa + CP_SA;
+    const int k0 = kt * 64;
+    const int tap = k0 / p.Cin, ci0 = k0 - tap * p.Cin;  // Cin % 64 == 0: a K tile is one tap
+    const int ky = tap / p.ks, kx = tap - ky * p.ks;
+    const int dy = ky - pad, dx = kx - pad;
+    const long shift = (long)(dy * p.W + dx) * p.lda + ci0;
+#pragma unroll
+    for (int i = 0; i < CP_PAW; ++i) {
+      if (i < npa) {
+        const int yy = (ayx[i] >> 16) + dy, xx = (ayx[i] & 0xffff) + dx;
+        const bool ok = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+        const void* src = ok ? (const void*)(p.A + (shift + abase[i])) : (const void*)cp_zero16;
+        glds_v<false>(src, sa + (wv + CP_W * i) * 1024);
+      }
+    }
+    const char* bsb = uniform_ptr(p.Bk + k0);
+#pragma unroll
+    for (int i = 0; i < CP_PBW; ++i) glds_s<false>(boff[i], bsb, sb + (wv + CP_W * i) * 1024);
+  };
+
+  f32x4 acc[CP_MB][CP_NB];
+#pragma unroll
+  for (int i = 0; i < CP_MB; ++i)
+#pragma unroll
+    for (int j = 0; j < CP_NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / 64;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      issue(kt + 1, cur ^ 1);
+      wait_vm(npa + CP_PBW);  // this wave's pieces of tile kt landed; tile kt+1 stays in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    const char* ia = smem + cur * CP_STAGE;
+    const char* ib = ia + CP_SA;
+    bf16x8 bfr[2][CP_NB];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int j = 0; j < CP_NB; ++j)
+        bfr[t][j] = *(const bf16x8*)(ib + cp_off(wn * CP_WN + 16 * j + (lane & 15), 4 * t + (lane >> 4)));
+    // A fragment f = (t = f / 9: 32-k half, mb = f % 9), read three ahead of its MFMAs
+    auto rdf = [&](int f) {
+      const int t = f / CP_MB, mb = f % CP_MB;
+      return *(const bf16x8*)(ia + cp_off(wm * CP_WM + 16 * mb + (lane & 15), 4 * t + (lane >> 4)));
+    };
+    bf16x8 fr[4];
+    fr[0] = rdf(0);
+    fr[1] = rdf(1);
+    fr[2] = rdf(2);
+#pragma unroll
+    for (int f = 0; f < 2 * CP_MB; ++f) {
+      const int t = f / CP_MB, mb = f % CP_MB;
+      if (f + 3 < 2 * CP_MB) fr[(f + 3) % 4] = rdf(f + 3);
+#pragma unroll
+      for (int j = 0; j < CP_NB; ++j)
+        acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[t][j], fr[f % 4], acc[mb][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of this stage are done
+    __builtin_amdgcn_s_barrier();                         // ... everyone's, before it is refilled
+  }
+
+  // epilogue: acc[mb][j] lane l = channels n .. n+3 (n = n0 + 64 wn + 16 j + 4 (l >> 4)) of pixel
+  // m0 + 144 wm + 16 mb + (l & 15)
+  O* Y = (O*)p.Y;
+  // every bias value before the first store (a load under the store branches makes the compiler
+  // wait vmcnt(0), i.e. for all earlier stores too, before each one)
+  float4 bv[CP_NB];
+#pragma unroll
+  for (int j = 0; j < CP_NB; ++j) {
+    const int n = min(n0 + wn * CP_WN + 16 * j + 4 * (lane >> 4), p.N - 4);
+    bv[j] = p.bias ? *(const float4*)(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int j = 0; j < CP_NB; ++j)
+#pragma unroll
+    for (int mb = 0; mb < CP_MB; ++mb) {
+      acc[mb][j] += f32x4{bv[j].x, bv[j].y, bv[j].z, bv[j].w};
+      asm volatile("" : "+v"(acc[mb][j]));  // the adds stay out of the store branches
+    }
+#pragma unroll
+  for (int j = 0; j < CP_NB; ++j) {
+    const int n = n0 + wn * CP_WN + 16 * j + 4 * (lane >> 4);
+#pragma unroll
+    for (int mb = 0; mb < CP_MB; ++mb) {
+      const int m = m0 + wm * CP_WM + 16 * mb + (lane & 15);
+      const f32x4 a = acc[mb][j];
+      O* y = Y + (long)m * p.ldy + n;
+      if (m < p.M && n < p.N) {
+        if constexpr (sizeof(O) == 4) *(float4*)y = make_float4(a[0], a[1], a[2], a[3]);
+        else *(uint2*)y = make_uint2(pk_bf16(a[0], a[1]), pk_bf16(a[2], a[3]));
+      }
+    }
+  }
+}
+
+// dgrad weights: Bt[ci][(ky', kx'), co] = w[co][ci][ks-1-ky'][ks-1-kx']  (torch f32 layout in)
+template <typename O>
+__global__ void pack_conv_t_kernel(const float* __restrict__ w, long Cout, long Cin, long ks, O* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = Cin * ks * ks * Cout;
+  if (i >= n) return;
+  const long co = i % Cout, t = i / Cout, tap = t % (ks * ks), ci = t / (ks * ks);
+  const long ky = ks - 1 - tap / ks, kx = ks - 1 - tap % ks;
+  out[i] = from_f32<O>(w[((co * Cin + ci) * ks + ky) * ks + kx]);
+}
+
+}  // namespace
+
+bool conv_panel_enabled() {
+  const char* v = getenv("IVIT_CONV_PANEL");
+  return v ? atoi(v) != 0 : true;
+}
+
+bool conv_panel_ok(long M, long N, long Cin, long lda, long ks) {
+  return M >= CP_BM && N >= 128 && N % 8 == 0 && Cin % 64 == 0 && lda % 8 == 0 && (ks == 1 || ks == 3 || ks == 5) &&
+         M * lda + 64 < 0x7fffffffL && N * ks * ks * Cin < 0x3fffffffL;
+}
+
+int conv_panel_launch(const bf16* A, long lda, int Bn, int H, int W, int Cin, int ks, const bf16* Bk, int N,
+                      const float* bias, void* Y, long ldy, bool y_bf16, hipStream_t st) {
+  const int M = Bn * H * W;
+  CpArgs p{A, lda, H, W, Cin, ks, M, Bk, N, ks * ks * Cin, bias, Y, ldy, ivit_cdiv(N, CP_BN)};
+  const dim3 grid(ivit_cdiv(M, CP_BM) * p.tilesN);
+  if (y_bf16)
+    hipLaunchKernelGGL(conv_panel_kernel<bf16>, grid, dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL(conv_panel_kernel<float>, grid, dim3(512), 0, st, p);
+  return 0;
+}
+
+}  // namespace ivit
+
+using namespace ivit;
+
+extern "C" int ivit_pack_conv_weight_t(int dtype, const float* w, long Cout, long Cin, long ks, void* out,
+                                       void* stream) {
+  hipStream_t st = ivit_stream(stream);
+  const long n = Cin * ks * ks * Cout;
+  if (dtype == IVIT_BF16)
+    hipLaunchKernelGGL(pack_conv_t_kernel<bf16>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, w, Cout, Cin, ks,
+                       (bf16*)out);
+  else
+    hipLaunchKernelGGL(pack_conv_t_kernel<float>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, w, Cout, Cin, ks,
+                       (float*)out);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int ivit_conv_dgrad_t(int dtype, const void* dY, long lddy, long B, long H, long W, long Cout,
+                                 const void* WpT, long Cin, long ks, void* dX, int dx_dtype, void* stream) {
+  IVIT_CHECK_ARG(dtype == IVIT_BF16, "ivit_conv_dgrad_t: bf16 only");
+  IVIT_CHECK_ARG(conv_panel_ok(B * H * W, Cin, Cout, lddy, ks), "ivit_conv_dgrad_t: shape not supported");
+  hipStream_t st = ivit_stream(stream);
+  conv_panel_launch((const bf16*)dY, lddy, (int)B, (int)H, (int)W, (int)Cout, (int)ks, (const bf16*)WpT, (int)Cin,
+                    nullptr, dX, Cin, dx_dtype == IVIT_BF16, st);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}

@@ -3,6 +3,7 @@
 #include <stdio.h>
 
 #include "gemm_engine.h"
+#include "conv_panel.h"
 #include "patch_embed.h"
 
 using namespace ivit;
@@ -485,6 +486,11 @@ static int conv_fwd_t(const void* X, long B, long H, long W, long Cin, const voi
                       long ks, void* Y, long ldy, hipStream_t st) {
   const bool bf = sizeof(S) == 2;
   const int M = (int)(B * H * W), Kc = (int)(ks * ks * Cin);
+  if constexpr (sizeof(S) == 2) {  // 288 x 256 panel tiles (conv_panel.hip) where the shape allows
+    if (conv_panel_enabled() && conv_panel_ok(M, Cout, Cin, Cin, ks) && ldy % 4 == 0)
+      return conv_panel_launch((const bf16*)X, Cin, (int)B, (int)H, (int)W, (int)Cin, (int)ks, (const bf16*)Wp,
+                               (int)Cout, bias, Y, ldy, sizeof(O) == 2, st);
+  }
   LdConv<S> la{(const S*)X, (int)H, (int)W, (int)Cin, (int)ks, M, Kc, Cin};
   LdDense<S> lb{(const S*)Wp, Kc, (int)Cout, Kc, 0, 0, 0, {}};
   EpiStore<O> e{(O*)Y, ldy, {}, bias, IVIT_ACT_NONE, nullptr, 1.f};

@@ -57,16 +57,17 @@ class _ConvSameFn(torch.autograd.Function):
         xh = ops.cast(x.reshape(-1, C).contiguous(), tdtype(cdt))
         wp = ops.pack_conv(w, cdt)
         y = ops.conv_fwd(xh, B, H, W, wp, b, cdt, torch.float32)
-        ctx.save_for_backward(xh, wp)
+        ctx.save_for_backward(xh, wp, w)
         ctx.meta = (B, H, W, C, Cout, k, cdt, b is not None)
         return y.view(B, H, W, Cout)
 
     @staticmethod
     def backward(ctx, dy):
-        xh, wp = ctx.saved_tensors
+        xh, wp, w = ctx.saved_tensors
         B, H, W, C, Cout, k, cdt, has_b = ctx.meta
         d2 = ops.cast(dy.reshape(-1, Cout).contiguous(), tdtype(cdt))
-        dx = ops.conv_dgrad(d2, B, H, W, wp, cdt, torch.float32).view(B, H, W, C) if ctx.needs_input_grad[0] else None
+        dx = (ops.conv_dgrad(d2, B, H, W, wp, cdt, torch.float32, w=w).view(B, H, W, C)
+              if ctx.needs_input_grad[0] else None)
         gp, db = ops.conv_wgrad(d2, xh, B, H, W, C, Cout, k, cdt, want_bias=has_b)
         return dx, ops.unpack_conv_grad(gp, Cout, C, k), db, None
 

@@ -452,9 +452,30 @@ def conv_fwd(x, B, H, W, wp, bias, cdt, out_dtype):
     return y
 
 
-def conv_dgrad(dy, B, H, W, wp, cdt, out_dtype):
+def conv_panel_enabled():
+    return os.environ.get("IVIT_CONV_PANEL", "1") != "0"
+
+
+def pack_conv_t(w, cdt):
+    """torch [Cout][Cin][k][k] -> the data gradient's K-contiguous weight [Cin][k][k][Cout], taps flipped."""
+    Cout, Cin, k, _ = w.shape
+    out = torch.empty((Cin, k, k, Cout), dtype=tdtype(cdt), device=w.device)
+    lib.ivit_pack_conv_weight_t(cdt, ptr(w), Cout, Cin, k, ptr(out), stream())
+    return out
+
+
+def conv_dgrad(dy, B, H, W, wp, cdt, out_dtype, w=None):
+    """dX of a stride-1 'same' conv. With the f32 weight `w` (torch layout) and a bf16 shape the
+    288 x 256 panel kernel takes (ivit_conv_dgrad_t: Cout % 64, Cin >= 128, >= 288 pixels), the
+    tap-flipped transposed pack is built and the panel kernel runs; otherwise the 128 x 128 engine
+    on the forward pack `wp`."""
     Cout, k, _, Cin = wp.shape
     dx = torch.empty((B * H * W, Cin), dtype=out_dtype, device=dy.device)
+    if (w is not None and cdt == BF16 and conv_panel_enabled() and Cout % 64 == 0 and Cin >= 128 and Cin % 8 == 0
+            and B * H * W >= 288 and dy.stride(0) % 8 == 0 and wp.shape[0] == w.shape[0]):
+        wt = pack_conv_t(w, cdt)
+        lib.ivit_conv_dgrad_t(cdt, ptr(dy), dy.stride(0), B, H, W, Cout, ptr(wt), Cin, k, ptr(dx), dt(dx), stream())
+        return dx
     lib.ivit_conv_dgrad(cdt, ptr(dy), dy.stride(0), B, H, W, Cout, ptr(wp), Cin, k, ptr(dx), dt(dx), stream())
     return dx
 
@@ -896,18 +917,19 @@ class NeckFn(torch.autograd.Function):
             Cm_ = c2.shape[1]
             gp2, _ = conv_wgrad(dc2, r1, B, Hf, Wf, r1.shape[1], Cm_, 3, cdt)
             G[p + "conv2.weight"] = unpack_conv_grad(gp2, Cm_, r1.shape[1], 3)
-            dr1 = conv_dgrad(dc2, B, Hf, Wf, packs[p + "2"], cdt, torch.float32)
+            dr1 = conv_dgrad(dc2, B, Hf, Wf, packs[p + "2"], cdt, torch.float32, w=P[p + "conv2.weight"])
             dc1, _, G[p + "bn1.weight"], G[p + "bn1.bias"] = bn_backward(c1, r1, dr1, s1, P[p + "bn1.weight"], True, cd)
             gp1, _ = conv_wgrad(dc1, x, B, Hf, Wf, x.shape[1], Cm_, 3, cdt)
             G[p + "conv1.weight"] = unpack_conv_grad(gp1, Cm_, x.shape[1], 3)
-            dxa = conv_dgrad(dc1, B, Hf, Wf, packs[p + "1"], cdt, torch.float32)
+            dxa = conv_dgrad(dc1, B, Hf, Wf, packs[p + "1"], cdt, torch.float32, w=P[p + "conv1.weight"])
             if has_ds:
                 dd, sd, idn = bns[p + "ds"]
                 ddd, _, G[p + "downsample.1.weight"], G[p + "downsample.1.bias"] = bn_backward(
                     dd, idn, dres, sd, P[p + "downsample.1.weight"], False, cd)
                 gpd, _ = conv_wgrad(ddd, x, B, Hf, Wf, x.shape[1], Cm_, 1, cdt)
                 G[p + "downsample.0.weight"] = unpack_conv_grad(gpd, Cm_, x.shape[1], 1)
-                dxb = conv_dgrad(ddd, B, Hf, Wf, packs[p + "ds"], cdt, torch.float32)
+                dxb = conv_dgrad(ddd, B, Hf, Wf, packs[p + "ds"], cdt, torch.float32,
+                                 w=P[p + "downsample.0.weight"])
             else:
                 dxb = dres
             if li == 0:

@@ -40,17 +40,14 @@ class FusedAdamW(torch.optim.Optimizer):
         for group in self.param_groups:
             b1, b2 = group["betas"]
             by_step = {}
-            for p in group["params"]:
-                if p.grad is None:
-                    continue
+            live = [p for p in group["params"] if p.grad is not None]
+            for p in live:
                 if p.dtype != torch.float32 or p.grad.dtype != torch.float32 or not p.is_contiguous() \
                         or not p.grad.is_contiguous():
                     raise TypeError("FusedAdamW: contiguous f32 params/grads required")
+            self._init_state([p for p in live if not self.state[p]])
+            for p in live:
                 st = self.state[p]
-                if not st:
-                    st["step"] = 0
-                    st["exp_avg"] = torch.zeros_like(p)
-                    st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] += 1
                 by_step.setdefault(st["step"], []).append(p)
             for step, ps_all in by_step.items():
@@ -85,6 +82,21 @@ class FusedAdamW(torch.optim.Optimizer):
                 if jobs:
                     lib.ivit_weight_pack_multi(len(jobs), ptr(self._pack_jobs(jobs, dev)), big, stream())
         return loss
+
+    def _init_state(self, fresh):
+        """Zero moments of the parameters seen for the first time: views into one flat buffer per
+        device and moment (a single fill each, not two per parameter)."""
+        by_dev = {}
+        for p in fresh:
+            by_dev.setdefault(p.device, []).append(p)
+        for dev, ps in by_dev.items():
+            n = sum(p.numel() for p in ps)
+            flat = torch.zeros((2, n), dtype=torch.float32, device=dev)
+            o = 0
+            for p in ps:
+                k = p.numel()
+                self.state[p].update(step=0, exp_avg=flat[0, o:o + k].view_as(p), exp_avg_sq=flat[1, o:o + k].view_as(p))
+                o += k
 
     def _table_ptrs(self, ptrs, device):
         key = ("ptrs",) + tuple(ptrs)
