@@ -359,6 +359,10 @@ def test_conv_panel(B, H, W, Cin, Cout, k, ybf):
         assert _rel(dx.reshape(B, H, W, Cin).permute(0, 3, 1, 2), xr.grad) < 1e-5
     dx0 = ops.conv_dgrad(dyh, B, H, W, wp, BF16, torch.float32)  # 128 x 128 engine
     assert _rel(dx, dx0) < 1e-5
+    # weight gradient: 256 x 256 panel tiles with the pixel reduction split (ivit_conv_wgrad)
+    gp, db = ops.conv_wgrad(dyh, xh, B, H, W, Cin, Cout, k, BF16, want_bias=True)
+    assert _rel(ops.unpack_conv_grad(gp, Cout, Cin, k), wr.grad) < 1e-5
+    assert _rel(db, dyh.float().cpu().double().sum(0)) < 1e-5
 
 
 def test_conv_panel_fusion_shape_vs_engine(monkeypatch):
@@ -373,10 +377,13 @@ def test_conv_panel_fusion_shape_vs_engine(monkeypatch):
     wp = ops.pack_conv(w, BF16)
     y1 = ops.conv_fwd(xh, B, H, W, wp, None, BF16, torch.float32)
     d1 = ops.conv_dgrad(xh, B, H, W, wp, BF16, torch.float32, w=w)
+    dy = (torch.randn(B * H * W, C, device=DEV) * 0.5).bfloat16()
+    g1, _ = ops.conv_wgrad(dy, xh, B, H, W, C, C, 3, BF16)
     monkeypatch.setenv("IVIT_CONV_PANEL", "0")
     y0 = ops.conv_fwd(xh, B, H, W, wp, None, BF16, torch.float32)
     d0 = ops.conv_dgrad(xh, B, H, W, wp, BF16, torch.float32, w=w)
-    assert _rel(y1, y0) < 1e-5 and _rel(d1, d0) < 1e-5
+    g0, _ = ops.conv_wgrad(dy, xh, B, H, W, C, C, 3, BF16)
+    assert _rel(y1, y0) < 1e-5 and _rel(d1, d0) < 1e-5 and _rel(g1, g0) < 1e-5
 
 
 @pytest.mark.parametrize("cd", [torch.float32, torch.bfloat16])

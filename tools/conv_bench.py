@@ -42,9 +42,11 @@ def main():
                 os.environ["IVIT_CONV_PANEL"] = mode
                 tf = timed(lambda: ops.conv_fwd(x, B, H, W, wp, None, BF16, torch.float32))
                 td = timed(lambda: ops.conv_dgrad(dy, B, H, W, wp, BF16, torch.float32, w=w))
+                tw = timed(lambda: ops.conv_wgrad(dy, x, B, H, W, cin, cout, k, BF16))
                 name = "panel " if mode == "1" else "engine"
                 print(f"{cin}->{cout} k{k} {name}: fwd {tf:7.1f} us ({fl / tf / 1e6:6.1f} TF/s)  "
-                      f"dgrad(+pack) {td:7.1f} us ({fl / td / 1e6:6.1f} TF/s)", flush=True)
+                      f"dgrad(+pack) {td:7.1f} us ({fl / td / 1e6:6.1f} TF/s)  "
+                      f"wgrad(+reduce) {tw:7.1f} us ({fl / tw / 1e6:6.1f} TF/s)", flush=True)
     os.environ["IVIT_CONV_PANEL"] = "1"
 
 

@@ -8,6 +8,6 @@ rc=$?; echo "tests rc=$rc"; tail -15 gpurun_out/tests_$TAG.log
 timeout -k 10 200 python -u tools/conv_bench.py > gpurun_out/convbench_$TAG.txt 2>&1
 rc=$?; echo "conv bench rc=$rc"; cat gpurun_out/convbench_$TAG.txt
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/fill_trace.py > gpurun_out/fill_$TAG.txt 2>&1
-rc=$?; echo "fill trace rc=$rc"; tail -40 gpurun_out/fill_$TAG.txt
+true
+rc=0
 exit $rc

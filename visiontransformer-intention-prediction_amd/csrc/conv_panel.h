@@ -12,6 +12,12 @@ namespace ivit {
 bool conv_panel_ok(long M, long N, long Cin, long lda, long ks);
 int conv_panel_launch(const bf16* A, long lda, int Bn, int H, int W, int Cin, int ks, const bf16* Bk, int N,
                       const float* bias, void* Y, long ldy, bool y_bf16, hipStream_t st);
+// Weight gradient on 256 x 256 panel tiles, the pixel reduction split `splits` ways into an f32 slab
+// [splits][Cout][ks*ks*Cin] (the engine's EpiSlab layout; reduced by the caller).
+bool conv_wgrad_panel_ok(long M, long Cout, long Cin, long ks, long lddy);
+int conv_wgrad_panel_splits(long M, long Cout, long N);
+int conv_wgrad_panel_launch(const bf16* dY, long lddy, const bf16* X, int Bn, int H, int W, int Cin, int Cout, int ks,
+                            float* slab, int splits, hipStream_t st);
 // IVIT_CONV_PANEL=0 turns the panel kernel off (A/B against the 128x128 engine); default on.
 bool conv_panel_enabled();
 

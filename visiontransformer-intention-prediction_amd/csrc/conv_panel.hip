@@ -18,6 +18,7 @@
 
 #include <stdlib.h>
 
+#include "gemm_engine.h"
 #include "panel_common.h"
 
 namespace ivit {
@@ -185,6 +186,150 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
   }
 }
 
+// ----------------------------------------------------------------------------- weight gradient
+// dW[co][tap * Cin + ci] = sum_p dY[p][co] X[p shifted by tap][ci]  (f32 partial slab per split)
+//
+// Output tiles of 256 co x 256 (tap, ci), the pixel reduction split S ways so that tiles x S
+// fills the 256 CUs once (512 -> 512 3x3: 36 tiles x 7). Both operands are pixel-major, so the
+// K-step images are [64 pixels][256 columns] (two 128-column halves in the engine's MN layout,
+// gemm_engine.h mn_off) read by transposing LDS reads (frag_mn) as 32x32x16 operands; 8 waves of
+// 128 co x 64 columns (4 x 2 blocks). The map operand's columns are (tap, ci) chunks: each lane
+// owns one chunk (its tap's shift) and four pixel rows, whose (y, x) advance by 64 pixels a step
+// without divisions; padding taps and pixels past the split read the zero page.
+constexpr int CW_BK = 64, CW_IMG = CW_BK * 256, CW_STAGE = 4 * CW_IMG;  // A halves | B halves: 64 KiB
+
+struct CwArgs {
+  const bf16* dy;
+  long lddy;
+  const bf16* x;
+  long ldx;
+  int H, W, Cin, ks, M, Cout, N;
+  int tilesM, tilesN, kchunk;
+  int qW, rW;  // 64 = qW * W + rW
+  float* slab;
+};
+
+__global__ __launch_bounds__(512, 1) void conv_wgrad_panel_kernel(CwArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * CW_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 2, wn = wv & 3;
+  const int tiles = p.tilesM * p.tilesN;
+  const int flat = xcd_remap(blockIdx.x, gridDim.x);  // a split's tiles on one XCD: its pixel panels shared in L2
+  const int split = flat / tiles, tile = flat - split * tiles;
+  const int tm = tile / p.tilesN, tn = tile - tm * p.tilesN;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int kbeg = split * p.kchunk, kend = min(p.M, kbeg + p.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + CW_BK - 1) / CW_BK : 0;
+  const int pad = p.ks >> 1;
+
+  // this wave's 4 pieces of each image: half h = wv >> 2, rows r_i = 16 (wv & 3) + 4 i + (lane >> 4),
+  // source chunk c (the same for the four rows: (r_i & 3) = (lane >> 4) & 3)
+  const int h = wv >> 2;
+  const int c = (lane & 15) ^ (((lane >> 4) & 3) << 2);
+  const int co = min(m0 + h * 128 + c * 8, p.Cout - 8);
+  const int n = min(n0 + h * 128 + c * 8, p.N - 8);
+  const int tap = n / p.Cin, ci = n - tap * p.Cin;
+  const int ky = tap / p.ks;
+  const int dy = ky - pad, dx = tap - ky * p.ks - pad;
+  const long xshift = (long)(dy * p.W + dx) * p.ldx + ci;
+  unsigned voffa[4];
+  int py[4], px[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 16 * (wv & 3) + 4 * i + (lane >> 4);
+    voffa[i] = 2u * (unsigned)(r * (int)p.lddy + co);
+    const int pp = min(kbeg + r, p.M - 1);
+    px[i] = pp % p.W;
+    py[i] = (pp / p.W) % p.H;
+  }
+  auto issue = [&](int kt, int s) {
+    char* sa = smem + s * CW_STAGE + h * CW_IMG + (wv & 3) * 4096;
+    char* sb = sa + 2 * CW_IMG;
+    const int k0 = kbeg + kt * CW_BK;
+    if (k0 + CW_BK <= kend) {
+      const char* ab = uniform_ptr(p.dy + (long)k0 * p.lddy);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds_s<false>(voffa[i], ab, sa + i * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pix = k0 + 16 * (wv & 3) + 4 * i + (lane >> 4);
+        const void* src = pix < kend ? (const void*)(p.dy + (long)pix * p.lddy + co) : (const void*)cp_zero16;
+        glds_v<false>(src, sa + i * 1024);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pix = k0 + 16 * (wv & 3) + 4 * i + (lane >> 4);
+      const bool ok = pix < kend && (unsigned)(py[i] + dy) < (unsigned)p.H && (unsigned)(px[i] + dx) < (unsigned)p.W;
+      const void* src = ok ? (const void*)(p.x + ((long)pix * p.ldx + xshift)) : (const void*)cp_zero16;
+      glds_v<false>(src, sb + i * 1024);
+      // advance the row's pixel by one K step (64 = qW * W + rW)
+      int xx = px[i] + p.rW, yy = py[i] + p.qW;
+      if (xx >= p.W) { xx -= p.W; ++yy; }
+      while (yy >= p.H) yy -= p.H;
+      px[i] = xx;
+      py[i] = yy;
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      issue(kt + 1, cur ^ 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt landed, kt+1's 8 pieces in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const char* ia = smem + cur * CW_STAGE + wm * CW_IMG;             // this wave's 128 co
+    const char* ib = smem + cur * CW_STAGE + (2 + (wn >> 1)) * CW_IMG; // its 64 columns' half
+    const int cb = (wn & 1) * 64;
+    bf16x8 fa[2][4], fb[2][2];
+    auto ldf = [&](int t, bf16x8 (&xa)[4], bf16x8 (&xb)[2]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xa[i] = frag_mn(ia, 16 * t, 32 * i, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) xb[j] = frag_mn(ib, 16 * t, cb + 32 * j, lane);
+    };
+    ldf(0, fa[0], fb[0]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t < 3) ldf(t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[t & 1][i], fb[t & 1][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  // partial tile -> slab[split][co][n]: col = lane & 31 (n), row = (r & 3) + 8 (r >> 2) + 4 hl (co)
+  float* slab = p.slab + (long)split * p.Cout * p.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn * 64 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 128 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (row < p.Cout && col < p.N) slab[(long)row * p.N + col] = acc[i][j][r];
+      }
+    }
+}
+
 // dgrad weights: Bt[ci][(ky', kx'), co] = w[co][ci][ks-1-ky'][ks-1-kx']  (torch f32 layout in)
 template <typename O>
 __global__ void pack_conv_t_kernel(const float* __restrict__ w, long Cout, long Cin, long ks, O* out) {
@@ -206,6 +351,29 @@ bool conv_panel_enabled() {
 bool conv_panel_ok(long M, long N, long Cin, long lda, long ks) {
   return M >= CP_BM && N >= 128 && N % 8 == 0 && Cin % 64 == 0 && lda % 8 == 0 && (ks == 1 || ks == 3 || ks == 5) &&
          M * lda + 64 < 0x7fffffffL && N * ks * ks * Cin < 0x3fffffffL;
+}
+
+int conv_wgrad_panel_splits(long M, long Cout, long N) {
+  const long tiles = (long)ivit_cdiv(Cout, 256) * ivit_cdiv(N, 256);
+  long s = 256 / tiles;
+  const long steps = (M + CW_BK - 1) / CW_BK;
+  if (s > steps / 4) s = steps / 4;  // at least ~4 K steps per workgroup
+  return s < 1 ? 1 : (int)s;
+}
+
+bool conv_wgrad_panel_ok(long M, long Cout, long Cin, long ks, long lddy) {
+  return M >= 256 && Cout >= 128 && Cout % 8 == 0 && Cin % 8 == 0 && lddy % 8 == 0 && (ks == 1 || ks == 3 || ks == 5) &&
+         ks * ks * Cin >= 128 && M * lddy < 0x7fffffffL && M * Cin < 0x7fffffffL;
+}
+
+int conv_wgrad_panel_launch(const bf16* dY, long lddy, const bf16* X, int Bn, int H, int W, int Cin, int Cout, int ks,
+                            float* slab, int splits, hipStream_t st) {
+  const int M = Bn * H * W, N = ks * ks * Cin;
+  const long steps = (M + CW_BK - 1) / CW_BK;
+  CwArgs p{dY, lddy, X, Cin, H, W, Cin, ks, M, Cout, N, ivit_cdiv(Cout, 256), ivit_cdiv(N, 256),
+           (int)((steps + splits - 1) / splits) * CW_BK, 64 / W, 64 % W, slab};
+  hipLaunchKernelGGL(conv_wgrad_panel_kernel, dim3(p.tilesM * p.tilesN * splits), dim3(512), 0, st, p);
+  return 0;
 }
 
 int conv_panel_launch(const bf16* A, long lda, int Bn, int H, int W, int Cin, int ks, const bf16* Bk, int N,

@@ -543,6 +543,8 @@ extern "C" long ivit_conv_wgrad_workspace(long B, long H, long W, long Cin, long
   long s = wgrad_splits(Cout, Kc, M, false);
   const long s2 = wgrad_splits(Cout, Kc, M, true);
   if (s2 > s) s = s2;
+  const long s3 = conv_wgrad_panel_splits(M, Cout, Kc);
+  if (s3 > s) s = s3;
   const long cw = ivit_colsum_workspace(M, Cout);
   return s * Cout * Kc * 4 + (s * Cout * 4 > cw ? s * Cout * 4 : cw);
 }
@@ -566,12 +568,15 @@ extern "C" int ivit_conv_wgrad(int dtype, const void* dY, long lddy, const void*
   hipStream_t st = ivit_stream(stream);
   const bool bf = dtype == IVIT_BF16;
   const long M = B * H * W, Kc = ks * ks * Cin;
-  const int splits = (int)wgrad_splits(Cout, Kc, M, bf);
+  const bool panel = bf && conv_panel_enabled() && conv_wgrad_panel_ok(M, Cout, Cin, ks, lddy);
+  const int splits = panel ? conv_wgrad_panel_splits(M, Cout, Kc) : (int)wgrad_splits(Cout, Kc, M, bf);
   float* slab = (float*)work;
   const long n = Cout * Kc;
-  float* bslab = (bf && dbias) ? slab + (long)splits * n : nullptr;
-  int rc = bf ? conv_wgrad_t<bf16>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, bslab, splits, st)
-              : conv_wgrad_t<float>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, nullptr, splits, st);
+  float* bslab = (bf && dbias && !panel) ? slab + (long)splits * n : nullptr;
+  int rc = panel ? conv_wgrad_panel_launch((const bf16*)dY, lddy, (const bf16*)X, (int)B, (int)H, (int)W, (int)Cin,
+                                           (int)Cout, (int)ks, slab, splits, st)
+           : bf  ? conv_wgrad_t<bf16>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, bslab, splits, st)
+                 : conv_wgrad_t<float>(dY, lddy, X, B, H, W, Cin, Cout, ks, slab, nullptr, splits, st);
   if (rc) return rc;
   rc = reduce_wgrad(st, slab, n, dWp, bslab, Cout, dbias, splits, accumulate);
   if (rc) return rc;
