@@ -476,10 +476,13 @@ def test_patch_wgrad_raster_exact(B, C, H, W):
     err = (got - ref).abs().max().item()
     assert err < 1e-5 * max(1.0, (B * Np) ** 0.5), err
     assert _rel(db, dt[:, 1:].sum((0, 1))) < 1e-5 and _rel(dpos, dt.sum(0)) < 1e-5
+    assert _rel(dcls, dt[:, 0].sum(0)) < 1e-5
     # accumulate = 1 adds onto the previous result
     assert lib.ivit_patch_embed_wgrad(BF16, ptr(dtd), ptr(imgd), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos),
                                       ptr(dcls), 1, ptr(ws), nws, stream()) == 0
     assert (dw.double().cpu().reshape(D, C * 64) - 2 * ref).abs().max().item() < 2 * err + 1e-5
+    assert _rel(db, 2 * dt[:, 1:].sum((0, 1))) < 1e-5 and _rel(dpos, 2 * dt.sum(0)) < 1e-5
+    assert _rel(dcls, 2 * dt[:, 0].sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("M,K,scale", [(36008, 384, True), (300, 1536, False), (1, 64, True), (145, 128, True)])

@@ -348,6 +348,107 @@ __global__ void pos_grad_kernel(const S* __restrict__ dtok, long B, long Ntok, l
   if (i < D && dcls) dcls[i] = accumulate ? dcls[i] + s : s;
 }
 
+// dpos[t][d] (+)= sum_b dtok[b][t][d] (dcls = row 0) and dbias[d] (+)= sum over t >= 1 of those sums,
+// in ONE pass over dtok: 8 columns per thread (16-B loads), 4 row phases, RB rows per block; the
+// block's partial bias row goes to `part` (reduced by colreduce_kernel). Replaces pos_grad_kernel's
+// 2-B loads plus a separate column-sum pass over the same token gradient.
+template <typename S>
+__global__ __launch_bounds__(1024) void pos_bias_grad_kernel(const S* __restrict__ dtok, int B, int Ntok, int D,
+                                                            int RB, float* dpos, float* dcls, float* part,
+                                                            int accumulate) {
+  __shared__ float red[4 * 1024];
+  const int nc = D / 8, cc = threadIdx.x % nc, ph = threadIdx.x / nc;
+  const int t0 = blockIdx.x * RB, t1 = min(Ntok, t0 + RB);
+  float ps[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ps[j] = 0.f;
+  for (int t = t0 + ph; t < t1; t += 4) {
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const S* q = dtok + ((long)b * Ntok + t) * D + 8 * cc;
+      float v[8];
+      load8f(q, v, 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += v[j];
+    }
+    float* o = dpos + (long)t * D + 8 * cc;
+    float x[8];
+    if (accumulate) {
+      load8f(o, x, 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] += s[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = s[j];
+    }
+    store8(o, x, 8);
+    if (t == 0) {
+      if (dcls) {
+        float* oc = dcls + 8 * cc;
+        float y[8];
+        if (accumulate) {
+          load8f(oc, y, 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[j] += s[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y[j] = s[j];
+        }
+        store8(oc, y, 8);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ps[j] += s[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[ph * D + 8 * cc + j] = ps[j];
+  __syncthreads();
+  if (ph == 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * cc + j;
+      part[(long)blockIdx.x * D + c] = ((red[c] + red[D + c]) + red[2 * D + c]) + red[3 * D + c];
+    }
+  }
+}
+
+// pos / cls / bias gradients of the patch embedding from the token gradient (see pos_bias_grad_kernel);
+// falls back to pos_grad_kernel + ivit_colsum for widths it does not take.
+static int patch_pos_bias_grad(int dtype, const void* dtok, long B, long Np, long D, float* dbias, float* dpos,
+                               float* dcls, int accumulate, void* cw, long cw_bytes, void* stream) {
+  hipStream_t st = ivit_stream(stream);
+  const long Ntok = Np + 1;
+  const long nb0 = ivit_cdiv(B * Np, CS_ROWS);  // the column-sum workspace's partial rows
+  int RB = (int)((Ntok + nb0 - 1) / nb0);
+  RB = ((RB < 32 ? 32 : RB) + 3) / 4 * 4;
+  const int nb = ivit_cdiv(Ntok, RB);
+  const bool al = ((uintptr_t)dtok & 15) == 0 && ((uintptr_t)dpos & 15) == 0 && (!dcls || ((uintptr_t)dcls & 15) == 0);
+  if (D % 8 == 0 && D <= 1024 && al && (long)nb * D * 4 <= cw_bytes && dbias) {
+    if (dtype == IVIT_BF16)
+      hipLaunchKernelGGL(pos_bias_grad_kernel<bf16>, dim3(nb), dim3(4 * D / 8), 0, st, (const bf16*)dtok, (int)B,
+                         (int)Ntok, (int)D, RB, dpos, dcls, (float*)cw, accumulate);
+    else
+      hipLaunchKernelGGL(pos_bias_grad_kernel<float>, dim3(nb), dim3(4 * D / 8), 0, st, (const float*)dtok, (int)B,
+                         (int)Ntok, (int)D, RB, dpos, dcls, (float*)cw, accumulate);
+    IVIT_LAUNCH_CHECK();
+    launch_colreduce(st, (const float*)cw, nb, D, (int)D, dbias, (int)D, nullptr, accumulate);
+    IVIT_LAUNCH_CHECK();
+    return 0;
+  }
+  if (dtype == IVIT_BF16)
+    hipLaunchKernelGGL(pos_grad_kernel<bf16>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const bf16*)dtok, B,
+                       Ntok, D, dpos, dcls, accumulate);
+  else
+    hipLaunchKernelGGL(pos_grad_kernel<float>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const float*)dtok,
+                       B, Ntok, D, dpos, dcls, accumulate);
+  IVIT_LAUNCH_CHECK();
+  return ivit_colsum(dtok, dtype, D, Np, Ntok, 1, B * Np, D, dbias, accumulate, cw, ivit_colsum_workspace(B * Np, D),
+                     stream);
+}
+
 extern "C" long ivit_patch_embed_wgrad_workspace(long B, long C, long H, long W, long D) {
   const long Np = (H / 8) * (W / 8);
   long s = wgrad_splits(D, C * 64, B * Np, false);
@@ -377,7 +478,7 @@ extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* 
   IVIT_CHECK_ARG(work_bytes >= ivit_patch_embed_wgrad_workspace(B, C, H, W, D), "patch wgrad: workspace too small");
   hipStream_t st = ivit_stream(stream);
   const bool bf = dtype == IVIT_BF16;
-  const long Np = (H / 8) * (W / 8), Ntok = Np + 1;
+  const long Np = (H / 8) * (W / 8);
   const long n = D * C * 64;
   const int splits = (int)wgrad_splits(D, C * 64, B * Np, bf);
   long cw_off = (long)splits * n * 4;  // colsum workspace after the slab
@@ -394,16 +495,9 @@ extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* 
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dW,
                        accumulate);
   }
-  if (bf)
-    hipLaunchKernelGGL(pos_grad_kernel<bf16>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const bf16*)dtok, B,
-                       Ntok, D, dpos, dcls, accumulate);
-  else
-    hipLaunchKernelGGL(pos_grad_kernel<float>, dim3(ivit_cdiv(Ntok * D, 256)), dim3(256), 0, st, (const float*)dtok,
-                       B, Ntok, D, dpos, dcls, accumulate);
-  IVIT_LAUNCH_CHECK();
   char* cw = (char*)work + cw_off;
-  return ivit_colsum(dtok, dtype, D, Np, Ntok, 1, B * Np, D, dbias, accumulate, cw, ivit_colsum_workspace(B * Np, D),
-                     stream);
+  return patch_pos_bias_grad(dtype, dtok, B, Np, D, dbias, dpos, dcls, accumulate, cw, ivit_colsum_workspace(B * Np, D),
+                             stream);
 }
 
 // bf16 patch matrix. One workgroup per (b, c, gy) = 8 consecutive raster rows (8*W floats,

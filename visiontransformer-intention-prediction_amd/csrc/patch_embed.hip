@@ -593,15 +593,16 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
   }
 }
 
-// dW[n][g*128 + k] (+)= sum of the partial tiles of pair g (workgroups whose unit range meets it)
+// dW[n][g*128 + k] (+)= sum of the partial tiles of pair g (workgroups whose unit range meets it).
+// D * 128 is a multiple of the block size, so a block's pair g, and the range of workgroups whose
+// unit range meets it, are block-uniform (scalar; one 64-bit division per block, not per element).
 __global__ __launch_bounds__(256) void patch_wgrad_reduce_kernel(const float* __restrict__ slab, int C, int J, int D,
                                                                  float* __restrict__ dW, int accumulate) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
   const int G = (C + 1) / 2;
-  if (i >= (long)G * D * 128) return;
-  const int g = (int)(i / ((long)D * 128));
-  const int e = (int)(i - (long)g * D * 128), n = e >> 7, k = e & 127;
-  if (2 * g + (k >> 6) >= C) return;
+  const long per = (long)D * 128, i0 = (long)blockIdx.x * 256;
+  const int g = (int)(i0 / per);
+  if (g >= G) return;
+  const int e = (int)(i0 - (long)g * per) + threadIdx.x, n = e >> 7, k = e & 127;
   const long U = (long)G * J, ga = (long)g * J, gb = ga + J;
   int w = (int)(ga * WG_NWG / U);
   while (w > 0 && wg_unit_start(w, U) > ga) --w;
@@ -612,6 +613,7 @@ __global__ __launch_bounds__(256) void patch_wgrad_reduce_kernel(const float* __
     const int slot = g - (int)(a / J);
     s += slab[(((long)w * 2 + slot) * D + n) * 128 + k];
   }
+  if (2 * g + (k >> 6) >= C) return;
   float* o = dW + (long)n * C * 64 + (long)g * 128 + k;
   *o = accumulate ? *o + s : s;
 }
@@ -668,6 +670,7 @@ int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long 
   // (LiDAR), 48.74-48.84 vs 48.64-48.69 ms per step.
   const char* sv = getenv("IVIT_PATCH_WGRAD_SPLIT");
   if (!(sv && atoi(sv))) {
+    if ((D * 128) % 256) return IVIT_ERR_UNSUPPORTED;  // the reduce's block-uniform pair
     hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, 0>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H,
                        (int)W, Wp, Np, M, J, slab);
     hipLaunchKernelGGL(patch_wgrad_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, (int)C, J, (int)D,
