@@ -115,13 +115,11 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
   issue(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      issue(kt + 1, cur ^ 1);
-      wait_vm(npa + CP_PBW);  // this wave's pieces of tile kt landed; tile kt+1 stays in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    // one barrier per K tile: it publishes tile kt (every wave's pieces landed) and tells that every
+    // wave is done reading stage cur ^ 1 (tile kt-1), which tile kt+1 then refills
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
     const char* ia = smem + cur * CP_STAGE;
     const char* ib = ia + CP_SA;
     bf16x8 bfr[2][CP_NB];
@@ -149,7 +147,6 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of this stage are done
-    __builtin_amdgcn_s_barrier();                         // ... everyone's, before it is refilled
   }
 
   // epilogue: acc[mb][j] lane l = channels n .. n+3 (n = n0 + 64 wn + 16 j + 4 (l >> 4)) of pixel
@@ -284,13 +281,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_panel_kernel(CwArgs p) {
   if (nk > 0) issue(0, 0);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      issue(kt + 1, cur ^ 1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt landed, kt+1's 8 pieces in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // one barrier per K tile (as conv_panel_kernel)
     __builtin_amdgcn_s_barrier();
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
     const char* ia = smem + cur * CW_STAGE + wm * CW_IMG;             // this wave's 128 co
     const char* ib = smem + cur * CW_STAGE + (2 + (wn >> 1)) * CW_IMG; // its 64 columns' half
     const int cb = (wn & 1) * 64;
@@ -313,7 +306,6 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_panel_kernel(CwArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
   }
   // partial tile -> slab[split][co][n]: col = lane & 31 (n), row = (r & 3) + 8 (r >> 2) + 4 hl (co)
   float* slab = p.slab + (long)split * p.Cout * p.N;

@@ -696,9 +696,8 @@ class ViTBlockFn(torch.autograd.Function):
         cd = tdtype(cdt)
         q2 = cdt == BF16
         panel = q2 and x.shape[1] == 384
-        if panel:  # row-panel kernels read the packed weights; only the last fc2 runs the engine GEMM
-            wq = wp = w1 = None
-            w2 = cast_weight(f2w, cd) if nxw is None else None
+        if panel:  # row-panel kernels read the packed weights
+            wq = wp = w1 = w2 = None
         else:
             wq, wp, w1, w2 = cast_weight(qkvw, cd), cast_weight(pw, cd), cast_weight(f1w, cd), cast_weight(f2w, cd)
         if ln_in is None:
@@ -729,6 +728,12 @@ class ViTBlockFn(torch.autograd.Function):
             a, h = linear_fwd(ln2, w1, f1b, cdt, act=ACT_GELU, want_pre=not infer)
         if nxw is not None and panel:
             x2, lnx, mx, rx = linear_resid_ln_fwd(a, f2w, f2b, x1, s2, N, nxw, nxb, eps)
+        elif panel:
+            # the last block: the same row-panel residual GEMM (its LayerNorm epilogue on unit
+            # parameters, outputs discarded) instead of the 128 x 128 engine's EpiResid GEMM
+            g1, b0 = _unit_ln_params(x.shape[1], x.device)
+            x2 = linear_resid_ln_fwd(a, f2w, f2b, x1, s2, N, g1, b0, eps)[0]
+            lnx = mx = rx = x2.new_empty(0)
         else:
             x2, _ = linear_fwd(a, w2, f2b, cdt, resid=x1, row_scale=s2, rps=N)
             lnx = mx = rx = x2.new_empty(0)
@@ -801,6 +806,17 @@ class ViTBlockFn(torch.autograd.Function):
         (dW2, db2), (dW1, db1), (dWp, dbp), (dWq, dbq) = g2, g1, gp, gq
         return (dx0, None, None, None, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, None, None,
                 None, None, None, None, None)
+
+
+_UNIT_LN = {}
+
+
+def _unit_ln_params(n, dev):
+    """(ones, zeros) LayerNorm parameters of width n on dev, cached."""
+    key = (n, str(dev))
+    if key not in _UNIT_LN:
+        _UNIT_LN[key] = (torch.ones(n, device=dev), torch.zeros(n, device=dev))
+    return _UNIT_LN[key]
 
 
 class NeckFn(torch.autograd.Function):
