@@ -164,6 +164,16 @@ int ivit_conv_wgrad(int dtype, const void* dY, long lddy, const void* X, long B,
  * panel kernel: Cout % 64 == 0, Cin % 8 == 0, B*H*W >= 288); same sums as ivit_conv_dgrad. */
 int ivit_conv_dgrad_t(int dtype, const void* dY, long lddy, long B, long H, long W, long Cout, const void* WpT,
                       long Cin, long ks, void* dX, int dx_dtype, void* stream);
+/* Convolution + the following BatchNorm2d's training-mode batch statistics in one pass (BasicBlock
+ * conv -> bn, model_vit.py:24-27,35-43): Y = conv(X, Wp) (no bias, dense: ldy == Cout) and mean /
+ * invstd (biased variance, eps) of Y's channels, running mean / var updated with momentum (unbiased
+ * variance) as ivit_bn_stats. bf16 panel shapes fold the statistics into the convolution's epilogue
+ * (per-tile sums and centred squares, merged across tiles in a fixed order); other shapes run
+ * ivit_conv_fwd + ivit_bn_stats. */
+long ivit_conv_bn_fwd_workspace(long B, long H, long W, long Cout);
+int ivit_conv_bn_fwd(int dtype, const void* X, long B, long H, long W, long Cin, const void* Wp, long Cout, long ks,
+                     void* Y, long ldy, int y_dtype, float* mean, float* invstd, float* run_mean, float* run_var,
+                     float momentum, float eps, void* work, long work_bytes, void* stream);
 /* torch [Cout][Cin][k][k] f32  ->  [Cin][k][k][Cout] (dtype) with the taps flipped: the K-contiguous
  * weight of the data gradient, WpT[ci][ky][kx][co] = w[co][ci][k-1-ky][k-1-kx]. */
 int ivit_pack_conv_weight_t(int dtype, const float* w, long Cout, long Cin, long ks, void* out, void* stream);

@@ -365,6 +365,30 @@ def test_conv_panel(B, H, W, Cin, Cout, k, ybf):
     assert _rel(db, dyh.float().cpu().double().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k", [(8, 50, 90, 384, 512, 3), (1, 19, 23, 64, 256, 1), (1, 7, 9, 48, 40, 3)])
+def test_conv_bn_stats_fused(B, H, W, Cin, Cout, k):
+    """ivit_conv_bn_fwd: the BatchNorm batch statistics out of the panel convolution's epilogue (per-
+    tile sums and centred squares merged by Chan's update) vs the two-pass ivit_bn_stats on the same
+    output, and the running-stat update; the last shape takes the fallback (engine + two passes)."""
+    import ops
+    from _lib import BF16
+    torch.manual_seed(11)
+    x = (torch.randn(B * H * W, Cin, device=DEV) + 0.5).bfloat16()
+    w = torch.randn(Cout, Cin, k, k, device=DEV) / math.sqrt(Cin * k * k)
+    wp = ops.pack_conv(w, BF16)
+    rm1, rv1 = torch.randn(Cout, device=DEV), torch.rand(Cout, device=DEV) + 0.5
+    rm0, rv0 = rm1.clone(), rv1.clone()
+    y1, s1 = ops.conv_bn_fwd(x, B, H, W, wp, BF16, torch.float32, rm1, rv1, True)
+    y0 = ops.conv_fwd(x, B, H, W, wp, None, BF16, torch.float32)
+    s0 = ops.bn_forward(y0, None, None, rm0, rv0, True)
+    assert torch.equal(y1, y0)
+    assert _rel(s1.mean, s0.mean) < 1e-5 and _rel(s1.invstd, s0.invstd) < 1e-5
+    assert _rel(rm1, rm0) < 1e-5 and _rel(rv1, rv0) < 1e-5
+    ref = y0.double().cpu()
+    assert _rel(s1.mean, ref.mean(0)) < 1e-5
+    assert _rel(s1.invstd, 1.0 / torch.sqrt(ref.var(0, unbiased=False) + 1e-5)) < 1e-5
+
+
 def test_conv_panel_fusion_shape_vs_engine(monkeypatch):
     """Full fusion-block shape (B = 8, 50 x 90, 512 -> 512, k = 3): panel kernel vs the 128 x 128
     engine (IVIT_CONV_PANEL=0), forward and data gradient — same bf16 products, f32 sums."""

@@ -51,9 +51,10 @@ struct CpArgs {
   void* Y;
   long ldy;
   int tilesN;
+  float* stats;  // STATS: [tilesM][2][N] per-tile channel sum and centred sum of squares
 };
 
-template <typename O>
+template <typename O, bool STATS>
 __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * CP_STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -86,8 +87,12 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
   auto issue = [&](int kt, int s) {
     char* sa = smem + s * CP_STAGE;
     char* sb = sa + CP_SA;
-    const int k0 = kt * 64;
-    const int tap = k0 / p.Cin, ci0 = k0 - tap * p.Cin;  // Cin % 64 == 0: a K tile is one tap
+    // K order: channel tile major, the k*k taps inside it (Cin % 64 == 0: a K tile is one tap), so
+    // the k*k shifted reads of a 64-channel slab of the pixel panel follow each other and all but
+    // the first hit the XCD's L2 (tap-major order streamed the whole panel once per tap: 9x the
+    // Infinity-Cache traffic for a 3x3 conv)
+    const int nt = p.ks * p.ks, ct = kt / nt, tap = kt - ct * nt, ci0 = ct * 64;
+    const int k0 = tap * p.Cin + ci0;  // the weight's K offset ([N][k][k][Cin] packing)
     const int ky = tap / p.ks, kx = tap - ky * p.ks;
     const int dy = ky - pad, dx = kx - pad;
     const long shift = (long)(dy * p.W + dx) * p.lda + ci0;
@@ -167,6 +172,53 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
       acc[mb][j] += f32x4{bv[j].x, bv[j].y, bv[j].z, bv[j].w};
       asm volatile("" : "+v"(acc[mb][j]));  // the adds stay out of the store branches
     }
+  if constexpr (STATS) {
+    // BatchNorm statistics of this tile's stored values (the next BatchNorm2d's training-mode batch
+    // statistics, model_vit.py:24-27): per channel the sum and the sum of squares about the TILE
+    // mean (two passes over the registers), merged across tiles by bn_merge_kernel (Chan et al.).
+    // Channel c = 64 wn + 16 j + 4 (lane >> 4) + e of the tile sits in the 16 lanes of one lane
+    // group and the 9 blocks mb of both row waves wm.
+    float* red = (float*)smem;  // [2 passes][2 wm][256]
+    __builtin_amdgcn_s_barrier();  // every wave is past its last fragment read of the stages
+    const int nv = min(CP_BM, p.M - m0);
+    float sm[CP_NB][4];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < CP_NB; ++j) {
+        float mu[4];
+        if (pass) {
+          const int c = wn * CP_WN + 16 * j + 4 * (lane >> 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) mu[e] = (red[c + e] + red[256 + c + e]) / (float)nv;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = 0.f;
+#pragma unroll
+          for (int mb = 0; mb < CP_MB; ++mb) {
+            const int m = m0 + wm * CP_WM + 16 * mb + (lane & 15);
+            const float v = acc[mb][j][e];
+            const float d = pass ? v - mu[e] : v;
+            t += m < p.M ? (pass ? d * d : d) : 0.f;
+          }
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+          sm[j][e] = t;
+        }
+      }
+      if (pass) __builtin_amdgcn_s_barrier();  // pass 0's sums read by every wave before reuse
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < CP_NB; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) red[wm * 256 + wn * CP_WN + 16 * j + 4 * (lane >> 4) + e] = sm[j][e];
+      }
+      lds_barrier();
+      if (threadIdx.x < 256 && n0 + (int)threadIdx.x < p.N)  // pass 0: tile sums, pass 1: centred squares
+        p.stats[((long)tm * 2 + pass) * p.N + n0 + threadIdx.x] = red[threadIdx.x] + red[256 + threadIdx.x];
+    }
+  }
 #pragma unroll
   for (int j = 0; j < CP_NB; ++j) {
     const int n = n0 + wn * CP_WN + 16 * j + 4 * (lane >> 4);
@@ -322,6 +374,50 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_panel_kernel(CwArgs p) {
     }
 }
 
+// BatchNorm batch statistics from the per-tile (sum, centred sum of squares) of conv_panel_kernel:
+// Chan et al.'s pairwise update, 16 phases per channel (tiles t = ph, ph + 16, ...) then the 16 phase
+// results in order — a fixed order (deterministic). Then as bn_var_kernel: invstd = 1/sqrt(var + eps)
+// (biased variance), running mean / unbiased running variance with the momentum.
+__global__ __launch_bounds__(1024) void bn_merge_kernel(const float* __restrict__ stats, int T, long M, int C,
+                                                       float* mean, float* invstd, float* run_mean, float* run_var,
+                                                       float mom, float eps) {
+  __shared__ float sn[16][64], smu[16][64], sm2[16][64];
+  const int lc = threadIdx.x & 63, ph = threadIdx.x >> 6, c = blockIdx.x * 64 + lc;
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  if (c < C) {
+    for (int t = ph; t < T; t += 16) {
+      const float nb = (float)min((long)CP_BM, M - (long)t * CP_BM);
+      const float mb = stats[(long)t * 2 * C + c] / nb, q = stats[((long)t * 2 + 1) * C + c];
+      const float nn = n + nb, d = mb - mu;
+      mu += d * (nb / nn);
+      m2 += q + d * d * (n * nb / nn);
+      n = nn;
+    }
+  }
+  sn[ph][lc] = n;
+  smu[ph][lc] = mu;
+  sm2[ph][lc] = m2;
+  __syncthreads();
+  if (ph == 0 && c < C) {
+    n = sn[0][lc];
+    mu = smu[0][lc];
+    m2 = sm2[0][lc];
+    for (int k = 1; k < 16; ++k) {
+      const float nb = sn[k][lc];
+      if (nb <= 0.f) continue;
+      const float nn = n + nb, d = smu[k][lc] - mu;
+      mu += d * (nb / nn);
+      m2 += sm2[k][lc] + d * d * (n * nb / nn);
+      n = nn;
+    }
+    const float var = m2 / (float)M;
+    mean[c] = mu;
+    invstd[c] = 1.0f / sqrtf(var + eps);
+    if (run_mean) run_mean[c] = (1.f - mom) * run_mean[c] + mom * mu;
+    if (run_var) run_var[c] = (1.f - mom) * run_var[c] + mom * (M > 1 ? m2 / (float)(M - 1) : var);
+  }
+}
+
 // dgrad weights: Bt[ci][(ky', kx'), co] = w[co][ci][ks-1-ky'][ks-1-kx']  (torch f32 layout in)
 template <typename O>
 __global__ void pack_conv_t_kernel(const float* __restrict__ w, long Cout, long Cin, long ks, O* out) {
@@ -369,16 +465,24 @@ int conv_wgrad_panel_launch(const bf16* dY, long lddy, const bf16* X, int Bn, in
 }
 
 int conv_panel_launch(const bf16* A, long lda, int Bn, int H, int W, int Cin, int ks, const bf16* Bk, int N,
-                      const float* bias, void* Y, long ldy, bool y_bf16, hipStream_t st) {
+                      const float* bias, void* Y, long ldy, bool y_bf16, hipStream_t st, float* stats) {
   const int M = Bn * H * W;
-  CpArgs p{A, lda, H, W, Cin, ks, M, Bk, N, ks * ks * Cin, bias, Y, ldy, ivit_cdiv(N, CP_BN)};
+  CpArgs p{A, lda, H, W, Cin, ks, M, Bk, N, ks * ks * Cin, bias, Y, ldy, ivit_cdiv(N, CP_BN), stats};
   const dim3 grid(ivit_cdiv(M, CP_BM) * p.tilesN);
-  if (y_bf16)
-    hipLaunchKernelGGL(conv_panel_kernel<bf16>, grid, dim3(512), 0, st, p);
-  else
-    hipLaunchKernelGGL(conv_panel_kernel<float>, grid, dim3(512), 0, st, p);
+  if (stats) {
+    if (y_bf16)
+      hipLaunchKernelGGL((conv_panel_kernel<bf16, true>), grid, dim3(512), 0, st, p);
+    else
+      hipLaunchKernelGGL((conv_panel_kernel<float, true>), grid, dim3(512), 0, st, p);
+  } else if (y_bf16) {
+    hipLaunchKernelGGL((conv_panel_kernel<bf16, false>), grid, dim3(512), 0, st, p);
+  } else {
+    hipLaunchKernelGGL((conv_panel_kernel<float, false>), grid, dim3(512), 0, st, p);
+  }
   return 0;
 }
+
+long conv_panel_stats_floats(long M, long N) { return (long)ivit_cdiv(M, CP_BM) * 2 * N; }
 
 }  // namespace ivit
 
@@ -407,4 +511,32 @@ extern "C" int ivit_conv_dgrad_t(int dtype, const void* dY, long lddy, long B, l
                     nullptr, dX, Cin, dx_dtype == IVIT_BF16, st);
   IVIT_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" long ivit_conv_bn_fwd_workspace(long B, long H, long W, long Cout) {
+  const long M = B * H * W;
+  const long a = conv_panel_stats_floats(M, Cout) * 4, b = ivit_bn_workspace(M, Cout);
+  return a > b ? a : b;
+}
+
+extern "C" int ivit_conv_bn_fwd(int dtype, const void* X, long B, long H, long W, long Cin, const void* Wp, long Cout,
+                                long ks, void* Y, long ldy, int y_dtype, float* mean, float* invstd, float* run_mean,
+                                float* run_var, float momentum, float eps, void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(work_bytes >= ivit_conv_bn_fwd_workspace(B, H, W, Cout), "ivit_conv_bn_fwd: workspace too small");
+  IVIT_CHECK_ARG(ldy == Cout, "ivit_conv_bn_fwd: the output must be dense (ldy == Cout)");
+  hipStream_t st = ivit_stream(stream);
+  const long M = B * H * W;
+  if (dtype == IVIT_BF16 && conv_panel_enabled() && conv_panel_ok(M, Cout, Cin, Cin, ks) && ldy % 4 == 0) {
+    float* stats = (float*)work;
+    conv_panel_launch((const bf16*)X, Cin, (int)B, (int)H, (int)W, (int)Cin, (int)ks, (const bf16*)Wp, (int)Cout,
+                      nullptr, Y, ldy, y_dtype == IVIT_BF16, st, stats);
+    IVIT_LAUNCH_CHECK();
+    hipLaunchKernelGGL(bn_merge_kernel, dim3(ivit_cdiv(Cout, 64)), dim3(1024), 0, st, stats, ivit_cdiv(M, CP_BM), M,
+                       (int)Cout, mean, invstd, run_mean, run_var, momentum, eps);
+    IVIT_LAUNCH_CHECK();
+    return 0;
+  }
+  int rc = ivit_conv_fwd(dtype, X, B, H, W, Cin, Wp, nullptr, Cout, ks, Y, ldy, y_dtype, stream);
+  if (rc) return rc;
+  return ivit_bn_stats(Y, y_dtype, M, Cout, mean, invstd, run_mean, run_var, momentum, eps, work, work_bytes, stream);
 }

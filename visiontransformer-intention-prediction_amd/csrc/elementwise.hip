@@ -29,6 +29,33 @@ __global__ void add_act_grad_kernel(const void* a, int adt, const void* b, int b
   stv(out, odt, i, v);
 }
 
+// 8 elements per thread (n % 8 == 0, row_elems % 8 == 0, 16-B aligned operands): the same per-element
+// arithmetic and order as add_act_grad_kernel, 16-B accesses
+__global__ __launch_bounds__(256) void add_act_grad8_kernel(const void* a, int adt, const void* b, int bdt,
+                                                           const void* pre, int pdt, const float* rs, long re,
+                                                           void* out, int odt, long n) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (i >= n) return;
+  float v[8], w[8];
+  ld8dt(a, adt, i, v);
+  if (b) {
+    ld8dt(b, bdt, i, w);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += w[e];
+  }
+  if (pre) {
+    ld8dt(pre, pdt, i, w);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= gelu_erf_grad(w[e]);
+  }
+  if (rs) {
+    const float r = rs[i / re];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= r;
+  }
+  st8dt(out, odt, i, v);
+}
+
 // standalone activation modules (nn.GELU exact erf / nn.ReLU) and their input gradients
 __global__ void act_fwd_kernel(int act, const void* x, int xdt, void* y, int ydt, long n) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -240,8 +267,13 @@ extern "C" int ivit_add_act_grad(const void* a, int a_dtype, const void* b, int 
                                  int pre_dtype, const float* row_scale, long row_elems, void* out, int out_dtype, long n,
                                  void* stream) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(add_act_grad_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), a, a_dtype, b,
-                     b_dtype, pre, pre_dtype, row_scale, row_elems > 0 ? row_elems : 1, out, out_dtype, n);
+  const long re = row_elems > 0 ? row_elems : 1;
+  if (n % 8 == 0 && (!row_scale || re % 8 == 0) && hal16(a) && (!b || hal16(b)) && (!pre || hal16(pre)) && hal16(out))
+    hipLaunchKernelGGL(add_act_grad8_kernel, dim3(ivit_cdiv(n / 8, 256)), dim3(256), 0, ivit_stream(stream), a, a_dtype,
+                       b, b_dtype, pre, pre_dtype, row_scale, re, out, out_dtype, n);
+  else
+    hipLaunchKernelGGL(add_act_grad_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, ivit_stream(stream), a, a_dtype, b,
+                       b_dtype, pre, pre_dtype, row_scale, re, out, out_dtype, n);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

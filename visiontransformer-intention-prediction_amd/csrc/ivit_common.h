@@ -114,6 +114,7 @@ template <typename O> IVIT_DEV float gelu_grad_t(float x) {
 }
 
 IVIT_DEV bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static inline bool hal16(const void* p) { return ((uintptr_t)p & 15) == 0; }  // host side
 
 // ---------------------------------------------------------------- diagnostic stamps
 // (ivit_debug_stamps) Kernels built with a stamping flag record clocks per workgroup; lane 0 of
@@ -172,6 +173,17 @@ IVIT_DEV void load8f(const T* p, float (&x)[8], int nv) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) x[k] = k < nv ? to_f32(p[k]) : 0.f;
   }
+}
+
+// 8 consecutive elements of a bf16 / f32 buffer selected by a runtime dtype code (16-B aligned when
+// the element offset is a multiple of 8 and the base is 16-B aligned)
+IVIT_DEV void ld8dt(const void* p, int dt, long i, float (&x)[8]) {
+  if (dt == IVIT_BF16) load8f((const bf16*)p + i, x, 8);
+  else load8f((const float*)p + i, x, 8);
+}
+IVIT_DEV void st8dt(void* p, int dt, long i, const float (&x)[8]) {
+  if (dt == IVIT_BF16) store8((bf16*)p + i, x, 8);
+  else store8((float*)p + i, x, 8);
 }
 
 // Raw v_exp_f32 (2^x; results below 2^-126 flush to 0 — harmless for softmax weights).

@@ -464,6 +464,25 @@ def pack_conv_t(w, cdt):
     return out
 
 
+def conv_bn_fwd(x, B, H, W, wp, cdt, out_dtype, rmean, rvar, training, momentum=0.1, eps=1e-5, nbt=None):
+    """conv (no bias) and the following BatchNorm2d's statistics: in training the batch statistics
+    come out of the convolution's epilogue (ivit_conv_bn_fwd; BasicBlock conv -> bn,
+    model_vit.py:24-27,35-43), in eval the running ones. -> (y, _BNState)."""
+    if not training:
+        y = conv_fwd(x, B, H, W, wp, None, cdt, out_dtype)
+        return y, bn_forward(y, None, None, rmean, rvar, False, momentum, eps)
+    Cout, k, _, Cin = wp.shape
+    y = torch.empty((B * H * W, Cout), dtype=out_dtype, device=x.device)
+    mean = torch.empty((Cout,), dtype=torch.float32, device=x.device)
+    invstd = torch.empty_like(mean)
+    ws = workspace(lib.ivit_conv_bn_fwd_workspace(B, H, W, Cout), x.device)
+    lib.ivit_conv_bn_fwd(cdt, ptr(x), B, H, W, Cin, ptr(wp), Cout, k, ptr(y), Cout, dt(y), ptr(mean), ptr(invstd),
+                         ptr(rmean), ptr(rvar), momentum, eps, ptr(ws), ws.numel(), stream())
+    if nbt is not None:
+        nbt.add_(1)
+    return y, _BNState(mean, invstd)
+
+
 def conv_dgrad(dy, B, H, W, wp, cdt, out_dtype, w=None):
     """dX of a stride-1 'same' conv. With the f32 weight `w` (torch layout) and a bf16 shape the
     288 x 256 panel kernel takes (ivit_conv_dgrad_t: Cout % 64, Cin >= 128, >= 288 pixels), the
@@ -857,19 +876,16 @@ class NeckFn(torch.autograd.Function):
             p = f"fusion_block.{li}."
             w1 = pack_conv(P[p + "conv1.weight"], cdt)
             w2 = pack_conv(P[p + "conv2.weight"], cdt)
-            c1 = conv_fwd(x, B, Hf, Wf, w1, None, cdt, torch.float32)
-            s1 = bn_forward(c1, P[p + "bn1.weight"], P[p + "bn1.bias"], P[p + "bn1.running_mean"],
-                            P[p + "bn1.running_var"], training, nbt=P.get(p + "bn1.num_batches_tracked"))
+            c1, s1 = conv_bn_fwd(x, B, Hf, Wf, w1, cdt, torch.float32, P[p + "bn1.running_mean"],
+                                 P[p + "bn1.running_var"], training, nbt=P.get(p + "bn1.num_batches_tracked"))
             r1 = bn_apply(c1, s1, P[p + "bn1.weight"], P[p + "bn1.bias"], cd, relu=True)
-            c2 = conv_fwd(r1, B, Hf, Wf, w2, None, cdt, torch.float32)
-            s2 = bn_forward(c2, P[p + "bn2.weight"], P[p + "bn2.bias"], P[p + "bn2.running_mean"],
-                            P[p + "bn2.running_var"], training, nbt=P.get(p + "bn2.num_batches_tracked"))
+            c2, s2 = conv_bn_fwd(r1, B, Hf, Wf, w2, cdt, torch.float32, P[p + "bn2.running_mean"],
+                                 P[p + "bn2.running_var"], training, nbt=P.get(p + "bn2.num_batches_tracked"))
             if (p + "downsample.0.weight") in P:
                 wd = pack_conv(P[p + "downsample.0.weight"], cdt)
-                dd = conv_fwd(x, B, Hf, Wf, wd, None, cdt, torch.float32)
-                sd = bn_forward(dd, P[p + "downsample.1.weight"], P[p + "downsample.1.bias"],
-                                P[p + "downsample.1.running_mean"], P[p + "downsample.1.running_var"], training,
-                                nbt=P.get(p + "downsample.1.num_batches_tracked"))
+                dd, sd = conv_bn_fwd(x, B, Hf, Wf, wd, cdt, torch.float32, P[p + "downsample.1.running_mean"],
+                                     P[p + "downsample.1.running_var"], training,
+                                     nbt=P.get(p + "downsample.1.num_batches_tracked"))
                 idn = bn_apply(dd, sd, P[p + "downsample.1.weight"], P[p + "downsample.1.bias"], cd)
                 bns[p + "ds"] = (dd, sd, idn)
                 packs[p + "ds"] = wd
