@@ -449,31 +449,41 @@ __global__ void bn_apply_kernel(const void* X, int xdt, long M, int C, const flo
   stv(Y, ydt, i, v);
 }
 
-// 8 consecutive channels per thread (C % 8 == 0, 16-B aligned operands): the same per-element
-// arithmetic as bn_apply_kernel / bn_bwd_apply_kernel (bitwise the same results), 16-B accesses.
+// 8 consecutive channels x BN8_R rows per thread (C % 8 == 0, 16-B aligned operands): the channel
+// parameters are loaded once per thread (per element they were 4x the bytes of the data), rows
+// strided by C; the same per-element arithmetic as bn_apply_kernel / bn_bwd_apply_kernel (bitwise
+// the same results), 16-B accesses. Thread t: chunk t % (C / 8), rows (t / (C / 8)) * BN8_R + 0..
+constexpr int BN8_R = 8;
 __global__ __launch_bounds__(256) void bn_apply8_kernel(const void* X, int xdt, long M, int C,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
                                                        const float* __restrict__ g, const float* __restrict__ b,
                                                        const void* R, int relu, void* Y, int ydt, int rdt) {
-  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (i >= M * C) return;
-  const int c = (int)(i % C);
-  float x[8], r[8], mu[8], is[8], gg[8], bb[8];
-  ld8dt(X, xdt, i, x);
-  if (R) ld8dt(R, rdt, i, r);
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nc = C / 8;
+  const int c = (int)(t % nc) * 8;
+  const long r0 = (t / nc) * BN8_R;
+  if (r0 >= M) return;
+  float mu[8], is[8], gg[8], bb[8];
   load8f(mean + c, mu, 8);
   load8f(invstd + c, is, 8);
   load8f(g + c, gg, 8);
   load8f(b + c, bb, 8);
+  const long r1 = min(M, r0 + BN8_R);
+  for (long r = r0; r < r1; ++r) {
+    const long i = r * C + c;
+    float x[8], q[8];
+    ld8dt(X, xdt, i, x);
+    if (R) ld8dt(R, rdt, i, q);
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    float v = (x[e] - mu[e]) * is[e] * gg[e] + bb[e];
-    if (R) v += r[e];
-    if (relu) v = fmaxf(v, 0.f);
-    x[e] = v;
+    for (int e = 0; e < 8; ++e) {
+      float v = (x[e] - mu[e]) * is[e] * gg[e] + bb[e];
+      if (R) v += q[e];
+      if (relu) v = fmaxf(v, 0.f);
+      x[e] = v;
+    }
+    st8dt(Y, ydt, i, x);
   }
-  st8dt(Y, ydt, i, x);
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(const void* X, int xdt, const void* Y, int ydt,
@@ -483,29 +493,40 @@ __global__ __launch_bounds__(256) void bn_bwd_apply8_kernel(const void* X, int x
                                                            const float* __restrict__ g,
                                                            const float* __restrict__ sums, int relu, void* dX,
                                                            int dxdt, void* dR) {
-  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (i >= M * C) return;
-  const int c = (int)(i % C);
-  float dz[8], y[8], x[8], mu[8], is[8], gg[8], s1[8], s2[8];
-  ld8dt(dY, dydt, i, dz);
-  if (relu) ld8dt(Y, ydt, i, y);
-  ld8dt(X, xdt, i, x);
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nc = C / 8;
+  const int c = (int)(t % nc) * 8;
+  const long r0 = (t / nc) * BN8_R;
+  if (r0 >= M) return;
+  float mu[8], is[8], gg[8], m1[8], m2[8];
   load8f(mean + c, mu, 8);
   load8f(invstd + c, is, 8);
   load8f(g + c, gg, 8);
-  load8f(sums + c, s1, 8);
-  load8f(sums + C + c, s2, 8);
-#pragma unroll
-  for (int e = 0; e < 8; ++e)
-    if (relu && y[e] <= 0.f) dz[e] = 0.f;
-  if (dR) st8dt(dR, dxdt, i, dz);
+  load8f(sums + c, m1, 8);
+  load8f(sums + C + c, m2, 8);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const float xh = (x[e] - mu[e]) * is[e];
-    const float m1 = s1[e] / (float)M, m2 = s2[e] / (float)M;
-    x[e] = is[e] * gg[e] * (dz[e] - m1 - xh * m2);
+    m1[e] = m1[e] / (float)M;
+    m2[e] = m2[e] / (float)M;
   }
-  st8dt(dX, dxdt, i, x);
+  const long r1 = min(M, r0 + BN8_R);
+  for (long r = r0; r < r1; ++r) {
+    const long i = r * C + c;
+    float dz[8], y[8], x[8];
+    ld8dt(dY, dydt, i, dz);
+    if (relu) ld8dt(Y, ydt, i, y);
+    ld8dt(X, xdt, i, x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (relu && y[e] <= 0.f) dz[e] = 0.f;
+    if (dR) st8dt(dR, dxdt, i, dz);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xh = (x[e] - mu[e]) * is[e];
+      x[e] = is[e] * gg[e] * (dz[e] - m1[e] - xh * m2[e]);
+    }
+    st8dt(dX, dxdt, i, x);
+  }
 }
 
 __global__ void bn_bwd_apply_kernel(const void* X, int xdt, const void* Y, int ydt, const void* dY, int dydt, long M,
@@ -635,7 +656,8 @@ extern "C" int ivit_bn_apply(const void* X, int x_dtype, long M, long C, const f
   const bool v8 = C % 8 == 0 && hal16(X) && hal16(Y) && (!R || hal16(R)) && hal16(mean) && hal16(invstd) && hal16(g) &&
                   hal16(b);
   if (v8)
-    hipLaunchKernelGGL(bn_apply8_kernel, dim3(ivit_cdiv(M * C / 8, 256)), dim3(256), 0, ivit_stream(stream), X, x_dtype,
+    hipLaunchKernelGGL(bn_apply8_kernel, dim3(ivit_cdiv(ivit_cdiv(M, BN8_R) * (C / 8), 256)), dim3(256), 0,
+                       ivit_stream(stream), X, x_dtype,
                        M, (int)C, mean, invstd, g, b, R, relu, Y, y_dtype, y_dtype);
   else
     hipLaunchKernelGGL(bn_apply_kernel, dim3(ivit_cdiv(M * C, 256)), dim3(256), 0, ivit_stream(stream), X, x_dtype, M,
@@ -659,7 +681,8 @@ extern "C" int ivit_bn_bwd(const void* X, int x_dtype, const void* Y, int y_dtyp
   const bool v8 = C % 8 == 0 && hal16(X) && (!relu || hal16(Y)) && hal16(dY) && hal16(dX) && (!dR || hal16(dR)) &&
                   hal16(mean) && hal16(invstd) && hal16(g) && hal16(sums);
   if (v8)
-    hipLaunchKernelGGL(bn_bwd_apply8_kernel, dim3(ivit_cdiv(M * C / 8, 256)), dim3(256), 0, st, X, x_dtype, Y, y_dtype,
+    hipLaunchKernelGGL(bn_bwd_apply8_kernel, dim3(ivit_cdiv(ivit_cdiv(M, BN8_R) * (C / 8), 256)), dim3(256), 0, st, X,
+                       x_dtype, Y, y_dtype,
                        dY, dy_dtype, M, (int)C, mean, invstd, g, sums, relu, dX, dx_dtype, dR);
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ivit_cdiv(M * C, 256)), dim3(256), 0, st, X, x_dtype, Y, y_dtype, dY,
