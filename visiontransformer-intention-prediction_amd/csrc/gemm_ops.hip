@@ -354,19 +354,29 @@ __global__ void pos_grad_kernel(const S* __restrict__ dtok, long B, long Ntok, l
 // 2-B loads plus a separate column-sum pass over the same token gradient.
 template <typename S>
 __global__ __launch_bounds__(1024) void pos_bias_grad_kernel(const S* __restrict__ dtok, int B, int Ntok, int D,
-                                                            int RB, float* dpos, float* dcls, float* part,
+                                                            int RB, int NPH, float* dpos, float* dcls, float* part,
                                                             int accumulate) {
-  __shared__ float red[4 * 1024];
+  __shared__ float red[16 * 512];
   const int nc = D / 8, cc = threadIdx.x % nc, ph = threadIdx.x / nc;
   const int t0 = blockIdx.x * RB, t1 = min(Ntok, t0 + RB);
   float ps[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) ps[j] = 0.f;
-  for (int t = t0 + ph; t < t1; t += 4) {
+  for (int t = t0 + ph; t < t1; t += NPH) {
     float s[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[j] = 0.f;
-    for (int b = 0; b < B; ++b) {
+    int b = 0;
+    for (; b + 4 <= B; b += 4) {  // four images' rows in flight, summed in image order
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load8f(dtok + ((long)(b + u) * Ntok + t) * D + 8 * cc, v[u], 8);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += v[u][j];
+    }
+    for (; b < B; ++b) {
       const S* q = dtok + ((long)b * Ntok + t) * D + 8 * cc;
       float v[8];
       load8f(q, v, 8);
@@ -410,7 +420,9 @@ __global__ __launch_bounds__(1024) void pos_bias_grad_kernel(const S* __restrict
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = 8 * cc + j;
-      part[(long)blockIdx.x * D + c] = ((red[c] + red[D + c]) + red[2 * D + c]) + red[3 * D + c];
+      float v = red[c];
+      for (int q = 1; q < NPH; ++q) v += red[q * D + c];
+      part[(long)blockIdx.x * D + c] = v;
     }
   }
 }
@@ -426,13 +438,16 @@ static int patch_pos_bias_grad(int dtype, const void* dtok, long B, long Np, lon
   RB = ((RB < 32 ? 32 : RB) + 3) / 4 * 4;
   const int nb = ivit_cdiv(Ntok, RB);
   const bool al = ((uintptr_t)dtok & 15) == 0 && ((uintptr_t)dpos & 15) == 0 && (!dcls || ((uintptr_t)dcls & 15) == 0);
-  if (D % 8 == 0 && D <= 1024 && al && (long)nb * D * 4 <= cw_bytes && dbias) {
+  if (D % 8 == 0 && D <= 512 && al && (long)nb * D * 4 <= cw_bytes && dbias) {
+    // row phases per block: as many as fit 1024 threads, at most 16 (the LDS partial rows)
+    int nph = 1024 / (int)(D / 8);
+    if (nph > 16) nph = 16;
     if (dtype == IVIT_BF16)
-      hipLaunchKernelGGL(pos_bias_grad_kernel<bf16>, dim3(nb), dim3(4 * D / 8), 0, st, (const bf16*)dtok, (int)B,
-                         (int)Ntok, (int)D, RB, dpos, dcls, (float*)cw, accumulate);
+      hipLaunchKernelGGL(pos_bias_grad_kernel<bf16>, dim3(nb), dim3(nph * D / 8), 0, st, (const bf16*)dtok, (int)B,
+                         (int)Ntok, (int)D, RB, nph, dpos, dcls, (float*)cw, accumulate);
     else
-      hipLaunchKernelGGL(pos_bias_grad_kernel<float>, dim3(nb), dim3(4 * D / 8), 0, st, (const float*)dtok, (int)B,
-                         (int)Ntok, (int)D, RB, dpos, dcls, (float*)cw, accumulate);
+      hipLaunchKernelGGL(pos_bias_grad_kernel<float>, dim3(nb), dim3(nph * D / 8), 0, st, (const float*)dtok, (int)B,
+                         (int)Ntok, (int)D, RB, nph, dpos, dcls, (float*)cw, accumulate);
     IVIT_LAUNCH_CHECK();
     launch_colreduce(st, (const float*)cw, nb, D, (int)D, dbias, (int)D, nullptr, accumulate);
     IVIT_LAUNCH_CHECK();

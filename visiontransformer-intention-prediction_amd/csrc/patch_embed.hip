@@ -604,14 +604,35 @@ __global__ __launch_bounds__(256) void patch_wgrad_reduce_kernel(const float* __
   if (g >= G) return;
   const int e = (int)(i0 - (long)g * per) + threadIdx.x, n = e >> 7, k = e & 127;
   const long U = (long)G * J, ga = (long)g * J, gb = ga + J;
-  int w = (int)(ga * WG_NWG / U);
-  while (w > 0 && wg_unit_start(w, U) > ga) --w;
+  // the contiguous workgroup range [w0, w1) whose unit ranges meet pair g (block-uniform); only w0
+  // can have begun in the previous pair (its partial tile of g is then its second slab slot)
+  int w0 = (int)(ga * WG_NWG / U);
+  while (w0 > 0 && wg_unit_start(w0, U) > ga) --w0;
+  while (w0 < WG_NWG && wg_unit_start(w0 + 1, U) <= ga) ++w0;
+  int w1 = w0;
+  while (w1 < WG_NWG && wg_unit_start(w1, U) < gb) ++w1;
+  const int slot0 = wg_unit_start(w0, U) < ga ? 1 : 0;
   float s = 0.f;
-  for (; w < WG_NWG && wg_unit_start(w, U) < gb; ++w) {
-    const long a = wg_unit_start(w, U), b = wg_unit_start(w + 1, U);
-    if (b <= ga || b <= a) continue;
-    const int slot = g - (int)(a / J);
-    s += slab[(((long)w * 2 + slot) * D + n) * 128 + k];
+  const long estride = 2L * D * 128;  // one workgroup's two slab slots
+  const float* base = slab + ((long)w0 * 2 * D + n) * 128 + k;
+  if (U < WG_NWG) {  // tiny grids: some workgroups own no units (and wrote no slab): skip them
+    for (int w = w0; w < w1; ++w) {
+      const long a = wg_unit_start(w, U), b = wg_unit_start(w + 1, U);
+      if (b <= a) continue;
+      s += slab[(((long)w * 2 + (a < ga ? 1 : 0)) * D + n) * 128 + k];
+    }
+  } else if (w0 < w1) {
+    s = base[(long)slot0 * D * 128];
+    // the rest start in pair g (slot 0): independent loads, eight in flight, summed in order
+    int w = w0 + 1;
+    for (; w + 8 <= w1; w += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = base[(long)(w - w0 + q) * estride];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s += v[q];
+    }
+    for (; w < w1; ++w) s += base[(long)(w - w0) * estride];
   }
   if (2 * g + (k >> 6) >= C) return;
   float* o = dW + (long)n * C * 64 + (long)g * 128 + k;
