@@ -292,8 +292,10 @@ extern "C" int ivit_patch_weight_pack(const float* w, long D, long C, void* wpac
 extern "C" int ivit_weight_pack_multi(long n, const void* jobs, long max_rows_cols, void* stream) {
   if (n <= 0) return 0;
   IVIT_CHECK_ARG(n < 65536 && jobs != nullptr, "ivit_weight_pack_multi: bad job table");
+  // x blocks per job: a grid of 1024 x jobs left most blocks of the ~150 small packs (<= 288 blocks
+  // of work each) empty; the large ones (the patch embedding's) grid-stride instead
   int gx = ivit_cdiv(max_rows_cols / 8, 256);
-  if (gx > 1024) gx = 1024;
+  if (gx > 288) gx = 288;
   hipLaunchKernelGGL(multi_pack_kernel, dim3(gx, n), dim3(256), 0, ivit_stream(stream), (const PackJob*)jobs);
   IVIT_LAUNCH_CHECK();
   return 0;
