@@ -174,9 +174,11 @@ long ivit_conv_bn_fwd_workspace(long B, long H, long W, long Cout);
 int ivit_conv_bn_fwd(int dtype, const void* X, long B, long H, long W, long Cin, const void* Wp, long Cout, long ks,
                      void* Y, long ldy, int y_dtype, float* mean, float* invstd, float* run_mean, float* run_var,
                      float momentum, float eps, void* work, long work_bytes, void* stream);
-/* torch [Cout][Cin][k][k] f32  ->  [Cin][k][k][Cout] (dtype) with the taps flipped: the K-contiguous
- * weight of the data gradient, WpT[ci][ky][kx][co] = w[co][ci][k-1-ky][k-1-kx]. */
-int ivit_pack_conv_weight_t(int dtype, const float* w, long Cout, long Cin, long ks, void* out, void* stream);
+/* torch [Cout][Cin][k][k] f32  ->  [Cin][k][k][Cout_pad] (dtype) with the taps flipped: the K-contiguous
+ * weight of the data gradient, WpT[ci][ky][kx][co] = w[co][ci][k-1-ky][k-1-kx], zero for co >= Cout
+ * (the pack for a gradient zero-padded to Cout_pad channels). */
+int ivit_pack_conv_weight_t(int dtype, const float* w, long Cout, long Cin, long ks, long Cout_pad, void* out,
+                            void* stream);
 /* torch [Cout][Cin][k][k] f32  ->  packed [Cout_pad][k][k][Cin] (dtype), rows >= Cout zeroed. */
 int ivit_pack_conv_weight(int dtype, const float* w, long Cout, long Cin, long ks, long Cout_pad, void* out,
                           void* stream);

@@ -365,6 +365,31 @@ def test_conv_panel(B, H, W, Cin, Cout, k, ybf):
     assert _rel(db, dyh.float().cpu().double().sum(0)) < 1e-5
 
 
+def test_conv_dgrad_zero_padded_head():
+    """The head conv's data gradient (heads.py:16,37: 75 output channels, packed to 80) on the panel
+    kernel: dy rows zero-padded to 128 channels and the transposed pack zero past channel 75
+    (ivit_pack_conv_weight_t Cout_pad) vs the 128 x 128 engine on the forward pack and vs f64."""
+    import ops
+    from _lib import BF16
+    torch.manual_seed(11)
+    B, H, W, Cin, Cw, Cp, Cq = 2, 50, 90, 512, 75, 80, 128
+    w = torch.randn(Cw, Cin, 3, 3) / math.sqrt(Cin * 9)
+    wd = w.to(DEV)
+    wp = ops.pack_conv(wd, BF16, cout_pad=Cp)
+    dyq = torch.zeros(B * H * W, Cq)
+    dyq[:, :Cw] = torch.randn(B * H * W, Cw)
+    dyh = ops.cast(dyq.to(DEV), torch.bfloat16)
+    wt = ops.pack_conv_t(wd, BF16, cout_pad=Cq)
+    assert torch.equal(wt[..., Cw:].float().cpu(), torch.zeros(Cin, 3, 3, Cq - Cw))
+    dx = ops.conv_dgrad(dyh, B, H, W, wp, BF16, torch.float32, w=wd, dy_zero_pad=True)
+    dx0 = ops.conv_dgrad(dyh, B, H, W, wp, BF16, torch.float32)  # engine, reads the first 80 channels
+    assert _rel(dx, dx0) < 1e-5
+    wr = w.bfloat16().double()
+    dyr = dyh.float().cpu().double()[:, :Cw].reshape(B, H, W, Cw).permute(0, 3, 1, 2)
+    ref = F.conv_transpose2d(dyr, wr, padding=1)
+    assert _rel(dx.reshape(B, H, W, Cin).permute(0, 3, 1, 2), ref) < 1e-5
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k", [(8, 50, 90, 384, 512, 3), (1, 19, 23, 64, 256, 1), (1, 7, 9, 48, 40, 3)])
 def test_conv_bn_stats_fused(B, H, W, Cin, Cout, k):
     """ivit_conv_bn_fwd: the BatchNorm batch statistics out of the panel convolution's epilogue (per-

@@ -48,6 +48,19 @@ def main():
                       f"dgrad(+pack) {td:7.1f} us ({fl / td / 1e6:6.1f} TF/s)  "
                       f"wgrad(+reduce) {tw:7.1f} us ({fl / tw / 1e6:6.1f} TF/s)", flush=True)
     os.environ["IVIT_CONV_PANEL"] = "1"
+    # head conv data gradient (75 channels packed to 80): engine vs the panel kernel on rows zero-padded to 128
+    cin, cw, cp, cq = 512, 75, 80, 128
+    w = torch.randn(cw, cin, 3, 3, device=dev) / (cin * 9) ** 0.5
+    wp = ops.pack_conv(w, BF16, cout_pad=cp)
+    dy = torch.zeros(M, cq, device=dev)
+    dy[:, :cw] = torch.randn(M, cw, device=dev)
+    dy = dy.bfloat16()
+    fl = 2.0 * M * cw * cin * 9
+    for rep in range(2):
+        te = timed(lambda: ops.conv_dgrad(dy, B, H, W, wp, BF16, torch.float32))
+        tp = timed(lambda: ops.conv_dgrad(dy, B, H, W, wp, BF16, torch.float32, w=w, dy_zero_pad=True))
+        print(f"head {cin}->{cw} k3 dgrad: engine {te:7.1f} us ({fl / te / 1e6:6.1f} TF/s)  "
+              f"panel(pad {cq}, +pack) {tp:7.1f} us ({fl / tp / 1e6:6.1f} TF/s)", flush=True)
 
 
 if __name__ == "__main__":

@@ -418,15 +418,16 @@ __global__ __launch_bounds__(1024) void bn_merge_kernel(const float* __restrict_
   }
 }
 
-// dgrad weights: Bt[ci][(ky', kx'), co] = w[co][ci][ks-1-ky'][ks-1-kx']  (torch f32 layout in)
+// dgrad weights: Bt[ci][(ky', kx'), co] = w[co][ci][ks-1-ky'][ks-1-kx']  (torch f32 layout in); Cpad >= Cout
+// channels per row, zero for co >= Cout (the pack of a gradient zero-padded to Cpad channels)
 template <typename O>
-__global__ void pack_conv_t_kernel(const float* __restrict__ w, long Cout, long Cin, long ks, O* out) {
+__global__ void pack_conv_t_kernel(const float* __restrict__ w, long Cout, long Cin, long ks, long Cpad, O* out) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long n = Cin * ks * ks * Cout;
+  const long n = Cin * ks * ks * Cpad;
   if (i >= n) return;
-  const long co = i % Cout, t = i / Cout, tap = t % (ks * ks), ci = t / (ks * ks);
+  const long co = i % Cpad, t = i / Cpad, tap = t % (ks * ks), ci = t / (ks * ks);
   const long ky = ks - 1 - tap / ks, kx = ks - 1 - tap % ks;
-  out[i] = from_f32<O>(w[((co * Cin + ci) * ks + ky) * ks + kx]);
+  out[i] = co < Cout ? from_f32<O>(w[((co * Cin + ci) * ks + ky) * ks + kx]) : from_f32<O>(0.f);
 }
 
 }  // namespace
@@ -488,15 +489,16 @@ long conv_panel_stats_floats(long M, long N) { return (long)ivit_cdiv(M, CP_BM) 
 
 using namespace ivit;
 
-extern "C" int ivit_pack_conv_weight_t(int dtype, const float* w, long Cout, long Cin, long ks, void* out,
+extern "C" int ivit_pack_conv_weight_t(int dtype, const float* w, long Cout, long Cin, long ks, long Cout_pad, void* out,
                                        void* stream) {
+  IVIT_CHECK_ARG(Cout_pad >= Cout && Cout > 0, "ivit_pack_conv_weight_t: Cout_pad < Cout");
   hipStream_t st = ivit_stream(stream);
-  const long n = Cin * ks * ks * Cout;
+  const long n = Cin * ks * ks * Cout_pad;
   if (dtype == IVIT_BF16)
-    hipLaunchKernelGGL(pack_conv_t_kernel<bf16>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, w, Cout, Cin, ks,
+    hipLaunchKernelGGL(pack_conv_t_kernel<bf16>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, w, Cout, Cin, ks, Cout_pad,
                        (bf16*)out);
   else
-    hipLaunchKernelGGL(pack_conv_t_kernel<float>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, w, Cout, Cin, ks,
+    hipLaunchKernelGGL(pack_conv_t_kernel<float>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, w, Cout, Cin, ks, Cout_pad,
                        (float*)out);
   IVIT_LAUNCH_CHECK();
   return 0;

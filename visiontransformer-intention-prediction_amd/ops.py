@@ -456,11 +456,13 @@ def conv_panel_enabled():
     return os.environ.get("IVIT_CONV_PANEL", "1") != "0"
 
 
-def pack_conv_t(w, cdt):
-    """torch [Cout][Cin][k][k] -> the data gradient's K-contiguous weight [Cin][k][k][Cout], taps flipped."""
+def pack_conv_t(w, cdt, cout_pad=None):
+    """torch [Cout][Cin][k][k] -> the data gradient's K-contiguous weight [Cin][k][k][Cout_pad], taps
+    flipped, zero for channels >= Cout."""
     Cout, Cin, k, _ = w.shape
-    out = torch.empty((Cin, k, k, Cout), dtype=tdtype(cdt), device=w.device)
-    lib.ivit_pack_conv_weight_t(cdt, ptr(w), Cout, Cin, k, ptr(out), stream())
+    cp = Cout if cout_pad is None else cout_pad
+    out = torch.empty((Cin, k, k, cp), dtype=tdtype(cdt), device=w.device)
+    lib.ivit_pack_conv_weight_t(cdt, ptr(w), Cout, Cin, k, cp, ptr(out), stream())
     return out
 
 
@@ -483,18 +485,24 @@ def conv_bn_fwd(x, B, H, W, wp, cdt, out_dtype, rmean, rvar, training, momentum=
     return y, _BNState(mean, invstd)
 
 
-def conv_dgrad(dy, B, H, W, wp, cdt, out_dtype, w=None):
+def conv_dgrad(dy, B, H, W, wp, cdt, out_dtype, w=None, dy_zero_pad=False):
     """dX of a stride-1 'same' conv. With the f32 weight `w` (torch layout) and a bf16 shape the
     288 x 256 panel kernel takes (ivit_conv_dgrad_t: Cout % 64, Cin >= 128, >= 288 pixels), the
     tap-flipped transposed pack is built and the panel kernel runs; otherwise the 128 x 128 engine
-    on the forward pack `wp`."""
+    on the forward pack `wp`. dy_zero_pad: dy's rows hold zeros from channel w.shape[0] up to its
+    row stride, so the panel kernel may run on the channel count rounded up to 64 (the pack's extra
+    channels are zero too)."""
     Cout, k, _, Cin = wp.shape
     dx = torch.empty((B * H * W, Cin), dtype=out_dtype, device=dy.device)
-    if (w is not None and cdt == BF16 and conv_panel_enabled() and Cout % 64 == 0 and Cin >= 128 and Cin % 8 == 0
-            and B * H * W >= 288 and dy.stride(0) % 8 == 0 and wp.shape[0] == w.shape[0]):
-        wt = pack_conv_t(w, cdt)
-        lib.ivit_conv_dgrad_t(cdt, ptr(dy), dy.stride(0), B, H, W, Cout, ptr(wt), Cin, k, ptr(dx), dt(dx), stream())
-        return dx
+    if w is not None and cdt == BF16 and conv_panel_enabled():
+        Cw = w.shape[0]
+        cpad = (Cw + 63) // 64 * 64 if dy_zero_pad else Cw
+        if (cpad % 64 == 0 and cpad <= dy.stride(0) and Cw <= Cout and Cin >= 128 and Cin % 8 == 0
+                and B * H * W >= 288 and dy.stride(0) % 8 == 0):
+            wt = pack_conv_t(w, cdt, cout_pad=cpad)
+            lib.ivit_conv_dgrad_t(cdt, ptr(dy), dy.stride(0), B, H, W, cpad, ptr(wt), Cin, k, ptr(dx), dt(dx),
+                                  stream())
+            return dx
     lib.ivit_conv_dgrad(cdt, ptr(dy), dy.stride(0), B, H, W, Cout, ptr(wp), Cin, k, ptr(dx), dt(dx), stream())
     return dx
 
@@ -911,7 +919,7 @@ class NeckFn(torch.autograd.Function):
         box = torch.empty((B, M // B * A, 6), dtype=torch.float32, device=dev)
         intent = torch.empty((B, M // B * A, K), dtype=torch.float32, device=dev)
         lib.ivit_split_heads(ptr(hout), Cp, M, A, K, ptr(cls), ptr(box), ptr(intent), stream())
-        ctx.st = (saved, cat, pre, acts, bns, packs, whp, x, Cp)
+        ctx.st = (saved, cat, pre, acts, bns, packs, (whp, wh), x, Cp)
         ctx.meta = meta
         ctx.P = P
         return cls, box, intent
@@ -919,7 +927,7 @@ class NeckFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *gouts):
         (B, Hf, Wf, cdt, training, A, K, layers, names) = ctx.meta
-        saved, cat, pre, acts, bns, packs, whp, x_last, Cp = ctx.st
+        saved, cat, pre, acts, bns, packs, (whp, wh), x_last, Cp = ctx.st
         P = ctx.P
         cd = tdtype(cdt)
         Np = Hf * Wf
@@ -930,16 +938,19 @@ class NeckFn(torch.autograd.Function):
             dx = gouts[0].contiguous().float()
         else:
             dcls, dbox, dint = gouts
-            dh = torch.empty((M, Cp), dtype=cd, device=dev)
+            # rows zero-padded to a multiple of 64 channels: the head conv's data gradient then runs
+            # on the panel kernel; the weight gradient reads the first Cp
+            Cq = (Cp + 63) // 64 * 64
+            dh = torch.empty((M, Cq), dtype=cd, device=dev)
             lib.ivit_merge_heads_grad(ptr(dcls.contiguous()), ptr(dbox.contiguous()), ptr(dint.contiguous()), M, A,
-                                      K, ptr(dh), Cp, dt(dh), stream())
+                                      K, ptr(dh), Cq, dt(dh), stream())
             Cin = x_last.shape[1]
             gp, dbh = conv_wgrad(dh, x_last, B, Hf, Wf, Cin, Cp, 3, cdt, want_bias=True)
             Cd, Ci = A * 7, A * K
             gw = unpack_conv_grad(gp, Cd + Ci, Cin, 3)
             G["det_head.conv.weight"], G["intention_head.conv.weight"] = gw[:Cd], gw[Cd:]
             G["det_head.conv.bias"], G["intention_head.conv.bias"] = dbh[:Cd].clone(), dbh[Cd:Cd + Ci].clone()
-            dx = conv_dgrad(dh, B, Hf, Wf, whp, cdt, torch.float32)
+            dx = conv_dgrad(dh, B, Hf, Wf, whp, cdt, torch.float32, w=wh, dy_zero_pad=True)
         for li in reversed(range(layers)):
             p = f"fusion_block.{li}."
             x, c1, s1, r1, c2, s2, out = acts[li]
