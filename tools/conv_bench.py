@@ -61,6 +61,17 @@ def main():
         tp = timed(lambda: ops.conv_dgrad(dy, B, H, W, wp, BF16, torch.float32, w=w, dy_zero_pad=True))
         print(f"head {cin}->{cw} k3 dgrad: engine {te:7.1f} us ({fl / te / 1e6:6.1f} TF/s)  "
               f"panel(pad {cq}, +pack) {tp:7.1f} us ({fl / tp / 1e6:6.1f} TF/s)", flush=True)
+    # head forward and weight gradient: engine on 80 channels vs panel on 128
+    x = (torch.randn(M, cin, device=dev) * 0.5).bfloat16()
+    wq = ops.pack_conv(w, BF16, cout_pad=cq)
+    bp, bq = torch.zeros(cp, device=dev), torch.zeros(cq, device=dev)
+    for rep in range(2):
+        fe = timed(lambda: ops.conv_fwd(x, B, H, W, wp, bp, BF16, torch.float32))
+        fp = timed(lambda: ops.conv_fwd(x, B, H, W, wq, bq, BF16, torch.float32))
+        we = timed(lambda: ops.conv_wgrad(dy, x, B, H, W, cin, cp, 3, BF16, want_bias=True))
+        wq_ = timed(lambda: ops.conv_wgrad(dy, x, B, H, W, cin, cq, 3, BF16, want_bias=True))
+        print(f"head {cin}->{cw} k3 fwd: engine(80) {fe:7.1f} us  panel(128) {fp:7.1f} us   "
+              f"wgrad: engine(80) {we:7.1f} us  panel(128) {wq_:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":
