@@ -232,16 +232,20 @@ IVIT_DEV uint4 f32x8_to_bf16x8(float4 a, float4 b) {
 }
 
 // Column reduction of per-block partial sums: out[c] (+)= sum_b part[b * pstride + c].
-// 1024 threads = 64 columns x 16 partial phases, so long partial lists reduce in parallel.
-// Columns >= C0 go to out1[c - C0] (two outputs packed in one partial row, e.g. dgamma|dbeta).
+// 256 threads = 16 columns x 16 partial phases (phase ph sums rows ph, ph + 16, ...; the phases are
+// then added in order), so long partial lists reduce in parallel; narrow 4-wave workgroups, many of
+// them (C / 16), find room on CUs that the other ViT stream's kernels hold. Columns >= C0 go to
+// out1[c - C0] (two outputs packed in one partial row, e.g. dgamma|dbeta).
 namespace {
-__global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict__ part, int nb, long pstride, int C,
-                                                         float* out0, int C0, float* out1, int acc) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+constexpr int CR_COLS = 16;
+__global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict__ part, int nb, long pstride, int C,
+                                                        float* out0, int C0, float* out1, int acc) {
+  const int cl = threadIdx.x & (CR_COLS - 1), ph = threadIdx.x / CR_COLS;
+  const int c = blockIdx.x * CR_COLS + cl;
   float s = 0.f;
   if (c < C) {
     // the first 16 rows of this phase loaded at once (16 loads in flight per lane: the reduce is
-    // latency-bound on a dozen workgroups), summed in the same order as the sequential loop
+    // latency-bound), summed in the same order as the sequential loop
     float v[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -253,21 +257,21 @@ __global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict
       if (ph + 16 * i < nb) s += v[i];
     for (int b = ph + 256; b < nb; b += 16) s += part[(long)b * pstride + c];
   }
-  __shared__ float red[16][64];
-  red[ph][threadIdx.x & 63] = s;
+  __shared__ float red[16][CR_COLS];
+  red[ph][cl] = s;
   __syncthreads();
   if (ph == 0 && c < C) {
     float t = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) t += red[k][threadIdx.x];
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
     float* o = c < C0 ? (out0 ? out0 + c : nullptr) : (out1 ? out1 + (c - C0) : nullptr);
     if (o) *o = acc ? *o + t : t;
   }
 }
 inline void launch_colreduce(hipStream_t st, const float* part, int nb, long pstride, int C, float* out0, int C0,
                              float* out1, int acc) {
-  hipLaunchKernelGGL(colreduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, nb, pstride, C, out0, C0, out1,
-                     acc);
+  hipLaunchKernelGGL(colreduce_kernel, dim3((C + CR_COLS - 1) / CR_COLS), dim3(256), 0, st, part, nb, pstride, C,
+                     out0, C0, out1, acc);
 }
 }  // namespace
 
