@@ -356,7 +356,7 @@ def main():
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t)
-    loss_v = float(d["loss"])
+    loss_v = float(d["loss"].detach())
     gb = B * world
     value = gb * args.steps / el
     ms = el / args.steps * 1e3
