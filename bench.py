@@ -208,14 +208,25 @@ def cpu_baseline(steps=3):
             "step_s": med, "steps_s": [round(t, 3) for t in ts]}
 
 
-def launch_ranks(n):
-    """Start ranks 0..n-1 of this same command as child processes (torchrun's environment: RANK,
-    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1) and return the first non-zero
-    exit status (the others are stopped then), else 0. This process never initialises the GPU
-    (torch.cuda.device_count() does not, on this image)."""
+def visible_gpus():
+    """GPUs this process may use, counted without initialising HIP: torch.cuda.device_count() reads
+    the device count without creating a context on this image — checked here, because the parent
+    of the rank processes must never touch the GPU (it would be forked / exec'd around a live
+    context)."""
+    n = torch.cuda.device_count()
+    if torch.cuda.is_initialized():
+        raise RuntimeError("bench.py: counting GPUs initialised HIP in the launcher process")
+    return n
+
+
+def launch_ranks(n, argv=None, have=None, poll_s=0.2):
+    """Start ranks 0..n-1 of this same command (or ``argv``) as child processes with torchrun's
+    environment (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1) and return
+    the first non-zero exit status (the other ranks are terminated then), else 0. ``have``: the
+    visible GPU count (default visible_gpus()); fewer than n is refused with status 2."""
     import socket
     import subprocess
-    have = torch.cuda.device_count()
+    have = visible_gpus() if have is None else have
     if have < n:
         print(f"bench.py: --gpus {n} needs {n} GPUs, {have} visible", file=sys.stderr, flush=True)
         return 2
@@ -223,11 +234,12 @@ def launch_ranks(n):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    argv = argv if argv is not None else [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        procs.append(subprocess.Popen(argv, env=env))
     rc = 0
     live = list(procs)
     while live:
@@ -240,8 +252,41 @@ def launch_ranks(n):
                 rc = c
                 for q in live:
                     q.terminate()
-        time.sleep(0.2)
+        time.sleep(poll_s)
     return rc
+
+
+def time_forced_buckets(model, opt, lf, anchors, batch, args, plain_ms):
+    """The DDP leg of configs 3 / 5 on one GPU: the same step through Trainer(force_buckets=True)
+    on a world-1 RCCL process group — every gradient a view into the 64-MB buckets, one event per
+    parameter on its producing ViT stream, the bucket all-reduces on the comm stream overlapping
+    backward, finish() waiting — timed exactly as the plain step, right after it."""
+    from trainer import Trainer
+    tr = Trainer(model, lf, opt, anchors, world=1, bucket_mb=args.bucket_mb, check_nan=False, force_buckets=True)
+    if tr.buckets is None or not tr.buckets.active:
+        raise RuntimeError("--force-collectives: the bucketed collective path is not active")
+    import ddp
+    n0 = ddp.GradBuckets.launched
+    for _ in range(args.warmup):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    per_step = (ddp.GradBuckets.launched - n0) / (args.warmup + args.steps)
+    ms = el / args.steps * 1e3
+    tr.buckets.remove()
+    return {"backend": dist.get_backend(), "world": dist.get_world_size(), "buckets": len(tr.buckets.buckets),
+            "bucket_mb": args.bucket_mb, "grad_mb": round(tr.buckets.numel * 4 / 2 ** 20, 1),
+            "all_reduces_per_step": per_step, "ms_per_step_buckets": round(ms, 3),
+            "ms_per_step_plain": round(plain_ms, 3), "overhead_ms": round(ms - plain_ms, 3),
+            "note": "same process, same batch, timed right after the plain step (which is `value`): "
+                    "Trainer(force_buckets=True) on a world-1 RCCL group, so every bucket is all-reduced "
+                    "(a world-1 ring moves no bytes over xGMI; this is the launch / stream / event cost "
+                    "of the DDP path inside the step)"}
 
 
 def main():
@@ -261,6 +306,10 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=64)
     ap.add_argument("--ddp", choices=["buckets", "torch"], default="buckets",
                     help="gradient exchange: ddp.GradBuckets (default) or torch DistributedDataParallel")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="N=1 train mode: also time the bucketed RCCL path (a world-1 process group, "
+                         "Trainer(force_buckets=True): comm stream, per-parameter events, the all-reduces) "
+                         "right after the plain step in the same process; both go into the line")
     args = ap.parse_args()
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
@@ -271,7 +320,19 @@ def main():
 
     sys.path.insert(0, PKG)
     from ddp import init_distributed
-    rank, local, world, dev = init_distributed()
+    force = args.force_collectives and args.gpus == 1 and args.mode == "train"
+    if force:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            import socket
+            so = socket.socket()
+            so.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(so.getsockname()[1])
+            so.close()
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("LOCAL_RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    rank, local, world, dev = init_distributed(force_group=force)
     if dev.type != "cuda":
         raise RuntimeError("bench.py needs a ROCm GPU (the HIP kernels have no CPU path)")
     world = dist.get_world_size() if dist.is_initialized() else 1
@@ -432,6 +493,8 @@ def main():
                                        "frac": round(afl / (iso * 1e-3) / 1e12 / peak, 4),
                                        "note": "mean of 20 back-to-back launches on random bf16 inputs of the "
                                                "bench shape (prescaled Q), HIP events, nothing else running"}
+    if force:
+        out["collectives_world1"] = time_forced_buckets(model, opt, lf, anchors, batch, args, ms)
     if train:
         out["loss"] = loss_v
     else:
@@ -440,7 +503,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

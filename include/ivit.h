@@ -282,17 +282,16 @@ int ivit_adamw_shadow(long n_tensors, void* const* params, void* const* grads, v
                       void* const* exp_avg_sq, void* const* shadows, const long* sizes, long max_size, float lr,
                       float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2_sqrt,
                       void* stream);
-/* Same update with up to three bf16 outputs per tensor: outs[3t] the shadow, outs[3t+1] the
- * row-panel pack of W [rows][cols[t]] (ivit_patch_weight_pack layout), outs[3t+2] the pack of
- * W^T (ivit_weight_pack_t layout); any may be null. A tensor with a pack needs rows % 32 == 0
- * and cols % 32 == 0 (it is walked in 8 x 8 tiles: max_work >= n / 64 for it, >= n otherwise).
- * finite (device f32, may be null): 0 skips the whole update — the train_vit.py:163-165 /
- * loss.py:190-198 non-finite-loss step without a host sync. tiled = 0: no tensor of the set has a
- * pack (outs[3t+1], outs[3t+2] ignored; a light streaming kernel), 1: some may. */
-int ivit_adamw_packed(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
-                      void* const* exp_avg_sq, void* const* outs, const long* cols, const long* sizes,
-                      long max_work, float lr, float beta1, float beta2, float eps, float weight_decay, float bc1,
-                      float bc2_sqrt, const float* finite, int tiled, void* stream);
+/* Same update (shadows may be null, or null per tensor) with the non-finite-loss guard of
+ * train_vit.py:163-165 / loss.py:190-198 without a host sync: finite (device f32, may be null) = 0
+ * skips the whole update. steps_in / steps_out (device f32 [n_tensors], both null or both set,
+ * distinct): per-tensor step counts before / after; when set, bc1 / bc2_sqrt are ignored and come
+ * from steps_in[t] + 1 in f64 with beta1 / beta2, and a skipped update does not advance the count
+ * (torch.optim.AdamW's state['step'] when the reference's disconnected zero loss leaves no grad). */
+int ivit_adamw_guarded(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
+                       void* const* exp_avg_sq, void* const* shadows, const long* sizes, long max_size, float lr,
+                       double beta1, double beta2, float eps, float weight_decay, float bc1, float bc2_sqrt,
+                       const float* finite, const float* steps_in, float* steps_out, void* stream);
 
 /* ---- Detection / intention loss (loss.py:58-206): assignment + focal + Smooth-L1 + CE. ----- */
 /* gt: [B, Gmax, 5] f32 padded, ngt[B] int32, gint[B, Gmax] int32. keep: [B, NA] f32 0/1 (dominant

@@ -588,6 +588,36 @@ def gen_cnn_small():
     print("cnn_small: params", sum(int(np.prod(s)) for _, s in keys), "loss", rec["train_loss"])
 
 
+def gen_ap():
+    """The reference's OWN calculate_ap (utils.py:564-575) on the recall / precision steps that
+    eval_vit.py:249-255 builds from a TP-flag sequence (torch f32 cumsum, / (num_gt + 1e-9),
+    / (arange + 1e-9)): seeded random walks, all-TP, all-FP, a single TP / FP, long FP runs (recall
+    plateaus: tied recall values), a late-TP tail and the empty array pair."""
+    import utils as ref_utils
+    rng = np.random.default_rng(2468)
+    cases = [(np.zeros(0, bool), 5), (np.ones(5, bool), 5), (np.zeros(6, bool), 3), (np.ones(1, bool), 1),
+             (np.zeros(1, bool), 1), (np.array([0, 0, 0, 1, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 1], bool), 4),
+             (np.array([1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1], bool), 7)]
+    for P, G, p_tp in ((50, 10, 0.2), (300, 25, 0.05), (700, 40, 0.04), (2000, 60, 0.02), (64, 64, 0.9)):
+        tp = rng.random(P) < p_tp
+        while tp.sum() > G:  # a GT is matched at most once
+            tp[np.nonzero(tp)[0][-1]] = False
+        cases.append((tp, G))
+    rec = {"n_cases": np.array([len(cases)])}
+    for k, (tp, G) in enumerate(cases):
+        t = torch.from_numpy(tp)
+        cum = torch.cumsum(t.float(), dim=0)
+        recall = cum / (G + 1e-9)
+        precision = cum / (torch.arange(1, t.numel() + 1).float() + 1e-9)
+        rec[f"c{k}_tp"] = tp
+        rec[f"c{k}_ngt"] = np.array([G])
+        rec[f"c{k}_recall"] = recall.numpy()
+        rec[f"c{k}_precision"] = precision.numpy()
+        rec[f"c{k}_ap"] = np.array([ref_utils.calculate_ap(recall.numpy(), precision.numpy())])
+    np.savez_compressed(os.path.join(OUT, "ap_reference.npz"), **rec)
+    print("ap_reference:", [float(rec[f"c{k}_ap"][0]) for k in range(len(cases))])
+
+
 def cross_check_vit():
     """HF ViTModel (stand-in) vs the oracle's timm restatement, 12 blocks, real widths."""
     cfg = model_cfg(img_size=SMALL_IMG)
@@ -625,3 +655,4 @@ if __name__ == "__main__":
     gen_map_raster()
     gen_model_stride2()
     gen_model_regrid()
+    gen_ap()

@@ -63,7 +63,7 @@ def test_workspace_queries_are_pure_host():
     dll = _lib.lib.load()
     B, N, H = 8, 4501, 6
     npad = (N + 63) // 64 * 64  # lse2 + delta rows, padded to the 64-row tile
-    assert dll.ivit_attn_workspace(_lib.BF16, B, N, H, 64, 1) == 6 * B * H * npad * 4
+    assert dll.ivit_attn_workspace(_lib.BF16, B, N, H, 64, 1) == 2 * B * H * npad * 4
     assert dll.ivit_attn_workspace(_lib.BF16, B, N, H, 64, 0) == 0
     assert dll.ivit_nms_workspace(22500) > 0
 

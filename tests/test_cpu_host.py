@@ -95,6 +95,28 @@ def test_calculate_ap_known_values():
     assert calculate_ap(np.array([0.0, 0.5]), np.array([0.0, 0.5])) == pytest.approx(0.25)
 
 
+def _ap_cases():
+    from conftest import golden
+    z = golden("ap_reference.npz")
+    return z, int(z["n_cases"][0])
+
+
+def test_calculate_ap_vs_reference_fixture():
+    """The build's calculate_ap and metrics' recall / precision steps vs the reference's OWN
+    utils.calculate_ap (utils.py:564-575) on eval_vit.py:249-255's steps (tests/golden/ap_reference.npz,
+    oracle/make_golden.py gen_ap): empty, all-TP, all-FP, single TP / FP, tied recall plateaus,
+    seeded walks up to 2000 predictions."""
+    z, n = _ap_cases()
+    for k in range(n):
+        tp, G = z[f"c{k}_tp"], int(z[f"c{k}_ngt"][0])
+        cum = np.cumsum(tp.astype(np.float32))  # metrics.detection_map's steps
+        rec = cum / (G + 1e-9)
+        prec = cum / (np.arange(1, tp.size + 1, dtype=np.float32) + 1e-9)
+        np.testing.assert_array_equal(rec, z[f"c{k}_recall"])
+        np.testing.assert_array_equal(prec, z[f"c{k}_precision"])
+        assert calculate_ap(z[f"c{k}_recall"], z[f"c{k}_precision"]) == float(z[f"c{k}_ap"][0]), k
+
+
 def test_synthetic_batch_format_and_ranges():
     b = synthetic.synthetic_batch(2, (32, 48), torch.Generator().manual_seed(1234))
     assert b["lidar_bev"].shape == (2, 290, 32, 48) and b["lidar_bev"].dtype == torch.float32

@@ -25,7 +25,7 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, H, W, q):
+def _worker(rank, world, port, H, W, B, q):
     try:
         import torch.distributed as dist
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
@@ -52,10 +52,10 @@ def _worker(rank, world, port, H, W, q):
             m.load_state_dict(sd, strict=True)
             return m.cuda().set_compute_dtype(torch.bfloat16).train()
 
-        lidar, mp_, gts = O.synthetic_batch(2, (H, W), seed=100 + rank, grid_scale=H / 400.0)
+        lidar, mp_, gts = O.synthetic_batch(B, (H, W), seed=100 + rank, grid_scale=H / 400.0)
         lidar, mp_ = lidar.cuda(), mp_.cuda()
         anchors = utils.generate_anchors(H, W, 8, device="cuda")
-        keep = (torch.rand((2, anchors.shape[0]), generator=torch.Generator().manual_seed(7 + rank)) < 0.15).float()
+        keep = (torch.rand((B, anchors.shape[0]), generator=torch.Generator().manual_seed(7 + rank)) < 0.15).float()
         lossf = L.DetectionIntentionLoss()
 
         def grads(m):
@@ -100,12 +100,14 @@ def _worker(rank, world, port, H, W, q):
         q.put((rank, None, None, None, repr(e)))
 
 
-@pytest.mark.parametrize("H,W", [(64, 96), (400, 720)])
-def test_ddp_two_ranks_bf16_model_on_gpu(H, W):
+@pytest.mark.parametrize("H,W,B", [(64, 96, 2), (400, 720, 2), (800, 1440, 1)])
+def test_ddp_two_ranks_bf16_model_on_gpu(H, W, B):
+    """(800, 1440, 1) is BASELINE config 5's per-rank workload (2x grid, N = 18 001 tokens per ViT
+    stream) through GradBuckets + Trainer."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, H, W, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, H, W, B, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]

@@ -89,7 +89,7 @@ def test_loss_guard_vs_golden(case):
     z = golden("loss_options.npz")
     anchors = utils.generate_anchors(*(int(v) for v in z["rot_grid"]), 8)
     ts = [t.to(DEV).requires_grad_(True) for t in _poisoned(z, case)]
-    lf = L.DetectionIntentionLoss(apply_intention_downsampling=False)
+    lf = L.DetectionIntentionLoss(apply_intention_downsampling=False, sync_guard=False)
     d = lf(*ts, anchors, _gts(z, "rot"))
     np.testing.assert_array_equal(_vec(d), z[f"guard_{case}_loss"])
     assert float(lf.last_finite) == 0.0
@@ -149,3 +149,69 @@ def test_train_step_guard_leaves_weights_bit_identical():
         for k, v in opt.state[p].items():
             ref = s0[id(p)][k]
             assert (torch.equal(v, ref) if torch.is_tensor(v) else v == ref), k
+
+
+@pytest.mark.parametrize("case", ["nan_cls", "inf_int_pos"])
+def test_loss_sync_guard_reference_contract(case, capsys):
+    """sync_guard (the default outside Trainer): loss.py:190-206 exactly — a disconnected
+    requires_grad zero leaf, zero terms, num_pos_anchors a Python int, the reference's message."""
+    import loss as L
+    import utils
+    z = golden("loss_options.npz")
+    anchors = utils.generate_anchors(*(int(v) for v in z["rot_grid"]), 8)
+    ts = [t.to(DEV).requires_grad_(True) for t in _poisoned(z, case)]
+    d = L.DetectionIntentionLoss(apply_intention_downsampling=False)(*ts, anchors, _gts(z, "rot"))
+    np.testing.assert_array_equal(_vec(d), z[f"guard_{case}_loss"])
+    assert type(d["num_pos_anchors"]) is int
+    assert d["loss"].is_leaf and d["loss"].requires_grad and d["loss"].grad_fn is None
+    assert "NaN or Inf DETECTED IN LOSS!" in capsys.readouterr().out
+    d["loss"].backward()
+    for t in ts:
+        assert t.grad is None
+    # finite inputs: the connected loss, num_pos still an int
+    d = L.DetectionIntentionLoss(apply_intention_downsampling=False)(
+        *[torch.from_numpy(z[k]).to(DEV) for k in ("rot_cls", "rot_box", "rot_int")], anchors, _gts(z, "rot"))
+    assert type(d["num_pos_anchors"]) is int and d["num_pos_anchors"] == int(z["rot_axis_loss"][4])
+
+
+def test_reference_loop_guard_leaves_weights_and_adamw_bit_identical():
+    """The reference's own loop (train_vit.py:151-187: zero_grad(set_to_none) → forward → loss →
+    loss.backward() → torch.optim.AdamW.step()) on an injected non-finite loss: the default
+    sync_guard returns the disconnected leaf, no parameter gets a .grad, and torch AdamW updates
+    nothing — weights, exp_avg / exp_avg_sq and step counts bit-identical."""
+    import model_vit
+    import utils
+    from oracle import ivit_oracle as O
+    cfg = model_cfg(img_size=(32, 48))
+    m = model_vit.IntentNetViT(backbone_cfg={"img_size": (32, 48)})
+    m.load_state_dict(make_state_dict(cfg, seed=0), strict=True)
+    m = m.to(DEV).set_compute_dtype(torch.bfloat16).train()
+    lidar, mp, gts = O.synthetic_batch(2, (32, 48), seed=1234, box_region=(54.0, 60.0, -72.0, -62.0))
+    lidar, mp = lidar.to(DEV), mp.to(DEV)
+    anchors = utils.generate_anchors(32, 48, 8, device=DEV)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    lf = _PoisonLoss(1)
+
+    def ref_step(loss_fn):
+        opt.zero_grad(set_to_none=True)
+        c, b, i = m(lidar, mp)
+        d = loss_fn(c, b, i, anchors, gts)
+        d["loss"].backward()
+        opt.step()
+        return d
+
+    d = ref_step(lf.inner)  # a normal step first: Adam state exists
+    assert float(d["loss"]) > 0 and type(d["num_pos_anchors"]) is int
+    w0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    s0 = {id(p): {k: v.clone() for k, v in opt.state[p].items()} for p in m.parameters()}
+    d = ref_step(lf)
+    torch.cuda.synchronize()
+    assert float(d["loss"]) == 0.0
+    assert all(p.grad is None for p in m.parameters())
+    for k, v in m.state_dict().items():
+        if "num_batches_tracked" in k or "running_" in k:
+            continue  # BN statistics move in the forward, as in the reference
+        assert torch.equal(v, w0[k]), k
+    for p in m.parameters():
+        for k, v in opt.state[p].items():
+            assert torch.equal(v, s0[id(p)][k]), k

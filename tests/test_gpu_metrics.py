@@ -101,3 +101,48 @@ def test_det_match_agrees_with_host_vectorised_path():
     dev = metrics.detection_map_device(res, THR)
     for thr in THR:
         assert dev[thr] == pytest.approx(host[thr], abs=1e-12)
+
+
+def test_det_match_ap_vs_reference_fixture():
+    """ivit_det_match's AP vs the reference's OWN calculate_ap (tests/golden/ap_reference.npz): each
+    case's TP sequence is laid out as a score-ordered IoU matrix (a TP row: 0.95 with the next
+    unmatched GT, 0 elsewhere; an FP row: 0.1 everywhere), all cases in one launch."""
+    from conftest import golden
+    from _lib import lib, ptr, stream, workspace
+    z = golden("ap_reference.npz")
+    n = int(z["n_cases"][0])
+    mats, npred, ngt = [], [], []
+    for k in range(n):
+        tp, G = z[f"c{k}_tp"], int(z[f"c{k}_ngt"][0])
+        m = np.full((tp.size, G), 0.1, np.float32)
+        j = 0
+        for r in np.nonzero(tp)[0]:
+            m[r] = 0.0
+            m[r, j] = 0.95
+            j += 1
+        mats.append(m.reshape(-1))
+        npred.append(tp.size)
+        ngt.append(G)
+    sizes = [p * g for p, g in zip(npred, ngt)]
+    iou = torch.from_numpy(np.concatenate(mats)).cuda()
+    iou_off = torch.from_numpy(np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)).cuda()
+    pred_off_np = np.concatenate([[0], np.cumsum(npred)[:-1]]).astype(np.int64)
+    pred_off = torch.from_numpy(pred_off_np).cuda()
+    d_np = torch.tensor(npred, dtype=torch.int32).cuda()
+    d_ng = torch.tensor(ngt, dtype=torch.int32).cuda()
+    thr = torch.tensor([0.5], dtype=torch.float32).cuda()
+    tot = int(sum(npred))
+    ap = torch.empty((n, 1), dtype=torch.float64, device="cuda")
+    best = torch.empty(tot, dtype=torch.int32, device="cuda")
+    tpo = torch.empty((1, tot), dtype=torch.uint8, device="cuda")
+    ws = workspace(8 * tot, torch.device("cuda"))
+    lib.ivit_det_match(ptr(iou), ptr(iou_off), ptr(d_np), ptr(d_ng), ptr(pred_off), n, tot, ptr(thr), 1, ptr(ap),
+                       ptr(best), ptr(tpo), ptr(ws), ws.numel(), max(ngt), stream())
+    ap = ap.cpu().numpy()[:, 0]
+    tpo = tpo.cpu().numpy()[0].astype(bool)
+    for k in range(n):
+        tp = z[f"c{k}_tp"]
+        np.testing.assert_array_equal(tpo[pred_off_np[k]:pred_off_np[k] + tp.size], tp)
+        # P == 0 is the eval flow's own case (eval_vit.py:210-212: 1.0 / 0.0, calculate_ap not called)
+        want = (1.0 if ngt[k] == 0 else 0.0) if tp.size == 0 else float(z[f"c{k}_ap"][0])
+        assert abs(ap[k] - want) < 1e-12, (k, ap[k], want)

@@ -712,8 +712,40 @@ def test_adamw_matches_torch():
         assert _rel(q.detach(), p.detach()) < 1e-6
 
 
+def test_adamw_device_guard_skips_step_count():
+    """The sync-free guard path (Trainer with check_nan=False: step(finite=flag)): a finite = 0
+    update changes nothing — weights, moments AND step counts — so the following updates match
+    torch.optim.AdamW with that step never taken (bias correction included)."""
+    from optim import FusedAdamW
+    ps = [torch.randn(1000), torch.randn(37, 5)]
+    gs = [[torch.randn_like(p) for p in ps] for _ in range(4)]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    dev = [p.clone().to(DEV).requires_grad_(True) for p in ps]
+    o1 = torch.optim.AdamW(ref, lr=1e-3, weight_decay=1e-2)
+    o2 = FusedAdamW(dev, lr=1e-3, weight_decay=1e-2)
+    one, zero = torch.ones((), device=DEV), torch.zeros((), device=DEV)
+    for k, step in enumerate(gs):
+        skip = k == 1
+        for p, q, g in zip(ref, dev, step):
+            p.grad = None if skip else g.clone()
+            q.grad = g.clone().to(DEV)
+        if skip:
+            before = [q.detach().clone() for q in dev]
+            o2.step(finite=zero)
+            assert all(torch.equal(q.detach(), b) for q, b in zip(dev, before))
+        else:
+            o1.step()
+            o2.step(finite=one)
+    for p, q in zip(ref, dev):
+        assert float(o2.state[q]["step"]) == 3.0 and float(o1.state[p]["step"]) == 3.0
+        assert _rel(q.detach(), p.detach()) < 1e-6
+        assert _rel(o2.state[q]["exp_avg_sq"], o1.state[p]["exp_avg_sq"]) < 1e-6
+    o2.step()  # the host path continues from the device counts
+    assert all(o2.state[q]["step"] == 4 for q in dev)
+
+
 def test_adamw_refreshes_bf16_weight_shadows():
-    """ops.cast_weight's cached bf16 copy is rewritten by the AdamW launch (ivit_adamw_shadow),
+    """ops.cast_weight's cached bf16 copy is rewritten by the AdamW launch (ivit_adamw_guarded),
     so after every step it equals bf16(p) exactly; a parameter without a shadow is unaffected."""
     import ops
     from optim import FusedAdamW
@@ -758,9 +790,9 @@ def test_vit_block_wgrad_grouped(M):
 
 
 def test_adamw_packs_unaligned_grads():
-    """ivit_adamw_packed on a packed weight whose gradient is a view at a 4-B (not 16-B) offset (a
-    DDP bucket view): the scalar-access path gives the same update as torch.optim.AdamW and packs
-    equal to freshly built ones."""
+    """FusedAdamW (ivit_adamw_guarded + ivit_weight_pack_multi) on a packed weight whose gradient
+    is a view at a 4-B (not 16-B) offset (a DDP bucket view): the same update as
+    torch.optim.AdamW and packs equal to freshly built ones."""
     import ops
     from optim import FusedAdamW
     p = torch.randn(384, 1536, device=DEV, requires_grad=True)

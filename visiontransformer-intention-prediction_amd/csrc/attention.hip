@@ -154,9 +154,7 @@ IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8
 
 // PRE: prescale Q by c2 in the kernel (ivit_attn_fwd, plain qkv); otherwise the Q block of qkv
 // already holds q * c2 (ivit_attn_fwd_q2).
-// AN (anatomy builds, IVIT_ATTN_AN): 0 product, 1 no K/V DMA after the prologue (compute on stale
-// stages), 2 DMA / barrier skeleton only (no tile compute).
-template <int W, bool PRE, int AN = 0>
+template <int W, bool PRE>
 __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const bf16* __restrict__ qkv, int N, int H,
                                                                         bf16* __restrict__ out,
                                                                         float* __restrict__ lse, float c2) {
@@ -248,10 +246,9 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
     constexpr int S = decltype(stage)::value;  // V_j in smem[S][1], K_{j+1} in smem[S^1][0]
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (AN != 1 && j + 2 < nt) issue1(Kb, j + 2, smem[S][0]);
-    if (AN != 1 && j + 1 < nt) issue1(Vb, j + 1, smem[S ^ 1][1]);
-    if (AN != 2)
-      rescale(fwd_step_fenced6(smem[S ^ 1][0], smem[S][1], qf, cur, nxt, o0, o1, lacc, ones, negm, lane,
+    if (j + 2 < nt) issue1(Kb, j + 2, smem[S][0]);
+    if (j + 1 < nt) issue1(Vb, j + 1, smem[S ^ 1][1]);
+    rescale(fwd_step_fenced6(smem[S ^ 1][0], smem[S][1], qf, cur, nxt, o0, o1, lacc, ones, negm, lane,
                                (j + 1) * AK, N),
               nxt);
   };
@@ -595,19 +592,14 @@ constexpr int BNS = 3;  // LDS stages of the v3 backward kernels
 // negated row constants (-lse2, -delta; padded rows -1e30 / 0, so P = 0 there, no mask).
 // (W = 8, one 512-thread workgroup per CU sharing each Q / dO tile, halves the L2 -> LDS bytes
 // but measured slower; the product uses W = 4.)
-// XR: the row constants arrive as exact bf16 triples (split3_bf16, written by the dQ kernel) and
-// enter each S / dP chain through one extra MFMA, [hi mid lo 0 ..] x [1 1 1 0 ..]^T, from a zero
-// accumulator: per 32-query unit two ds_read_b64 instead of eight ds_read_b128 of f32 row
-// vectors (a third of the unit's LDS-array cycles), for two more MFMAs.
-template <int W, bool XR = false>
+template <int W>
 __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ nlse2p,
                                                                  const float* __restrict__ ndeltap, int N, int Npad,
                                                                  int H, bf16* __restrict__ dqkv, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][Q|dO]
-  constexpr int RW = XR ? 2 : 1;  // words per row constant
-  __shared__ __attribute__((aligned(16))) float srow[BNS][2][RW * AK];  // [stage][-lse2|-delta]
+  __shared__ __attribute__((aligned(16))) float srow[BNS][2][AK];  // [stage][-lse2|-delta]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int2 bid = attn_block_id();
@@ -618,8 +610,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
   const bf16* Kb = Qb + D;
   const bf16* Vb = Qb + 2 * D;
   const bf16* Gb = dout + (long)b * N * D + h * 64;
-  const char* Ls = uniform_ptr(nlse2p + (long)RW * z * Npad);
-  const char* Ds = uniform_ptr(ndeltap + (long)RW * z * Npad);
+  const char* Ls = uniform_ptr(nlse2p + (long)z * Npad);
+  const char* Ds = uniform_ptr(ndeltap + (long)z * Npad);
   constexpr int PW = 8 / W;  // DMA pieces per wave per 8-KiB tile image
   const int key = bid.x * (32 * W) + wv * 32 + (lane & 31);
   bf16x8 kf[4], vf[4];
@@ -655,11 +647,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
       glds_s<false>(og, gb, gimg + piece * 1024);
     }
     if (wv == 0) {  // bases in SGPRs, the tile offset in the per-lane offset
-#pragma unroll
-      for (int i = 0; i < RW; ++i) {
-        glds4_s(4u * (lane + (RW * qt + i) * AK), Ls, &srow[S][0][i * AK]);
-        glds4_s(4u * (lane + (RW * qt + i) * AK), Ds, &srow[S][1][i * AK]);
-      }
+      glds4_s(4u * (lane + qt * AK), Ls, &srow[S][0][0]);
+      glds4_s(4u * (lane + qt * AK), Ds, &srow[S][1][0]);
     }
   };
 
@@ -677,15 +666,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
     const float4 d4 = *(const float4*)(dr + 32 * t + 8 * part + 4 * hl);
     sn[4 * part] = l4.x; sn[4 * part + 1] = l4.y; sn[4 * part + 2] = l4.z; sn[4 * part + 3] = l4.w;
     dn[4 * part] = d4.x; dn[4 * part + 1] = d4.y; dn[4 * part + 2] = d4.z; dn[4 * part + 3] = d4.w;
-  };
-  // XR operands: A = this lane's query row pair in k 0..1 (lanes >= 32 hold k 8..15, multiplied by
-  // B's zero rows), B = (1, 1) in k 0..1 of every key column
-  uint2 xl = make_uint2(0, 0), xd = make_uint2(0, 0);
-  const bf16x8 xb =
-      __builtin_bit_cast(bf16x8, make_uint4(hl ? 0u : pk_bf16(1.f, 1.f), hl ? 0u : pk_bf16(1.f, 0.f), 0u, 0u));
-  auto read_xrows = [&](const float* lr, const float* dr, int t) {
-    xl = *(const uint2*)(lr + 2 * (32 * t + (lane & 31)));
-    xd = *(const uint2*)(dr + 2 * (32 * t + (lane & 31)));
   };
   unsigned up[8], ud[8];  // packed P / dS of the pending B (words 4ss..4ss+3: 16-row half ss)
   bf16x8 tg0[2], tg1[2], tq0[2], tq1[2];
@@ -711,16 +691,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
     constexpr int SA = decltype(sa)::value, TA = decltype(ta)::value, SB = decltype(sb)::value;
     constexpr int TB = decltype(tb)::value, SN = decltype(sn_)::value, TN = decltype(tn)::value;
     constexpr bool BAR = decltype(bar)::value;
-    f32x16 s, dp;
-    if constexpr (XR) {
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, make_uint4(xl.x, xl.y, 0u, 0u)), xb,
-                                                  zero16(), 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, make_uint4(xd.x, xd.y, 0u, 0u)), xb,
-                                                   zero16(), 0, 0, 0);
-    } else {
-      s = sn;
-      dp = dn;
-    }
+    f32x16 s = sn, dp = dn;
 #pragma unroll
     for (int g = 0; g < 8; ++g) {
       const int ks = g >> 1;
@@ -747,11 +718,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
         default: dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq1[ss], dk1, 0, 0, 0); break;
       }
       if (more) {
-        if constexpr (XR) {
-          if (g == 3) read_xrows(srow[SN][0], srow[SN][1], TN);
-        } else if (g & 1) {
-          read_rows(srow[SN][0], srow[SN][1], TN, g >> 1);
-        }
+        if (g & 1) read_rows(srow[SN][0], srow[SN][1], TN, g >> 1);
         if (g == 6) read_frag(smem[SN][0], smem[SN][1], TN, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -775,12 +742,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  if constexpr (XR) {
-    read_xrows(srow[0][0], srow[0][1], 0);
-  } else {
 #pragma unroll
-    for (int part = 0; part < 4; ++part) read_rows(srow[0][0], srow[0][1], 0, part);
-  }
+  for (int part = 0; part < 4; ++part) read_rows(srow[0][0], srow[0][1], 0, part);
   read_frag(smem[0][0], smem[0][1], 0, 0);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -834,262 +797,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
   }
 }
 
-// ------------------------------------------------------------------------- backward v4 dK/dV
-// v3's pipeline with 64 keys per wave (two 32-key blocks kb), one wave per SIMD (4 waves = 256
-// keys per workgroup, one workgroup per CU): every Q / dO fragment read from LDS feeds two S / dP
-// MFMAs and every transposed fragment two dV / dK MFMAs (half v3's LDS reads per MFMA), and one
-// 16-KiB Q / dO tile serves 256 keys instead of 128 (half the LDS-DMA per flop). Per unit of 32
-// queries: 16 chain MFMAs (S, dP of both key blocks) beside 32 exp / 32 mul / 32 cvt of the
-// previous unit, then 16 product MFMAs (dV, dK of both blocks) beside the next unit's reads.
-// MFMAs as inline asm, so the register file is split as the v4 kernels need it: the dK / dV
-// accumulators pinned to AGPRs ("a"), the S / dP chains in VGPRs ("v") where the softmax VALU
-// reads them. (With the builtins the compiler put the chains in AGPRs too and copied them out:
-// ~1500 v_accvgpr moves and a scratch spill.) hipcc pads no hazard inside an asm statement
-// (cdna_hip_programming.md 5.7): accumulate chains need none; a chain's first MFMA takes its
-// initial accumulator C from registers written by LDS reads a phase earlier; every VALU read of a
-// chain result is at least a 16-MFMA phase later; the AGPR accumulators are read once, after
-// asm_mfma_drain().
-IVIT_DEV void mfma_acc_a(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-// chain MFMAs: B operand (the wave's K / V fragments, loaded once) from AGPRs
-IVIT_DEV void mfma_acc_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
-}
-IVIT_DEV f32x16 mfma_init_v(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  f32x16 d;
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(d) : "v"(a), "a"(b), "v"(c));
-  return d;
-}
-IVIT_DEV void asm_mfma_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory"); }
-
-template <int W>
-__global__ __launch_bounds__(64 * W, 1) void attn_bwd_dkv_v4_kernel(const bf16* __restrict__ qkv,
-                                                             const bf16* __restrict__ dout,
-                                                             const float* __restrict__ nlse2p,
-                                                             const float* __restrict__ ndeltap, int N, int Npad,
-                                                             int H, bf16* __restrict__ dqkv, float scale) {
-  constexpr int KB = 2;  // 32-key blocks per wave
-  __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][Q|dO]
-  __shared__ __attribute__((aligned(16))) float srow[BNS][2][AK];    // [stage][-lse2|-delta]
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int2 bid = attn_block_id();
-  const int z = bid.y, b = z / H, h = z - b * H;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
-  const bf16* Gb = dout + (long)b * N * D + h * 64;
-  const char* Ls = uniform_ptr(nlse2p + (long)z * Npad);
-  const char* Ds = uniform_ptr(ndeltap + (long)z * Npad);
-  constexpr int PW = 8 / W;  // DMA pieces per wave per 8-KiB tile image
-  const int kw0 = bid.x * (64 * W) + wv * 64;
-  bf16x8 kf[KB][4], vf[KB][4];
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    const int key = kw0 + 32 * kb + (lane & 31);
-    load_row_frags(Kb + (long)key * ld, key < N, lane, kf[kb]);
-    load_row_frags(Vb + (long)key * ld, key < N, lane, vf[kb]);
-    retire_loads(kf[kb], vf[kb]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) asm volatile("" : "+a"(kf[kb][i]), "+a"(vf[kb][i]));  // home: AGPRs
-  }
-  f32x16 dk0[KB], dk1[KB], dv0[KB], dv1[KB];
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) dk0[kb] = dk1[kb] = dv0[kb] = dv1[kb] = zero16();
-  const int nt = (N + AK - 1) / AK, nfull = N / AK;
-  unsigned offq[PW], offg[PW];
-#pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    offq[i] = 2u * dma_off<W>(i, wv, lane, ld);
-    offg[i] = 2u * dma_off<W>(i, wv, lane, D);
-  }
-  auto issue = [&](int qt, int S) {
-    char* qimg = smem[S][0];
-    char* gimg = smem[S][1];
-    const char* qb = uniform_ptr(Qb + (long)qt * AK * ld);
-    const char* gb = uniform_ptr(Gb + (long)qt * AK * D);
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int piece = wv * PW + i;
-      unsigned oq = offq[i], og = offg[i];
-      if (qt >= nfull) {
-        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128(row);
-        const int r = min(qt * AK + row, N - 1) - qt * AK;
-        oq = 2u * (unsigned)(r * ld + c * 8);
-        og = 2u * (unsigned)(r * D + c * 8);
-      }
-      glds_s<false>(oq, qb, qimg + piece * 1024);
-      glds_s<false>(og, gb, gimg + piece * 1024);
-    }
-    if (wv == 0) {
-      glds4_s(4u * (lane + qt * AK), Ls, &srow[S][0][0]);
-      glds4_s(4u * (lane + qt * AK), Ds, &srow[S][1][0]);
-    }
-  };
-
-  bf16x8 qa[4], ga[4];
-  f32x16 sn, dn;          // A(u+1) chains' initial accumulators (shared by both key blocks)
-  f32x16 sc[KB], dc[KB];  // A(u) results
-  auto read_frag = [&](const char* qimg, const char* gimg, int t, int ks) {
-    qa[ks] = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-    ga[ks] = *(const bf16x8*)(gimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-  };
-  auto read_rows = [&](const float* lr, const float* dr, int t, int part) {
-    const float4 l4 = *(const float4*)(lr + 32 * t + 8 * part + 4 * hl);
-    const float4 d4 = *(const float4*)(dr + 32 * t + 8 * part + 4 * hl);
-    sn[4 * part] = l4.x; sn[4 * part + 1] = l4.y; sn[4 * part + 2] = l4.z; sn[4 * part + 3] = l4.w;
-    dn[4 * part] = d4.x; dn[4 * part + 1] = d4.y; dn[4 * part + 2] = d4.z; dn[4 * part + 3] = d4.w;
-  };
-  unsigned up[KB][8], ud[KB][8];
-  bf16x8 tg0[2], tg1[2], tq0[2], tq1[2];
-  auto e_step = [&](int kb, int i) {
-    const float p0 = fast_exp2(sc[kb][2 * i]), p1 = fast_exp2(sc[kb][2 * i + 1]);
-    up[kb][i] = pk_bf16(p0, p1);
-    ud[kb][i] = pk_bf16(p0 * dc[kb][2 * i], p1 * dc[kb][2 * i + 1]);
-  };
-  auto word8 = [&](const unsigned (&w)[8], int ss) {
-    return __builtin_bit_cast(bf16x8, make_uint4(w[4 * ss], w[4 * ss + 1], w[4 * ss + 2], w[4 * ss + 3]));
-  };
-  auto read_b = [&](const char* qimg, const char* gimg, int t, int ss) {
-    const int rb = 32 * t + 16 * ss;
-    tg0[ss] = tr_acc_order(gimg, rb, 0, lane);
-    tg1[ss] = tr_acc_order(gimg, rb, 32, lane);
-    tq0[ss] = tr_acc_order(qimg, rb, 0, lane);
-    tq1[ss] = tr_acc_order(qimg, rb, 32, lane);
-  };
-  auto body = [&](auto sa, auto ta, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
-    constexpr int SB = decltype(sb)::value, TB = decltype(tb)::value;
-    constexpr int SN = decltype(sn_)::value, TN = decltype(tn)::value;
-    constexpr bool BAR = decltype(bar)::value;
-    (void)sa;
-    (void)ta;
-    f32x16 s[KB], dp[KB];
-    // A(u): key block 0's S / dP chains (g < 8), then block 1's, on the Q / dO fragments read
-    // during the previous B phase. Beside them: the E steps of the previous unit's block 0 and
-    // half of block 1 (the rest run in the B phase: 16 E steps over 32 MFMA gaps), and the
-    // transposed reads of B(u-1).
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int kb = g >> 3, ks = (g >> 1) & 3;
-      if ((g & 1) == 0) {
-        if (ks == 0) s[kb] = mfma_init_v(qa[0], kf[kb][0], sn);
-        else mfma_acc_v(s[kb], qa[ks], kf[kb][ks]);
-      } else {
-        if (ks == 0) dp[kb] = mfma_init_v(ga[0], vf[kb][0], dn);
-        else mfma_acc_v(dp[kb], ga[ks], vf[kb][ks]);
-      }
-      if (g < 12) e_step(g >> 3, g & 7);
-      if (g == 2) read_b(smem[SB][0], smem[SB][1], TB, 0);
-      if (g == 6) read_b(smem[SB][0], smem[SB][1], TB, 1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (BAR) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (jn < nt) issue(jn, jn % BNS);
-    }
-    // B(u-1): dV / dK of both key blocks; beside them block 1's last E steps (consumed from g =
-    // 12) and ALL of A(u+1)'s reads (its fragments and row constants), a phase ahead of use
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int kb = g >> 3, ss = (g >> 2) & 1;
-      switch (g & 3) {
-        case 0: mfma_acc_a(dv0[kb], word8(up[kb], ss), tg0[ss]); break;
-        case 1: mfma_acc_a(dk0[kb], word8(ud[kb], ss), tq0[ss]); break;
-        case 2: mfma_acc_a(dv1[kb], word8(up[kb], ss), tg1[ss]); break;
-        default: mfma_acc_a(dk1[kb], word8(ud[kb], ss), tq1[ss]); break;
-      }
-      if (g < 4) e_step(1, 4 + g);
-      if (more) {
-        if (g >= 4 && g < 12 && (g & 1) == 0) read_frag(smem[SN][0], smem[SN][1], TN, (g - 4) >> 1);
-        if (g >= 5 && g < 13 && (g & 1)) read_rows(srow[SN][0], srow[SN][1], TN, (g - 5) >> 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb) {
-      sc[kb] = s[kb];
-      dc[kb] = dp[kb];
-    }
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using F = std::false_type;
-  using T = std::true_type;
-
-  issue(0, 0);
-  if (nt > 1) issue(1, 1);
-  {
-    uint4* z2 = (uint4*)&smem[2][0][0];  // B(-1)'s stage: finite zeros
-    for (int i = tid; i < 2 * 8192 / 16; i += 64 * W) z2[i] = make_uint4(0, 0, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int part = 0; part < 4; ++part) read_rows(srow[0][0], srow[0][1], 0, part);
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) read_frag(smem[0][0], smem[0][1], 0, ks);
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sc[kb][r] = NEG_BIG;
-      dc[kb][r] = 0.f;
-    }
-  auto tile = [&](auto s, int j) {
-    constexpr int S = decltype(s)::value;
-    using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
-    using SNX = std::integral_constant<int, (S + 1) % BNS>;
-    using SC = std::integral_constant<int, S>;
-    body(SC{}, I0{}, SP{}, I1{}, SC{}, I1{}, F{}, 0, true);
-    body(SC{}, I1{}, SC{}, I0{}, SNX{}, I0{}, T{}, j + 2, j + 1 < nt);
-  };
-  int j = 0;
-  for (; j + 3 <= nt; j += 3) {
-    tile(I0{}, j);
-    tile(I1{}, j + 1);
-    tile(I2{}, j + 2);
-  }
-  if (j < nt) tile(I0{}, j);
-  if (j + 1 < nt) tile(I1{}, j + 1);
-  {
-    const int S = (nt - 1) % BNS;
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) e_step(kb, i);
-    read_b(smem[S][0], smem[S][1], 1, 0);
-    read_b(smem[S][0], smem[S][1], 1, 1);
-#pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        mfma_acc_a(dv0[kb], word8(up[kb], ss), tg0[ss]);
-        mfma_acc_a(dk0[kb], word8(ud[kb], ss), tq0[ss]);
-        mfma_acc_a(dv1[kb], word8(up[kb], ss), tg1[ss]);
-        mfma_acc_a(dk1[kb], word8(ud[kb], ss), tq1[ss]);
-      }
-    asm_mfma_drain();
-  }
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int kk = kw0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hl;
-      if (kk < N) {
-        bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
-        row[D + (lane & 31)] = (bf16)(dk0[kb][r] * scale);
-        row[D + 32 + (lane & 31)] = (bf16)(dk1[kb][r] * scale);
-        row[2 * D + (lane & 31)] = (bf16)dv0[kb][r];
-        row[2 * D + 32 + (lane & 31)] = (bf16)dv1[kb][r];
-      }
-    }
-}
-
 // dQ: 4 waves x 32 queries (prescaled Q and dO fragments in registers), key tiles of 64 rows;
 // also forms the queries' row constants (as attn_bwd_dq_v2_kernel<true, true>) and writes them
 // negated for the dK/dV kernel. The pipeline runs over the full key tiles; a ragged last tile
@@ -1101,8 +808,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v3_kernel(const bf1
                                                                 float* __restrict__ ndeltap, int N, int Npad, int H,
                                                                 bf16* __restrict__ dqkv, float scale,
                                                                 const bf16* __restrict__ out,
-                                                                const float* __restrict__ lse,
-                                                                unsigned* __restrict__ xpair, long xstride) {
+                                                                const float* __restrict__ lse) {
   __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1134,10 +840,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v3_kernel(const bf1
     if (hl == 0 && q < Npad) {
       nlse2p[(long)z * Npad + q] = -lse2;
       ndeltap[(long)z * Npad + q] = -dlt;
-      if (xpair) {  // the same as bf16 triples, for the dK/dV kernel's extra chain MFMA
-        ((uint2*)xpair)[(long)z * Npad + q] = split3_bf16(-lse2);
-        ((uint2*)(xpair + xstride))[(long)z * Npad + q] = split3_bf16(-dlt);
-      }
     }
   }
   f32x16 a0 = zero16(), a1 = zero16();
@@ -1348,8 +1050,8 @@ long ld_scores(long N) { return (N + 7) / 8 * 8; }
 }  // namespace
 
 extern "C" long ivit_attn_workspace(int dtype, long B, long N, long H, long Dh, int backward) {
-  // bf16 backward: -lse2 and -delta rows (f32) and the same as bf16 triples (2 words each)
-  if (dtype == IVIT_BF16) return backward ? 6 * B * H * ((N + AK - 1) / AK * AK) * 4 : 0;
+  // bf16 backward: the -lse2 and -delta rows (f32, padded to whole key tiles)
+  if (dtype == IVIT_BF16) return backward ? 2 * B * H * ((N + AK - 1) / AK * AK) * 4 : 0;
   const long one = B * H * N * ld_scores(N) * 4;
   return backward ? 2 * one : one;
 }
@@ -1543,17 +1245,8 @@ extern "C" int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh
   (void)work_bytes;
   if (B * N * H == 0) return 0;
   dim3 g(ivit_cdiv(N, 128), B * H);
-  const char* an = getenv("IVIT_ATTN_AN");
-  const int anm = an ? atoi(an) : 0;
-  if (anm == 1)
-    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false, 1>, g, dim3(256), ivit_stream(stream),
-              (const bf16*)qkv, (int)N, (int)H, (bf16*)out, lse, 1.0f);
-  else if (anm == 2)
-    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false, 2>, g, dim3(256), ivit_stream(stream),
-              (const bf16*)qkv, (int)N, (int)H, (bf16*)out, lse, 1.0f);
-  else
-    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream), (const bf16*)qkv,
-              (int)N, (int)H, (bf16*)out, lse, 1.0f);
+  kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream), (const bf16*)qkv,
+            (int)N, (int)H, (bf16*)out, lse, 1.0f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -1570,13 +1263,6 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   const long Npad = (N + AK - 1) / AK * AK;
   float* lse2p = (float*)work;
   float* deltap = lse2p + B * H * Npad;
-  unsigned* xpair = (unsigned*)(deltap + B * H * Npad);
-  // IVIT_ATTN_XR=1: dK/dV with the row constants through the extra chain MFMA (correct, measured
-  // 0.825 vs 0.812 ms per pair: the two MFMAs cost more than the LDS reads they remove)
-  static const bool xr = [] {
-    const char* e = getenv("IVIT_ATTN_XR");
-    return e && atoi(e) != 0;
-  }();
   // dQ also forms the row constants (-lse2, -delta) the dK/dV kernel reads: no rows kernel.
   // 4 waves per workgroup, two workgroups per CU: 8-wave workgroups (half the L2 -> LDS bytes,
   // one per CU) measured 0.875 vs 0.814 ms per pair (the 8-wave tile barrier, no second
@@ -1584,25 +1270,9 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   constexpr int BW = 4;
   const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
   kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse,
-            xpair, 2 * B * H * Npad);
-  const char* v4e = getenv("IVIT_ATTN_DKV_V4");
-  if (v4e && atoi(v4e) == 1) {  // 64 keys per wave, one wave per SIMD (attn_bwd_dkv_v4_kernel)
-    const dim3 g4(ivit_cdiv(N, 64 * BW), B * H);
-    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<BW>, g4, dim3(64 * BW), st, (const bf16*)qkv,
-              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
-  } else if (v4e && atoi(v4e) == 2) {  // the same with 2-wave workgroups (two per CU)
-    const dim3 g4(ivit_cdiv(N, 128), B * H);
-    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<2>, g4, dim3(128), st, (const bf16*)qkv,
-              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
-  } else if (xr) {  // row constants through one extra MFMA per chain (bf16 pairs)
-    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW, true>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-              (const bf16*)dout, (const float*)xpair, (const float*)(xpair + 2 * B * H * Npad), (int)N, (int)Npad, (int)H,
-              (bf16*)dqkv, 0.69314718055994531f);
-  } else {
-    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
-  }
+            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
+  kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -116,13 +116,29 @@ __global__ void merge_heads_kernel(const float* dcls, const float* dbox, const f
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // shadows (optional): per tensor a bf16 copy of the updated parameter (nullptr: none) — the
 // compute-dtype weights the next forward reads, refreshed here instead of by per-step casts.
-// (shadows: stride sstride entries per tensor; finite: as adamw_packed_kernel below)
+// finite (optional, device): 0 = the loss guard fired (loss.py:190-198) — nothing is updated, as
+// when the reference's step sees no grad.
+// steps_in / steps_out (optional, device f32 per tensor): the step counts before / after this
+// update. With them bc1 / bc2 come from steps_in[t] + 1 in f64 (what the host computes from its
+// counter), and a skipped (finite = 0) update leaves the count where it was, so the NEXT update's
+// bias correction is the one torch.optim.AdamW uses when that step never happened. The count is
+// written to a second buffer (block 0 of the tensor) so that no block reads a count another
+// block has already advanced; the caller swaps the two buffers.
 __global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* const* grads, void* const* ms,
                                                     void* const* vs, const long* sizes, float lr, float b1, float b2,
                                                     float eps, float wd, float bc1, float bc2s, void* const* shadows,
-                                                    int sstride, const float* finite) {
-  if (finite != nullptr && !(*finite != 0.f)) return;
+                                                    int sstride, const float* finite, const float* steps_in,
+                                                    float* steps_out, double b1d, double b2d) {
   const int t = blockIdx.y;
+  const bool go = finite == nullptr || *finite != 0.f;
+  if (steps_in != nullptr) {
+    const float s0 = steps_in[t];
+    if (blockIdx.x == 0 && threadIdx.x == 0) steps_out[t] = go ? s0 + 1.f : s0;
+    const double s = (double)s0 + 1.0;
+    bc1 = (float)(1.0 - pow(b1d, s));
+    bc2s = (float)sqrt(1.0 - pow(b2d, s));
+  }
+  if (!go) return;
   const long n = sizes[t];
   float* p = (float*)params[t];
   const float* g = (const float*)grads[t];
@@ -142,114 +158,6 @@ __global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* c
     m[i] = mi;
     v[i] = vi;
     if (sh) sh[i] = (bf16)pi;
-  }
-}
-
-// The same update for tensors that also carry row-panel weight packs (ops.packed_weight /
-// packed_weight_t: MFMA fragment order, rebuilt only when the parameter's version moves — the
-// pointer-table update here does not move it, so the packs are rewritten in this launch).
-// outs[3 t + 0..2] = bf16 shadow | pack of W [rows][cols] | pack of W^T (each may be null);
-// cols[t] = row length. A tensor with a pack is walked in 8 x 8 tiles, one per thread: per tile
-// row, 8 consecutive elements (the shadow's 16 B and the pack's 16-B fragment piece), and the
-// transposed pack's eight 16-B pieces after the 8 rows. finite (optional, device): 0 = the loss
-// guard fired (loss.py:190-198) — nothing is updated, as when the reference's step sees no grad.
-struct Adam {
-  float lr, b1, b2, eps, wd, step, bc2s;
-  IVIT_DEV float upd(float pi, float gi, float& mi, float& vi) const {
-    pi = pi * (1.f - lr * wd);
-    mi = mi + (1.f - b1) * (gi - mi);
-    vi = vi * b2 + (1.f - b2) * gi * gi;
-    const float den = sqrtf(vi) / bc2s + eps;
-    return pi - step * (mi / den);
-  }
-};
-
-__global__ __launch_bounds__(256) void adamw_packed_kernel(void* const* params, void* const* grads, void* const* ms, void* const* vs,
-                                    void* const* outs, const long* cols, const long* sizes, Adam a,
-                                    const float* finite) {
-  if (finite != nullptr && !(*finite != 0.f)) return;
-  const int t = blockIdx.y;
-  const long n = sizes[t];
-  float* p = (float*)params[t];
-  const float* g = (const float*)grads[t];
-  float* m = (float*)ms[t];
-  float* v = (float*)vs[t];
-  bf16* sh = (bf16*)outs[3 * t];
-  uint4* pk = (uint4*)outs[3 * t + 1];
-  uint4* pkt = (uint4*)outs[3 * t + 2];
-  if (pk == nullptr && pkt == nullptr) {
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-      float mi = m[i], vi = v[i];
-      const float pi = a.upd(p[i], g[i], mi, vi);
-      p[i] = pi;
-      m[i] = mi;
-      v[i] = vi;
-      if (sh) sh[i] = (bf16)pi;
-    }
-    return;
-  }
-  const long C = cols[t], R = n / C, tc = C / 8, ntile = (R / 8) * tc;
-  // grads may be views into DDP buckets at any 4-B offset: 16-B accesses only when all four
-  // streams are aligned (uniform per tensor)
-  const bool vec = ((((unsigned long)p) | ((unsigned long)g) | ((unsigned long)m) | ((unsigned long)v)) & 15) == 0;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < ntile; i += (long)gridDim.x * blockDim.x) {
-    const unsigned tr = (unsigned)i / (unsigned)tc;  // ntile < 2^31: 32-bit division
-    const long r0 = (long)tr * 8, c0 = (i - (long)tr * tc) * 8;
-    unsigned tw[8][4];  // transposed pack: column e of the tile, rows 2j, 2j+1
-    float prev[8];      // the even row's values until the odd row pairs them
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const long o = (r0 + r) * C + c0;
-      float pv[8], gv[8], mv[8], vv[8];
-      if (vec) {
-        *(float4*)&pv[0] = *(const float4*)(p + o); *(float4*)&pv[4] = *(const float4*)(p + o + 4);
-        *(float4*)&gv[0] = *(const float4*)(g + o); *(float4*)&gv[4] = *(const float4*)(g + o + 4);
-        *(float4*)&mv[0] = *(const float4*)(m + o); *(float4*)&mv[4] = *(const float4*)(m + o + 4);
-        *(float4*)&vv[0] = *(const float4*)(v + o); *(float4*)&vv[4] = *(const float4*)(v + o + 4);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          pv[e] = p[o + e]; gv[e] = g[o + e]; mv[e] = m[o + e]; vv[e] = v[o + e];
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) pv[e] = a.upd(pv[e], gv[e], mv[e], vv[e]);
-      if (vec) {
-        *(float4*)(p + o) = *(float4*)&pv[0]; *(float4*)(p + o + 4) = *(float4*)&pv[4];
-        *(float4*)(m + o) = *(float4*)&mv[0]; *(float4*)(m + o + 4) = *(float4*)&mv[4];
-        *(float4*)(v + o) = *(float4*)&vv[0]; *(float4*)(v + o + 4) = *(float4*)&vv[4];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          p[o + e] = pv[e]; m[o + e] = mv[e]; v[o + e] = vv[e];
-        }
-      }
-      const uint4 w8 = make_uint4(pk_bf16(pv[0], pv[1]), pk_bf16(pv[2], pv[3]), pk_bf16(pv[4], pv[5]),
-                                  pk_bf16(pv[6], pv[7]));
-      if (sh) {
-        if (vec) *(uint4*)(sh + o) = w8;
-        else
-#pragma unroll
-          for (int e = 0; e < 8; ++e) sh[o + e] = (bf16)pv[e];
-      }
-      if (pk) {  // W [R][C]: lane (row & 15) + 16 ((c & 31) / 8) of 16-row block row / 16, k step c / 32
-        const long row = r0 + r;
-        pk[((c0 / 32) * (R / 16) + row / 16) * 64 + (row & 15) + 16 * ((c0 & 31) / 8)] = w8;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        if (r & 1) tw[e][r >> 1] = pk_bf16(prev[e], pv[e]);
-        else prev[e] = pv[e];
-      }
-    }
-    if (pkt) {  // W^T [C][R]: k = row (r0..r0+7 = one 8-element piece), n = column c0 + e
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const long col = c0 + e;
-        pkt[((r0 / 32) * (C / 16) + col / 16) * 64 + (col & 15) + 16 * ((r0 & 31) / 8)] =
-            make_uint4(tw[e][0], tw[e][1], tw[e][2], tw[e][3]);
-      }
-    }
   }
 }
 
@@ -315,7 +223,7 @@ extern "C" int ivit_adamw(long n_tensors, void* const* params, void* const* grad
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
                      exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, (void* const*)nullptr, 1,
-                     (const float*)nullptr);
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, 0.0, 0.0);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -331,29 +239,25 @@ extern "C" int ivit_adamw_shadow(long n_tensors, void* const* params, void* cons
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
                      exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, shadows, 1,
-                     (const float*)nullptr);
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, 0.0, 0.0);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
 
-extern "C" int ivit_adamw_packed(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
-                                 void* const* exp_avg_sq, void* const* outs, const long* cols, const long* sizes,
-                                 long max_work, float lr, float beta1, float beta2, float eps, float weight_decay,
-                                 float bc1, float bc2_sqrt, const float* finite, int tiled, void* stream) {
+extern "C" int ivit_adamw_guarded(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
+                                  void* const* exp_avg_sq, void* const* shadows, const long* sizes, long max_size,
+                                  float lr, double beta1, double beta2, float eps, float weight_decay, float bc1,
+                                  float bc2_sqrt, const float* finite, const float* steps_in, float* steps_out,
+                                  void* stream) {
   if (n_tensors <= 0) return 0;
-  IVIT_CHECK_ARG(n_tensors < 65536, "ivit_adamw_packed: too many tensors");
-  IVIT_CHECK_ARG(outs != nullptr && cols != nullptr, "ivit_adamw_packed: null outs / cols table");
-  int gx = ivit_cdiv(max_work, 256);
+  IVIT_CHECK_ARG(n_tensors < 65536, "ivit_adamw_guarded: too many tensors");
+  IVIT_CHECK_ARG((steps_in == nullptr) == (steps_out == nullptr), "ivit_adamw_guarded: steps_in / steps_out pair");
+  IVIT_CHECK_ARG(steps_in == nullptr || steps_in != steps_out, "ivit_adamw_guarded: steps_out aliases steps_in");
+  int gx = ivit_cdiv(max_size, 256);
   if (gx > 1024) gx = 1024;
-  if (!tiled) {  // no packs: the light streaming kernel (the tile kernel's registers cap occupancy)
-    hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
-                       exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, outs, 3, finite);
-    IVIT_LAUNCH_CHECK();
-    return 0;
-  }
-  const Adam a{lr, beta1, beta2, eps, weight_decay, lr / bc1, bc2_sqrt};
-  hipLaunchKernelGGL(adamw_packed_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads,
-                     exp_avg, exp_avg_sq, outs, cols, sizes, a, finite);
+  hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
+                     exp_avg_sq, sizes, lr, (float)beta1, (float)beta2, eps, weight_decay, bc1, bc2_sqrt, shadows, 1,
+                     finite, steps_in, steps_out, beta1, beta2);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -220,13 +220,6 @@ typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 IVIT_DEV unsigned pk_bf16(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
 }
-// x as three bf16 (hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid)), element order hi,
-// mid, lo, 0 in two words: hi + mid + lo = x for normal f32 x (24 significant bits), e.g. as an
-// MFMA operand against (1, 1, 1, 0)
-IVIT_DEV uint2 split3_bf16(float x) {
-  const float hi = (float)(bf16)x, r = x - hi, mid = (float)(bf16)r;
-  return make_uint2(pk_bf16(hi, mid), pk_bf16(r - mid, 0.f));
-}
 IVIT_DEV uint4 f32x8_to_bf16x8(float4 a, float4 b) {
   return make_uint4(pk_bf16(a.x, a.y), pk_bf16(a.z, a.w), pk_bf16(b.x, b.y), pk_bf16(b.z, b.w));
 }

@@ -2,8 +2,19 @@
 
 Same constructor arguments, same forward signature and the same returned dict keys. The
 whole assignment + focal/Smooth-L1/CE computation is four HIP kernels with no host
-synchronisation (the reference syncs per GT and per `.item()`); ``num_pos_anchors`` is
-therefore returned as a 0-dim device tensor (callers in train_vit.py already handle both).
+synchronisation (the reference syncs per GT and per `.item()`).
+
+The non-finite guard (loss.py:190-206), two forms:
+  * ``sync_guard=True`` (the default outside ``trainer.Trainer``, and under ``run_with_ivit.py``):
+    exactly the reference's contract. The device finite flag and the positive-anchor count are
+    read once (one host sync, where the reference syncs too: ``torch.isnan(...).any()`` and
+    ``num_pos_total_batch.item()``); ``num_pos_anchors`` is a Python int and a non-finite total
+    returns a disconnected ``requires_grad`` zero leaf, so a reference-style
+    ``loss.backward(); torch.optim.AdamW.step()`` leaves ``.grad`` None and updates nothing.
+  * ``sync_guard=False`` (what ``Trainer.step`` selects through ``device_guard()``): no host
+    sync. ``num_pos_anchors`` is a 0-d device tensor, a non-finite total returns a zero loss still
+    connected to the logits with exact-zero gradients, and ``last_finite`` (device 1.0 / 0.0)
+    tells the Trainer / FusedAdamW to skip the update.
 
 Intention down-sampling (loss.py:169-182), two random streams:
   * ``downsample_rng="device"`` (default): one uniform per anchor on the device
@@ -17,11 +28,30 @@ Intention down-sampling (loss.py:169-182), two random streams:
 """
 from __future__ import annotations
 
+import contextlib
+import threading
+
 import torch
 import torch.nn as nn
 
 import ops
 from constants import DOMINANT_CLASSES_FOR_DOWNSAMPLING, INTENTION_DOWNSAMPLE_RATIO
+
+
+_TLS = threading.local()
+
+
+@contextlib.contextmanager
+def device_guard():
+    """Inside this block a loss built with ``sync_guard=None`` (the default) takes the sync-free
+    device guard; ``trainer.Trainer.step`` wraps its loss call in it (wrappers around the loss
+    included). An explicit ``sync_guard=True / False`` on the module always wins."""
+    prev = getattr(_TLS, "device", False)
+    _TLS.device = True
+    try:
+        yield
+    finally:
+        _TLS.device = prev
 
 
 def pack_gt(gt_list, device):
@@ -50,8 +80,12 @@ class DetectionIntentionLoss(nn.Module):
                  intention_class_weights=None, use_rotated_iou=False, focal_loss_alpha=0.25, focal_loss_gamma=2.0,
                  smooth_l1_beta=1.0 / 9.0, apply_intention_downsampling=True,
                  dominant_intentions=DOMINANT_CLASSES_FOR_DOWNSAMPLING,
-                 intention_downsample_ratio=INTENTION_DOWNSAMPLE_RATIO, downsample_rng="device"):
+                 intention_downsample_ratio=INTENTION_DOWNSAMPLE_RATIO, downsample_rng="device",
+                 sync_guard=None):
         super().__init__()
+        if sync_guard not in (None, True, False):
+            raise ValueError(f"sync_guard must be None, True or False, got {sync_guard!r}")
+        self.sync_guard = sync_guard
         if downsample_rng not in ("device", "reference"):
             raise ValueError(f"downsample_rng must be 'device' or 'reference', got {downsample_rng!r}")
         self.downsample_rng = downsample_rng
@@ -104,8 +138,29 @@ class DetectionIntentionLoss(nn.Module):
         # 1.0 / 0.0 on device: 0 means the guard of loss.py:190-198 fired (loss and terms are 0,
         # and the backward writes exact zero gradients); trainer.Trainer skips the update on it
         self.last_finite = stats[9].detach()
+        sync = self.sync_guard if self.sync_guard is not None else not getattr(_TLS, "device", False)
+        if sync:
+            return self._reference_guard(loss, stats, dev)
         return {"loss": loss, "cls_loss": stats[6].detach(), "box_loss": stats[7].detach(),
                 "intent_loss": stats[8].detach(), "num_pos_anchors": stats[3].detach().round().long()}
+
+    def _reference_guard(self, loss, stats, dev):
+        """loss.py:190-206 with one host read of (finite flag, positive count, raw terms)."""
+        h = stats.detach()[:16].cpu()
+        num_pos = int(round(float(h[3])))
+        if float(h[9]) == 0.0:
+            # the reference prints the raw (non-finite) terms before zeroing them: rebuilt from
+            # the device's raw sums and denominators (loss_final_kernel: slots 0-4, 10, 11)
+            cden, iden = float(h[10]), float(h[11])
+            cl = float(h[0]) / cden
+            bl = float(h[1]) / cden if num_pos > 0 else 0.0
+            il = float(h[2]) / iden if num_pos > 0 else 0.0
+            print(f"NaN or Inf DETECTED IN LOSS! Cls: {cl}, Box: {bl}, Intent: {il}")
+            z = torch.tensor(0.0, device=dev)
+            return {"loss": torch.tensor(0.0, device=dev, requires_grad=True), "cls_loss": z,
+                    "box_loss": z.clone(), "intent_loss": z.clone(), "num_pos_anchors": num_pos}
+        return {"loss": loss, "cls_loss": stats[6].detach(), "box_loss": stats[7].detach(),
+                "intent_loss": stats[8].detach(), "num_pos_anchors": num_pos}
 
     def _reference_keep(self, cls_logits, box_preds, intention_logits, anchors, gt, ng, gi):
         """The keep mask of the reference's draws (loss.py:170-178): the per-anchor targets from one

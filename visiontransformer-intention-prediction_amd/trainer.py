@@ -25,6 +25,7 @@ from __future__ import annotations
 import torch
 
 from ddp import GradBuckets, any_rank, broadcast_state, min_on_device
+from loss import device_guard
 from optim import FusedAdamW
 
 
@@ -66,7 +67,8 @@ class Trainer:
             if any_rank(bool(bad), dev):
                 self.skipped += 1
                 return None
-        d = self.loss_fn(cls, box, intent, self.anchors, gts)
+        with device_guard():  # the sync-free guard: last_finite decides below (loss.py docstring)
+            d = self.loss_fn(cls, box, intent, self.anchors, gts)
         if self.check_nan and any_rank(not self._loss_finite(d), dev):
             self.nonfinite += 1
             return d

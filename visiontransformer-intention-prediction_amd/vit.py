@@ -63,13 +63,17 @@ class Block(nn.Module):
         self.drop_path_scales = None
         self.last_scales = (None, None)
 
-    def _scales(self, B, device):
+    def _scales(self, B, device, drawn=None):
         """timm DropPath: per-sample Bernoulli(1-p) / (1-p), independent per branch (identity
-        in eval mode or at p = 0)."""
+        in eval mode or at p = 0). ``drawn``: this block's [2, B] factors from the stream's one
+        draw for all blocks (VisionTransformer._draw_drop_path)."""
         p = self.drop_path_rate
         if not self.training or p <= 0.0:
             self.last_scales = (None, None)
             return None, None
+        if drawn is not None and self.drop_path_scales is None:
+            self.last_scales = (drawn[0], drawn[1])
+            return self.last_scales
         if self.drop_path_scales is not None:
             s = torch.stack([torch.as_tensor(v, dtype=torch.float32).reshape(B) for v in self.drop_path_scales])
             s = s.to(device)
@@ -79,12 +83,12 @@ class Block(nn.Module):
         self.last_scales = (s[0].contiguous(), s[1].contiguous())
         return self.last_scales
 
-    def forward_flat(self, x, B, N, cdt, ln_in=None, next_norm=None, hand_mine=None, hand_prev=None):
+    def forward_flat(self, x, B, N, cdt, ln_in=None, next_norm=None, hand_mine=None, hand_prev=None, drawn=None):
         """-> (x_out, (y, mean, rstd) of the next block's norm1 or empty tensors): `ln_in` is
         this block's (y, mean, rstd) of norm1 computed by the previous block's fc2 epilogue;
         `next_norm` the next block's norm1, whose forward this block's fc2 epilogue runs
         (ops.ViTBlockFn, bf16 row-panel path)."""
-        s1, s2 = self._scales(B, x.device)
+        s1, s2 = self._scales(B, x.device, drawn)
         nxw = next_norm.weight if next_norm is not None else None
         nxb = next_norm.bias if next_norm is not None else None
         li, mi, ri = ln_in if ln_in is not None else (None, None, None)
@@ -124,6 +128,22 @@ class VisionTransformer(nn.Module):
         for i, blk in enumerate(self.blocks):
             blk.drop_path_scales = None if scales is None else scales[i]
 
+    def _draw_drop_path(self, B, device):
+        """Every block's DropPath factors of this forward in ONE draw: torch.bernoulli over a cached
+        device tensor of the per-block keep probabilities ([depth, 2, B]: attention / MLP branch),
+        then one divide — 2 launches per stream instead of 2 per block (timm draws per block and
+        branch, the same Bernoulli(1-p)/(1-p) law, a different stream). None when no block drops."""
+        if not self.training or all(b.drop_path_rate <= 0.0 for b in self.blocks):
+            return None
+        key = (device, B)
+        cache = getattr(self, "_keep_cache", None)
+        if cache is None or cache[0] != key:
+            keep = torch.tensor([1.0 - b.drop_path_rate for b in self.blocks], dtype=torch.float32)
+            keep = keep.view(-1, 1, 1).expand(len(self.blocks), 2, B).contiguous().to(device)
+            self._keep_cache = cache = (key, keep)
+        keep = cache[1]
+        return torch.bernoulli(keep).div_(keep)
+
     def _cdt(self):
         return BF16 if self.compute_dtype == torch.bfloat16 else F32
 
@@ -141,11 +161,13 @@ class VisionTransformer(nn.Module):
         ln = None
         # ... and in the backward, block i+1 hands block i its DropPath-scaled bf16 gradient
         hands = [ops.GradHandoff() for _ in self.blocks] if fuse and torch.is_grad_enabled() else None
+        drawn = self._draw_drop_path(B, x.device)
         for i, blk in enumerate(self.blocks):
             nxt = self.blocks[i + 1].norm1 if fuse and i + 1 < len(self.blocks) else None
             t, nxt_ln = blk.forward_flat(t, B, N, cdt, ln_in=ln, next_norm=nxt,
                                          hand_mine=hands[i] if hands else None,
-                                         hand_prev=hands[i - 1] if hands and i > 0 else None)
+                                         hand_prev=hands[i - 1] if hands and i > 0 else None,
+                                         drawn=drawn[i] if drawn is not None else None)
             ln = nxt_ln if nxt is not None else None
         return t
 
