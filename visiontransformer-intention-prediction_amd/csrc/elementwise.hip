@@ -116,6 +116,8 @@ __global__ void merge_heads_kernel(const float* dcls, const float* dbox, const f
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // shadows (optional): per tensor a bf16 copy of the updated parameter (nullptr: none) — the
 // compute-dtype weights the next forward reads, refreshed here instead of by per-step casts.
+// omb1 / omb2: the (1 - beta) weights of lerp / addcmul (torch computes them in f64 from its Python
+// floats; the guarded entry point does the same).
 // finite (optional, device): 0 = the loss guard fired (loss.py:190-198) — nothing is updated, as
 // when the reference's step sees no grad.
 // steps_in / steps_out (optional, device f32 per tensor): the step counts before / after this
@@ -128,7 +130,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* c
                                                     void* const* vs, const long* sizes, float lr, float b1, float b2,
                                                     float eps, float wd, float bc1, float bc2s, void* const* shadows,
                                                     int sstride, const float* finite, const float* steps_in,
-                                                    float* steps_out, double b1d, double b2d) {
+                                                    float* steps_out, double b1d, double b2d, float omb1,
+                                                    float omb2) {
   const int t = blockIdx.y;
   const bool go = finite == nullptr || *finite != 0.f;
   if (steps_in != nullptr) {
@@ -150,8 +153,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* c
     const float gi = g[i];
     float pi = p[i] * (1.f - lr * wd);
     float mi = m[i];
-    mi = mi + (1.f - b1) * (gi - mi);
-    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    mi = mi + omb1 * (gi - mi);
+    float vi = v[i] * b2 + omb2 * gi * gi;
     const float den = sqrtf(vi) / bc2s + eps;
     pi = pi - step * (mi / den);
     p[i] = pi;
@@ -223,7 +226,7 @@ extern "C" int ivit_adamw(long n_tensors, void* const* params, void* const* grad
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
                      exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, (void* const*)nullptr, 1,
-                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, 0.0, 0.0);
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, 0.0, 0.0, 1.f - beta1, 1.f - beta2);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -239,7 +242,7 @@ extern "C" int ivit_adamw_shadow(long n_tensors, void* const* params, void* cons
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
                      exp_avg_sq, sizes, lr, beta1, beta2, eps, weight_decay, bc1, bc2_sqrt, shadows, 1,
-                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, 0.0, 0.0);
+                     (const float*)nullptr, (const float*)nullptr, (float*)nullptr, 0.0, 0.0, 1.f - beta1, 1.f - beta2);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -257,7 +260,7 @@ extern "C" int ivit_adamw_guarded(long n_tensors, void* const* params, void* con
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(adamw_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), params, grads, exp_avg,
                      exp_avg_sq, sizes, lr, (float)beta1, (float)beta2, eps, weight_decay, bc1, bc2_sqrt, shadows, 1,
-                     finite, steps_in, steps_out, beta1, beta2);
+                     finite, steps_in, steps_out, beta1, beta2, (float)(1.0 - beta1), (float)(1.0 - beta2));
   IVIT_LAUNCH_CHECK();
   return 0;
 }
