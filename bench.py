@@ -332,7 +332,21 @@ def main():
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("LOCAL_RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-    rank, local, world, dev = init_distributed(force_group=force)
+    # RCCL prints its version banner to stdout (C level) when the communicator comes up: route fd 1 to
+    # stderr around the group's creation and first collective, so stdout carries only the JSON line
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        rank, local, world, dev = init_distributed(force_group=force)
+        if dist.is_initialized():
+            dist.barrier()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
     if dev.type != "cuda":
         raise RuntimeError("bench.py needs a ROCm GPU (the HIP kernels have no CPU path)")
     world = dist.get_world_size() if dist.is_initialized() else 1
