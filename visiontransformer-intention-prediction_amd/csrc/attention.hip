@@ -284,275 +284,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
   if (q < N && hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
 }
 
-// ------------------------------------------------------------------------- forward ping-pong (bf16, prescaled Q)
-// 8 waves = two groups of 4 on 128 queries: wave w and wave w + 4 own the same 32 queries and sit
-// on the same SIMD (waves are dealt round-robin over the 4 SIMDs). Group g takes the key tiles
-// t = g, g + 2, g + 4, ... (an in-workgroup split of the key sweep, merged at the end as two
-// online-softmax states), and the two groups run phase-locked, half a period apart:
-//     phase 2i    : group 0  V(i) = softmax of S_t (max, lazy rescale, exp2, cvt)   | group 1  M(i-1)
-//     phase 2i + 1: group 0  M(i) = S_{t+2} = K_{t+2} Q^T (8), O += V_t P_t (8), l (4) | group 1  V(i)
-// with one s_barrier per phase, so on every SIMD one wave streams its 20 MFMAs while its partner
-// issues the softmax VALU in the matrix pipe's shadow (MI355X_MICROARCH.md "Two waves per SIMD":
-// the merged interval pairs matrix with VALU, never matrix with matrix). Each group has its own
-// K / V rings (2 stages each, 32 KiB): the M phase of iteration i issues the LDS-DMA of K_{t+4}
-// and V_{t+2} (4 pieces per wave), the V phase of iteration i+1 retires them before its barrier.
-// 128 queries per workgroup keep the grid fine-grained (48 x 36 workgroups at N = 4501: 6.75 rounds
-// of 256 CUs) where one 8-wave workgroup per 256 queries would run 3.375 rounds (a 16 % tail).
-// PRIO: s_setprio 1 for the M phase (the MFMA stream first, the VALU in its gaps).
-constexpr int PP_SMEM = 65536;  // [group][K0 K1 V0 V1][8 KiB]
-
-IVIT_DEV void pp_pack_p(f32x16 (&s)[2], bf16x8 (&p)[4]) {
-  // all 32 exponentials first (in place), then the 16 conversions: a conversion right behind the
-  // v_exp_f32 it reads costs a hazard s_nop
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[t][r] = fast_exp2(s[t][r]);
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const f32x16& a = s[g >> 1];
-    const int o = 8 * (g & 1);
-    const uint4 u = make_uint4(pk_bf16(a[o], a[o + 1]), pk_bf16(a[o + 2], a[o + 3]), pk_bf16(a[o + 4], a[o + 5]),
-                               pk_bf16(a[o + 6], a[o + 7]));
-    p[g] = __builtin_bit_cast(bf16x8, u);
-  }
-}
-
-template <int PRIO>
-__global__ __launch_bounds__(512, 1) void attn_fwd_pp_kernel(const bf16* __restrict__ qkv, int N, int H,
-                                                             bf16* __restrict__ out, float* __restrict__ lse) {
-  __shared__ __attribute__((aligned(16))) char smem[PP_SMEM];
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = wv >> 2, w4 = wv & 3;
-  const int2 bid = attn_block_id();
-  const int z = bid.y, b = z / H, h = z - b * H;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
-  const int q = bid.x * 128 + w4 * 32 + (lane & 31);
-  char* gbase = smem + g * 32768;
-  auto kst = [&](int st) { return gbase + st * 8192; };
-  auto vst = [&](int st) { return gbase + 16384 + st * 8192; };
-  const int nt = (N + AK - 1) / AK, nfull = N / AK;
-  const int nit = (nt + 1) / 2;  // iterations of group 0 (group 1 has nt / 2 real ones)
-  // this wave's 2 of the 8 1-KiB pieces of a tile image (group-local wave w4)
-  unsigned off[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) off[i] = 2u * dma_off<4>(i, w4, lane, ld);
-  auto issue = [&](const bf16* base, int kt, char* img) __attribute__((always_inline)) {
-    const char* sb = uniform_ptr(base + (long)kt * AK * ld);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int piece = w4 * 2 + i;
-      unsigned o = off[i];
-      if (kt >= nfull) {  // ragged last tile: rows past N clamped to row N-1 (masked to P = 0)
-        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128(row);
-        o = 2u * (unsigned)((min(kt * AK + row, N - 1) - kt * AK) * ld + c * 8);
-      }
-      glds_s<false>(o, sb, img + piece * 1024);
-    }
-  };
-  bf16x8 qf[4];
-  load_row_frags(Qb + (long)(q < N ? q : 0) * ld, q < N, lane, qf);
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-  // prologue DMA: K_g -> K0, K_{g+2} -> K1, V_g -> V0
-  if (g < nt) {
-    issue(Kb, g, kst(0));
-    issue(Vb, g, vst(0));
-  }
-  if (g + 2 < nt) issue(Kb, g + 2, kst(1));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // the Q fragments are final here: without this the compiler waits for their loads at a use inside
-  // the loop, where vmcnt also counts (and drains) the M phase's fresh K / V DMA
-#pragma unroll
-  for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(qf[i]));
-  __builtin_amdgcn_s_barrier();
-
-  auto mask_tile = [&](f32x16 (&s)[2], int kbase) __attribute__((always_inline)) {
-    if (kbase + AK > N) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          s[t][r] = key >= N ? NEG_BIG : s[t][r];
-        }
-    }
-  };
-  f32x16 s[2];
-  f32x16 negm, o0 = zero16(), o1 = zero16(), lacc = zero16();
-  float m = NEG_BIG;
-  // prologue S_g (zero accumulators), m = its row max, S' = S - m
-  if (g < nt) {
-    qk_tile_c(kst(0), qf, zero16(), s, lane);
-    mask_tile(s, g * AK);
-    m = tile_rowmax<false>(s, 0, N, lane);
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[t][r] -= m;
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) negm[r] = -m;
-  bf16x8 p[4];
-
-  auto vphase = [&](int t) __attribute__((always_inline)) {
-    if (t < nt) {
-      if (t > g) mask_tile(s, t * AK);  // the prologue tile is already masked
-      float a = NEG_BIG, bm = NEG_BIG;
-#pragma unroll
-      for (int v = 0; v < 32; v += 2) {
-        if ((v >> 1) & 1) bm = vmax3(bm, s[v >> 4][v & 15], s[v >> 4][(v & 15) + 1]);
-        else a = vmax3(a, s[v >> 4][v & 15], s[v >> 4][(v & 15) + 1]);
-      }
-      const float mt = half_swap_max(fmaxf(a, bm));
-      const bool moved = mt > TAU;
-      if (__any(moved)) {
-        const float d = moved ? mt : 0.f;
-        const float alpha = fast_exp2(-d);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { o0[r] *= alpha; o1[r] *= alpha; lacc[r] *= alpha; }
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) s[tt][r] -= d;
-        m += d;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) asm volatile("v_sub_f32 %0, %0, %1" : "+v"(negm[r]) : "v"(d));
-      }
-      pp_pack_p(s, p);
-    }
-  };
-  // M(i): O += V_t P_t, l += 1 P_t; S_{t+2} = K_{t+2} Q^T - m (QK: t + 2 < nt); DMA K_{t+4}, V_{t+2}
-  auto mphase_body = [&](int t, auto stage, auto qkc) __attribute__((always_inline)) {
-    constexpr int ST = decltype(stage)::value;
-    constexpr bool QK = decltype(qkc)::value;
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
-    const char* kimg = kst(ST ^ 1);
-    const char* vimg = vst(ST);
-    bf16x8 vf[8], ka[8];
-    auto vread = [&](int f) { vf[f] = tr_acc_order(vimg, 16 * (f >> 1), 32 * (f & 1), lane); };
-    auto kread = [&](int i) {
-      ka[i] = *(const bf16x8*)(kimg + t_off(32 * (i >> 2) + (lane & 31), 2 * (i & 3) + hl));
-    };
-    vread(0);
-    vread(1);
-    if constexpr (QK) {
-      kread(0);
-      kread(4);
-    }
-    if (t + 4 < nt) issue(Kb, t + 4, kst(ST));
-    if (t + 2 < nt) issue(Vb, t + 2, vst(ST ^ 1));
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      if (kk < 3) {
-        vread(2 * kk + 2);
-        vread(2 * kk + 3);
-        if constexpr (QK) {
-          kread(kk + 1);
-          kread(kk + 5);
-        }
-      }
-      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * kk], p[kk], o0, 0, 0, 0);
-      if constexpr (QK) s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk], qf[kk], kk == 0 ? negm : s[0], 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * kk + 1], p[kk], o1, 0, 0, 0);
-      if constexpr (QK)
-        s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk + 4], qf[kk], kk == 0 ? negm : s[1], 0, 0, 0);
-      lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[kk], lacc, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (!QK) {  // dead S (no later tile), defined so the QK path's S needs no copy at the join
-      s[0] = zero16();
-      s[1] = zero16();
-    }
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
-  };
-  auto mphase = [&](int t, auto stage) __attribute__((always_inline)) {
-    if (t + 2 < nt) mphase_body(t, stage, std::true_type{});
-    else if (t < nt) mphase_body(t, stage, std::false_type{});
-  };
-  auto bar = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  if (g == 1) bar();
-  int i = 0;
-  for (; i + 1 < nit; i += 2) {
-    vphase(2 * i + g);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    mphase(2 * i + g, I0{});
-    bar();
-    vphase(2 * i + 2 + g);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    mphase(2 * i + 2 + g, I1{});
-    bar();
-  }
-  if (i < nit) {
-    vphase(2 * i + g);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    mphase(2 * i + g, I0{});
-    bar();
-  }
-  if (g == 0) bar();
-  // merge: group 1 hands (O, l, m) to group 0 through LDS ([w4][9][64 lanes] float4, 36 KiB)
-  float4* xb = (float4*)smem + (w4 * 9) * 64 + lane;
-  if (g == 1) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) xb[k * 64] = make_float4(o0[4 * k], o0[4 * k + 1], o0[4 * k + 2], o0[4 * k + 3]);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      xb[(4 + k) * 64] = make_float4(o1[4 * k], o1[4 * k + 1], o1[4 * k + 2], o1[4 * k + 3]);
-    xb[8 * 64] = make_float4(lacc[0], m, 0.f, 0.f);
-  }
-  lds_barrier();
-  if (g == 1) return;
-  const float4 lm = xb[8 * 64];
-  const float mm = fmaxf(m, lm.y);
-  const float a0 = fast_exp2(m - mm), a1 = fast_exp2(lm.y - mm);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float4 u = xb[k * 64], w = xb[(4 + k) * 64];
-    o0[4 * k] = o0[4 * k] * a0 + u.x * a1;
-    o0[4 * k + 1] = o0[4 * k + 1] * a0 + u.y * a1;
-    o0[4 * k + 2] = o0[4 * k + 2] * a0 + u.z * a1;
-    o0[4 * k + 3] = o0[4 * k + 3] * a0 + u.w * a1;
-    o1[4 * k] = o1[4 * k] * a0 + w.x * a1;
-    o1[4 * k + 1] = o1[4 * k + 1] * a0 + w.y * a1;
-    o1[4 * k + 2] = o1[4 * k + 2] * a0 + w.z * a1;
-    o1[4 * k + 3] = o1[4 * k + 3] * a0 + w.w * a1;
-  }
-  const float l = lacc[0] * a0 + lm.x * a1;
-  const float inv = 1.f / l;
-  bf16* orow = out + ((long)b * N + (q < N ? q : 0)) * D + h * 64;
-  auto emit = [&](const f32x16& o, int dbase) {
-#pragma unroll
-    for (int gg = 0; gg < 4; gg += 2) {
-      const unsigned e0 = pk_bf16(o[4 * gg] * inv, o[4 * gg + 1] * inv);
-      const unsigned e1 = pk_bf16(o[4 * gg + 2] * inv, o[4 * gg + 3] * inv);
-      const unsigned d0 = pk_bf16(o[4 * gg + 4] * inv, o[4 * gg + 5] * inv);
-      const unsigned d1 = pk_bf16(o[4 * gg + 6] * inv, o[4 * gg + 7] * inv);
-      const auto s0 = __builtin_amdgcn_permlane32_swap(d0, e0, false, false);
-      const auto s1 = __builtin_amdgcn_permlane32_swap(d1, e1, false, false);
-      if (q < N) *(uint4*)(orow + dbase + 8 * (hl ? gg : gg + 1)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-    }
-  };
-  emit(o0, 0);
-  emit(o1, 32);
-  if (q < N && hl == 0) lse[(long)z * N + q] = (mm + log2f(l)) * 0.69314718055994531f;
-}
-
 // ------------------------------------------------------------------------- backward v2 (bf16)
 // Row constants for the backward in a padded layout [z][Npad] (Npad = N rounded up to 64):
 // lse2 = lse * log2(e) (+1e30 on padding rows, so their probabilities are exactly 0) and
@@ -1514,21 +1245,8 @@ extern "C" int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh
   (void)work_bytes;
   if (B * N * H == 0) return 0;
   dim3 g(ivit_cdiv(N, 128), B * H);
-  // IVIT_ATTN_FWD: 0 = v6 (default: one software-pipelined wave stream, two workgroups per CU),
-  // 1 = ping-pong, 2 = ping-pong with the M phase at s_setprio 1 (both measured slower)
-  static const int fv = [] {
-    const char* e = getenv("IVIT_ATTN_FWD");
-    return e ? atoi(e) : 0;
-  }();
-  if (fv == 0)
-    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream), (const bf16*)qkv,
-              (int)N, (int)H, (bf16*)out, lse, 1.0f);
-  else if (fv == 2)
-    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_pp_kernel<1>, g, dim3(512), ivit_stream(stream), (const bf16*)qkv, (int)N,
-              (int)H, (bf16*)out, lse);
-  else
-    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_pp_kernel<0>, g, dim3(512), ivit_stream(stream), (const bf16*)qkv, (int)N,
-              (int)H, (bf16*)out, lse);
+  kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream), (const bf16*)qkv,
+            (int)N, (int)H, (bf16*)out, lse, 1.0f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
