@@ -293,12 +293,6 @@ int ivit_adamw_guarded(long n_tensors, void* const* params, void* const* grads, 
                        double beta1, double beta2, float eps, float weight_decay, float bc1, float bc2_sqrt,
                        const float* finite, const float* steps_in, float* steps_out, void* stream);
 
-/* Multi-tensor f32 copy, one launch: dst[t][0..numel[t]) = src[t][...] for t < n_tensors (device
- * pointer / size tables). Replaces the per-parameter gradient copies of torch
- * DistributedDataParallel's bucket fill (gradient_as_bucket_view) in ddp.GradBuckets. */
-int ivit_copy_multi(long n_tensors, const float* const* src, float* const* dst, const long* numel, long max_numel,
-                    void* stream);
-
 /* ---- Detection / intention loss (loss.py:58-206): assignment + focal + Smooth-L1 + CE. ----- */
 /* gt: [B, Gmax, 5] f32 padded, ngt[B] int32, gint[B, Gmax] int32. keep: [B, NA] f32 0/1 (dominant
  * intent keep mask) or null. stats (f32[8]): focal_sum, box_sum, ce_sum, num_pos, keep_sum, loss,

@@ -206,12 +206,6 @@ def test_single_process_buckets_are_views():
     assert all(any(p.grad.data_ptr() >= q and p.grad.data_ptr() < q + b_.flat.numel() * 4
                    for q, b_ in zip(sorted(ptrs), sorted(gb.buckets, key=lambda x: x.flat.data_ptr())))
                for p in m.parameters())
-    # zero_grad leaves every .grad None (autograd then hands over fresh gradients without a copy);
-    # the next finish() gathers them into the buckets again
+    m.a.weight.grad = None  # replaced outside the bucket → zero_grad re-attaches the view
     gb.zero_grad()
-    assert all(p.grad is None for p in m.parameters())
-    c, b, i = m(d["lidar_bev"], d["map_bev"])
-    _loss(c, b, i, None, None)["loss"].backward()
-    gb.finish()
-    views = {id(p): v.data_ptr() for p, v in gb._view.items()}
-    assert all(p.grad is None or p.grad.data_ptr() == views[id(p)] for p in m.parameters())
+    assert m.a.weight.grad is not None and float(m.a.weight.grad.abs().sum()) == 0.0

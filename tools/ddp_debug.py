@@ -1,0 +1,60 @@
+"""World-1 gloo group, GradBuckets(force_collectives) vs plain backward on the same bf16 model:
+per-parameter gradient differences (the direct bucket writes of ops.ViTBlockFn)."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, os.path.join(HERE, "..", "visiontransformer-intention-prediction_amd"))
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29541", RANK="0", WORLD_SIZE="1")
+dist.init_process_group("gloo", rank=0, world_size=1)
+import loss as L  # noqa: E402
+import model_vit  # noqa: E402
+import utils  # noqa: E402
+from ddp import GradBuckets  # noqa: E402
+from oracle import ivit_oracle as O  # noqa: E402
+from oracle.weights import make_state_dict, model_cfg  # noqa: E402
+
+H, W = 64, 96
+sd = make_state_dict(model_cfg(img_size=(H, W)), seed=0)
+
+
+def build():
+    m = model_vit.IntentNetViT(backbone_cfg={"img_size": (H, W), "drop_path_rate_lidar": 0.0, "drop_path_rate_map": 0.0})
+    m.load_state_dict(sd, strict=True)
+    return m.cuda().set_compute_dtype(torch.bfloat16).train()
+
+
+lidar, mp_, gts = O.synthetic_batch(2, (H, W), seed=100, grid_scale=H / 400.0)
+lidar, mp_ = lidar.cuda(), mp_.cuda()
+anchors = utils.generate_anchors(H, W, 8, device="cuda")
+keep = (torch.rand((2, anchors.shape[0]), generator=torch.Generator().manual_seed(7)) < 0.15).float()
+lossf = L.DetectionIntentionLoss()
+mb = build()
+c, b, i = mb(lidar, mp_)
+lossf(c, b, i, anchors, gts, intent_keep=keep)["loss"].backward()
+ref = {n: p.grad.detach().clone() for n, p in mb.named_parameters() if p.grad is not None}
+ma = build()
+for n_, p_ in ma.named_parameters():
+    p_._dbg_name = n_
+gb = GradBuckets(ma.parameters(), bucket_mb=float(sys.argv[1]) if len(sys.argv) > 1 else 8, force_collectives=True)
+gb.zero_grad()
+c, b, i = ma(lidar, mp_)
+lossf(c, b, i, anchors, gts, intent_keep=keep)["loss"].backward()
+gb.finish()
+torch.cuda.synchronize()
+errs = []
+for n, p in ma.named_parameters():
+    r = ref.get(n)
+    g = p.grad
+    if r is None:
+        continue
+    e = float((g - r).abs().max() / (r.abs().max() + 1e-30))
+    errs.append((e, n))
+errs.sort(reverse=True)
+for e, n in errs[:12]:
+    print(f"{e:.3e} {n}")
+print("n params", len(errs), "bad", sum(1 for e, _ in errs if e > 1e-6))

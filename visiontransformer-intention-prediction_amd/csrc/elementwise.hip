@@ -164,39 +164,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* c
   }
 }
 
-// Multi-tensor f32 copy: tensor t (blockIdx.y) of n[t] elements from src[t] to dst[t]; 16-B accesses
-// when both are 16-B aligned (uniform per tensor). The DDP gradient buckets gather a bucket's
-// freshly produced parameter gradients into the flat all-reduce buffer with one launch.
-__global__ __launch_bounds__(256) void copy_multi_kernel(const float* const* __restrict__ src,
-                                                         float* const* __restrict__ dst, const long* __restrict__ n) {
-  const int t = blockIdx.y;
-  const float* a = src[t];
-  float* b = dst[t];
-  const long m = n[t];
-  const long stride = (long)gridDim.x * blockDim.x;
-  long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (((((unsigned long)a) | ((unsigned long)b)) & 15) == 0) {
-    const long m4 = m / 4;
-    for (long i = i0; i < m4; i += stride) ((float4*)b)[i] = ((const float4*)a)[i];
-    for (long i = m4 * 4 + i0; i < m; i += stride) b[i] = a[i];
-  } else {
-    for (long i = i0; i < m; i += stride) b[i] = a[i];
-  }
-}
-
 }  // namespace
-
-extern "C" int ivit_copy_multi(long n_tensors, const float* const* src, float* const* dst, const long* numel,
-                               long max_numel, void* stream) {
-  if (n_tensors <= 0) return 0;
-  IVIT_CHECK_ARG(n_tensors < 65536 && src && dst && numel, "ivit_copy_multi: bad tables");
-  int gx = ivit_cdiv(ivit_cdiv(max_numel, 4), 256);
-  if (gx > 512) gx = 512;
-  if (gx < 1) gx = 1;
-  hipLaunchKernelGGL(copy_multi_kernel, dim3(gx, n_tensors), dim3(256), 0, ivit_stream(stream), src, dst, numel);
-  IVIT_LAUNCH_CHECK();
-  return 0;
-}
 
 extern "C" int ivit_cast(const void* x, int x_dtype, void* y, int y_dtype, long n, void* stream) {
   if (n <= 0) return 0;

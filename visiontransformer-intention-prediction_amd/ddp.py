@@ -53,18 +53,40 @@ def init_distributed(backend: str | None = None, force_group: bool = False):
 
 
 class _Bucket:
-    __slots__ = ("params", "flat", "views", "ready", "work", "events", "streams", "pending", "tables")
+    __slots__ = ("params", "flat", "ready", "work", "events", "streams")
 
-    def __init__(self, params, flat, views):
+    def __init__(self, params, flat):
         self.params = params
         self.flat = flat
-        self.views = views
         self.ready = 0
         self.work = None
         self.events = []
         self.streams = {}  # producing streams of this bucket's gradients (stream_id -> stream)
-        self.pending = []  # (param, fresh gradient) to gather into the flat buffer
-        self.tables = None  # (key, device pointer / size tables) of the last gather
+
+
+class GradSink:
+    """A parameter's slot in the gradient buckets, for ops that write the gradient themselves
+    (ops.ViTBlockFn: the block's weight / bias / LayerNorm gradients): ``claim()`` -> the bucket view
+    to overwrite (None when the view is not freshly zeroed this step, e.g. a second backward
+    without zero_grad — the op then returns its gradient to autograd, which adds it), ``done()``
+    after the writes are enqueued on the current stream (the bucket bookkeeping of the
+    post-accumulate hook, which does not run for a gradient the op returns as None)."""
+    __slots__ = ("gb", "p", "view")
+
+    def __init__(self, gb, p, view):
+        self.gb, self.p, self.view = gb, p, view
+
+    def claim(self):
+        gb = self.gb
+        if not gb.direct:
+            return None
+        if id(self.p) not in gb._fresh or self.p.grad is None or self.p.grad.data_ptr() != self.view.data_ptr():
+            return None
+        return self.view
+
+    def done(self):
+        self.gb._direct.add(id(self.p))
+        self.gb._on_grad(self.p, direct=True)
 
 
 class GradBuckets:
@@ -78,13 +100,10 @@ class GradBuckets:
         gb.finish()               # wait + average
         optimizer.step()
 
-    Gradients are NOT accumulated into the buckets by autograd: zero_grad() leaves every ``.grad``
-    None, so autograd hands each parameter its freshly computed gradient without a copy (the
-    AccumulateGrad "steal"), and when a bucket's last gradient arrives its gradients are gathered
-    into the flat buffer by ONE multi-tensor copy launch (ivit_copy_multi) on the comm stream, the
-    ``.grad`` fields become views of the buffer, and the buffer is all-reduced. (Pre-set bucket views
-    made autograd add every fresh gradient into the view: one add kernel per parameter, 327 per
-    step, plus the per-step zero fill of the buffers — about 1.5 ms of kernels per step.)
+    Every ``.grad`` is a persistent view into a flat bucket. Autograd accumulates a returned
+    gradient into it (one add kernel per parameter); the ViT blocks' gradients (288 of the 327
+    IntentNetViT parameters) skip that: their kernels write straight into the views
+    (``GradSink``, ``ops.grad_sinks``) and report completion themselves.
     """
 
     launched = 0  # collectives issued (tests)
@@ -99,7 +118,12 @@ class GradBuckets:
             raise ValueError("GradBuckets: duplicate parameters")
         cap = max(1, int(bucket_mb * (1 << 20)))
         self.buckets: list[_Bucket] = []
-        self._of, self._view, self._done = {}, {}, set()
+        self._of, self._ptr = {}, {}
+        self._fresh = set()  # ids of parameters whose bucket view is zeroed and not written yet
+        self._seen = set()  # ids of parameters whose gradient arrived in this backward
+        self._direct = set()  # ids of parameters written through their GradSink in this backward
+        self.direct = os.environ.get("IVIT_DDP_DIRECT", "1") == "1"
+        self.per_param_events = os.environ.get("IVIT_DDP_EVENTS", "stream") == "param"
         cur, cur_bytes = [], 0
         for p in reversed(ps):
             nb = p.numel() * p.element_size()
@@ -115,16 +139,14 @@ class GradBuckets:
     def _add(self, params):
         n = sum(p.numel() for p in params)
         flat = torch.zeros(n, dtype=params[0].dtype, device=params[0].device)
-        views, off = [], 0
+        b = _Bucket(params, flat)
+        off = 0
         for p in params:
-            v = flat[off:off + p.numel()].view_as(p)
-            views.append(v)
-            self._view[p] = v
-            p.grad = v
-            off += p.numel()
-        b = _Bucket(params, flat, views)
-        for p in params:
+            p.grad = flat[off:off + p.numel()].view_as(p)
             self._of[p] = b
+            self._ptr[p] = p.grad.data_ptr()
+            p._ivit_sink = GradSink(self, p, p.grad)
+            off += p.numel()
         self.buckets.append(b)
 
     @property
@@ -132,68 +154,52 @@ class GradBuckets:
         return sum(b.flat.numel() for b in self.buckets)
 
     def zero_grad(self):
-        """Every ``.grad`` None: the coming backward's gradients are taken over without a copy."""
         for b in self.buckets:
             if b.work is not None:
                 raise RuntimeError("GradBuckets.zero_grad() with collectives in flight; call finish() first")
+            b.flat.zero_()
             b.ready = 0
-            b.pending = []
             b.streams = {}
-            b.events = []
-            for p in b.params:
-                p.grad = None
-        self._done = set()
+            off = 0
+            for p in b.params:  # re-attach views if something replaced .grad
+                view = b.flat[off:off + p.numel()]
+                if p.grad is None or p.grad.data_ptr() != view.data_ptr():
+                    p.grad = view.view_as(p)
+                off += p.numel()
+        self._fresh = {id(p) for b in self.buckets for p in b.params}
+        self._seen = set()
+        self._direct = set()
 
-    def _on_grad(self, p):
+    def _on_grad(self, p, direct=False):
+        if not direct and id(p) in self._direct:
+            # written and counted by its op (GradSink.done); the engine still runs the post-accumulate
+            # hook for the None gradient the op returned
+            return
         b = self._of[p]
-        g = p.grad
-        if g is None:
-            raise RuntimeError("GradBuckets: post-accumulate hook without a gradient")
-        if id(p) in self._done:
-            raise RuntimeError("GradBuckets: a parameter received two gradients in one backward "
-                               "(call GradBuckets.zero_grad() before each backward)")
-        self._done.add(id(p))
+        if p.grad is None or p.grad.data_ptr() != self._ptr[p]:
+            raise RuntimeError("GradBuckets: a parameter's .grad was replaced outside the bucket "
+                               "(use GradBuckets.zero_grad(), not optimizer.zero_grad(set_to_none=True))")
+        self._fresh.discard(id(p))
+        if id(p) in self._seen:
+            raise RuntimeError(f"GradBuckets: a second gradient for one parameter in one backward "
+                               f"({getattr(p, '_dbg_name', tuple(p.shape))})")
+        self._seen.add(id(p))
         b.ready += 1
-        if g.data_ptr() != self._view[p].data_ptr():
-            b.pending.append((p, g))
         if not self.active:
             return
         if b.flat.is_cuda:
             # the two ViT streams produce gradients on two HIP streams (model_vit.stream_tokens):
-            # the bucket's gather + collective must wait for every producer, not just the last one.
-            # The hook runs after its gradient was enqueued, so one event per producing stream
-            # recorded when the bucket fills covers all of them
+            # the bucket's collective must wait for every producer, not just the last one. A
+            # gradient's accumulation is enqueued before its hook runs, so one event per producing
+            # stream recorded when the bucket fills covers all of them (a few waits per bucket
+            # instead of one event + wait per parameter)
             st = torch.cuda.current_stream(b.flat.device)
-            b.streams[st.stream_id] = st
+            if self.per_param_events:
+                b.events.append(st.record_event())
+            else:
+                b.streams[st.stream_id] = st
         if b.ready == len(b.params):
             self._launch(b)
-
-    def _gather(self, b):
-        """The bucket's fresh gradients into its flat buffer (current stream), ``.grad`` -> views."""
-        if not b.pending:
-            return
-        views = [self._view[p] for p, _ in b.pending]
-        srcs = [g if g.is_contiguous() and g.dtype == b.flat.dtype else g.contiguous().to(b.flat.dtype)
-                for _, g in b.pending]
-        if b.flat.is_cuda:
-            from _lib import lib, ptr, stream
-            key = tuple(s.data_ptr() for s in srcs) + tuple(v.data_ptr() for v in views)
-            if b.tables is None or b.tables[0] != key:
-                host = torch.tensor([s.data_ptr() for s in srcs] + [v.data_ptr() for v in views] +
-                                    [s.numel() for s in srcs], dtype=torch.int64).pin_memory()
-                b.tables = (key, host.to(b.flat.device, non_blocking=True))
-            tab, n = b.tables[1], len(srcs)
-            lib.ivit_copy_multi(n, ptr(tab[:n]), ptr(tab[n:2 * n]), ptr(tab[2 * n:]),
-                                max(s.numel() for s in srcs), stream())
-            cur = torch.cuda.current_stream(b.flat.device)
-            for s in srcs:
-                s.record_stream(cur)  # freed by autograd / below; reused only after this copy
-        else:
-            for v, s in zip(views, srcs):
-                v.copy_(s)
-        for (p, _), v in zip(b.pending, views):
-            p.grad = v
-        b.pending = []
 
     def _launch(self, b):
         if b.flat.is_cuda:
@@ -205,10 +211,8 @@ class GradBuckets:
             b.events = []
             b.streams = {}
             with torch.cuda.stream(comm):
-                self._gather(b)
                 b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
         else:
-            self._gather(b)
             b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
         GradBuckets.launched += 1
 
@@ -218,25 +222,18 @@ class GradBuckets:
         return self._comm
 
     def finish(self):
-        """Launch any bucket that did not fill (parameters without a gradient this step read zero,
-        as DistributedDataParallel's buckets), wait, and average."""
+        """Launch any bucket that did not fill (unused parameters), wait, and average."""
+        self._fresh = set()
+        self._seen = set()
+        self._direct = set()
         if not self.active:
             for b in self.buckets:
-                self._gather(b)
-                for p, v in zip(b.params, b.views):
-                    if id(p) not in self._done:
-                        v.zero_()
-                        p.grad = v
                 b.ready = 0
             return
         for b in self.buckets:
             if b.work is None:
-                missing = [(p, v) for p, v in zip(b.params, b.views) if id(p) not in self._done]
-                if b.flat.is_cuda:  # everything queued so far is final
+                if b.flat.is_cuda:  # unused parameters: everything queued so far is final
                     b.events = [torch.cuda.current_stream(b.flat.device).record_event()]
-                for p, v in missing:
-                    v.zero_()
-                    p.grad = v
                 self._launch(b)
         inv = 1.0 / self.world
         for b in self.buckets:
@@ -255,6 +252,10 @@ class GradBuckets:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for b in self.buckets:
+            for p in b.params:
+                if getattr(p, "_ivit_sink", None) is not None and p._ivit_sink.gb is self:
+                    del p._ivit_sink
 
 
 @torch.no_grad()

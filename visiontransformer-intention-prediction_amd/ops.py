@@ -144,16 +144,22 @@ def linear_wgrad(dy, x, cdt, want_bias=True):
     return dw, db
 
 
-def vit_block_wgrad(dy2, a, dh, x2, dyp, o, dyq, x1):
+def vit_block_wgrad(dy2, a, dh, x2, dyp, o, dyq, x1, outs=None):
     """The four weight + bias gradients of one bf16 timm Block (fc2, fc1, proj, qkv) in one grouped
     launch + one reduce (ivit_vit_block_wgrad): dW = dY^T X, db = colsum(dY) for
-    (dY, X) = (dx2s, a), (dh, ln2), (dx1s, o), (dqkv, ln1). -> [(dW, db)] * 4."""
+    (dY, X) = (dx2s, a), (dh, ln2), (dx1s, o), (dqkv, ln1). -> [(dW, db)] * 4. ``outs``: the eight
+    contiguous f32 destinations (dW2, db2, dW1, db1, dWp, dbp, dWq, dbq), e.g. gradient-bucket views."""
     M, D = dy2.shape
     Hd = a.shape[1]
     dev = dy2.device
     shapes = ((D, Hd), (Hd, D), (D, D), (3 * D, D))
-    dws = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in shapes]
-    dbs = [torch.empty((sh[0],), dtype=torch.float32, device=dev) for sh in shapes]
+    if outs is not None:
+        dws, dbs = list(outs[0::2]), list(outs[1::2])
+        assert all(t.is_contiguous() and t.dtype == torch.float32 and tuple(t.shape) == sh
+                   for t, sh in zip(dws, shapes))
+    else:
+        dws = [torch.empty(sh, dtype=torch.float32, device=dev) for sh in shapes]
+        dbs = [torch.empty((sh[0],), dtype=torch.float32, device=dev) for sh in shapes]
     ws = workspace(lib.ivit_vit_block_wgrad_workspace(M, D, Hd), dev)
     lib.ivit_vit_block_wgrad(M, D, Hd, ptr(dy2), ptr(a), ptr(dh), ptr(x2), ptr(dyp), ptr(o), ptr(dyq), ptr(x1),
                              ptr(dws[0]), ptr(dbs[0]), ptr(dws[1]), ptr(dbs[1]), ptr(dws[2]), ptr(dbs[2]), ptr(dws[3]),
@@ -187,17 +193,19 @@ def linear_resid_ln_fwd(a, w, b, resid, row_scale, rps, g, beta, eps):
     return x, y, mean, rstd
 
 
-def linear_dgrad_ln_bwd(dy, w, x, g, mean, rstd, dres=None, dx=None, xs_dtype=None, row_scale=None, rps=1):
+def linear_dgrad_ln_bwd(dy, w, x, g, mean, rstd, dres=None, dx=None, xs_dtype=None, row_scale=None, rps=1,
+                        dg=None, db=None):
     """dgrad G = dy [M, K] (bf16) @ w [K, 384] with the LayerNorm backward of (x, g, mean, rstd) in
     the epilogue: dx = dres + LN_bwd(G) (f32, may alias dres), optional bf16 dxs = dx * row_scale,
-    dgamma, dbeta — one kernel + the column reduction (ivit_linear_dgrad_ln_bwd)."""
+    dgamma, dbeta (into ``dg`` / ``db`` when given) — one kernel + the column reduction
+    (ivit_linear_dgrad_ln_bwd)."""
     M, K = dy.shape
     N = w.shape[1]
     if dx is None:
         dx = torch.empty((M, N), dtype=torch.float32, device=dy.device) if dres is None else dres
     dxs = torch.empty((M, N), dtype=xs_dtype, device=dy.device) if xs_dtype is not None else None
-    dg = torch.empty((N,), dtype=torch.float32, device=dy.device)
-    db = torch.empty((N,), dtype=torch.float32, device=dy.device)
+    dg = torch.empty((N,), dtype=torch.float32, device=dy.device) if dg is None else dg
+    db = torch.empty((N,), dtype=torch.float32, device=dy.device) if db is None else db
     ws = workspace(lib.ivit_linear_dgrad_ln_bwd_workspace(M, N), dy.device)
     lib.ivit_linear_dgrad_ln_bwd(ptr(dy), dy.stride(0), M, N, K, ptr(packed_weight_t(w)), ptr(x), x.stride(0), ptr(g),
                                  ptr(mean), ptr(rstd), ptr(dres), dres.stride(0) if dres is not None else N, ptr(dx),
@@ -705,6 +713,19 @@ class GradHandoff:
         return (t._cdata, t.data_ptr(), t._version)
 
 
+def grad_sinks(params):
+    """Destinations for writing these parameters' gradients directly (ddp.GradSink: gradient-bucket
+    views, freshly zeroed this step), or None when any parameter has none — the op then returns its
+    gradients to autograd as usual."""
+    sinks = [getattr(p, "_ivit_sink", None) for p in params]
+    if any(sk is None for sk in sinks):
+        return None
+    views = [sk.claim() for sk in sinks]
+    if any(v is None for v in views):
+        return None
+    return sinks, views
+
+
 class ViTBlockFn(torch.autograd.Function):
     """timm Block: x + dp1(proj(attn(norm1 x))); x + dp2(fc2(gelu(fc1(norm2 x)))).
     x: (B*N, D) f32 residual stream; GEMM operands in the compute dtype (f32 or bf16).
@@ -774,6 +795,8 @@ class ViTBlockFn(torch.autograd.Function):
         ctx.meta = meta
         ctx.q2 = q2
         ctx.panel = panel
+        # the parameters themselves (not saved tensors): their gradient-bucket sinks, if any
+        ctx.params = (n1w, n1b, qkvw, qkvb, pw, pb, n2w, n2b, f1w, f1b, f2w, f2b)
         ctx.hand_mine, ctx.hand_prev = (hand_mine, hand_prev) if panel else (None, None)
         if ctx.hand_mine is not None:
             ctx.hand_mine.scale, ctx.hand_mine.g, ctx.hand_mine.key = s2, None, None
@@ -802,10 +825,13 @@ class ViTBlockFn(torch.autograd.Function):
         dh = panel_dgrad_mul(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
         # bf16 row-panel blocks: the four weight gradients in one grouped launch after the dgrads
         group = ctx.panel and GROUP_WGRAD and fork is None
+        # DDP: the twelve parameter gradients straight into their bucket views (no autograd add)
+        direct = grad_sinks(ctx.params) if group else None
+        dv = direct[1] if direct is not None else [None] * 12
         g2 = None if group else _wgrad(fork, dx2s, a, cdt)
         if ctx.panel:  # fc1 dgrad with norm2's backward in the epilogue
             dx1, dx1s, dg2, dbe2 = linear_dgrad_ln_bwd(dh, f1w, x1, n2w, m2, r2, dres=dx2, dx=torch.empty_like(dx2),
-                                                       xs_dtype=cd, row_scale=s1, rps=N)
+                                                       xs_dtype=cd, row_scale=s1, rps=N, dg=dv[6], db=dv[7])
         else:
             dln2 = linear_dgrad(dh, w1, cdt, torch.float32)
             dx1, dx1s, dg2, dbe2 = layernorm_bwd(x1, n2w, m2, r2, dln2, dres=dx2, dx=torch.empty_like(dx2),
@@ -817,19 +843,25 @@ class ViTBlockFn(torch.autograd.Function):
         if ctx.panel:  # qkv dgrad with norm1's backward in the epilogue
             if hp is not None:  # also the previous block's bf16(dx0 * s2) (GradHandoff)
                 dx0, dx0s, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1, xs_dtype=cd,
-                                                           row_scale=hp.scale, rps=N)
+                                                           row_scale=hp.scale, rps=N, dg=dv[0], db=dv[1])
                 hp.g, hp.key = dx0s, GradHandoff.ident(dx0)
             else:
-                dx0, _, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1)
+                dx0, _, dg1, dbe1 = linear_dgrad_ln_bwd(dqkv, qkvw, x, n1w, m1, r1, dres=dx1, dx=dx1, dg=dv[0],
+                                                        db=dv[1])
         else:
             dln1 = linear_dgrad(dqkv, wq, cdt, torch.float32)
             dx0, _, dg1, dbe1 = layernorm_bwd(x, n1w, m1, r1, dln1, dres=dx1, dx=dx1)
         if group:
-            g2, g1, gp, gq = vit_block_wgrad(dx2s, a, dh, ln2, dx1s, o, dqkv, ln1)
+            outs = None if direct is None else (dv[10], dv[11], dv[8], dv[9], dv[4], dv[5], dv[2], dv[3])
+            g2, g1, gp, gq = vit_block_wgrad(dx2s, a, dh, ln2, dx1s, o, dqkv, ln1, outs=outs)
         else:
             gq = _wgrad(fork, dqkv, ln1, cdt)
         if fork is not None:
             fork.join((dx2s, dh, dx1s, dqkv, a, ln2, o, ln1))
+        if direct is not None:  # written into the buckets: nothing for autograd to accumulate
+            for sk in direct[0]:
+                sk.done()
+            return (dx0,) + (None,) * 22
         (dW2, db2), (dW1, db1), (dWp, dbp), (dWq, dbq) = g2, g1, gp, gq
         return (dx0, None, None, None, dg1, dbe1, dWq, dbq, dWp, dbp, dg2, dbe2, dW1, db1, dW2, db2, None, None,
                 None, None, None, None, None)
