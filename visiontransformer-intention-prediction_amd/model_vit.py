@@ -9,6 +9,8 @@ the exact-f32 parity path.
 """
 from __future__ import annotations
 
+import os
+
 import warnings
 
 import torch
@@ -136,10 +138,29 @@ class TwoStreamViTBackbone(nn.Module):
         s1, s2 = _side_streams(lidar_bev.device)
         s1.wait_stream(main)
         s2.wait_stream(main)
-        with torch.cuda.stream(s1):
-            tl = self.vit_lidar.forward_tokens(lidar_bev)
-        with torch.cuda.stream(s2):
-            tm = self.vit_map.forward_tokens(map_bev)
+        # block by block, alternating (vit.VisionTransformer.forward_tokens_steps): with each ViT
+        # launched whole, the backward engine enqueued the map stream's entire backward before the
+        # LiDAR stream's first kernel, and the LiDAR stream ran its last blocks alone
+        if not INTERLEAVE:  # A/B switch (IVIT_STREAM_INTERLEAVE=0): each ViT launched whole
+            with torch.cuda.stream(s1):
+                tl = self.vit_lidar.forward_tokens(lidar_bev)
+            with torch.cuda.stream(s2):
+                tm = self.vit_map.forward_tokens(map_bev)
+            live, out = [], {"l": tl, "m": tm}
+        else:
+            out = {}
+            live = [(s1, "l", self.vit_lidar.forward_tokens_steps(lidar_bev)),
+                    (s2, "m", self.vit_map.forward_tokens_steps(map_bev))]
+        while live:
+            for item in list(live):
+                st, key, gen = item
+                with torch.cuda.stream(st):
+                    try:
+                        next(gen)
+                    except StopIteration as stop:
+                        out[key] = stop.value
+                        live.remove(item)
+        tl, tm = out["l"], out["m"]
         main.wait_stream(s1)
         main.wait_stream(s2)
         lidar_bev.record_stream(s1)
@@ -223,6 +244,7 @@ class TwoStreamViTBackbone(nn.Module):
 
 
 _SIDE_STREAMS = {}
+INTERLEAVE = os.environ.get("IVIT_STREAM_INTERLEAVE", "1") == "1"
 
 
 def _side_streams(device):

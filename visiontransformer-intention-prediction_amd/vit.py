@@ -149,6 +149,20 @@ class VisionTransformer(nn.Module):
 
     def forward_tokens(self, x):
         """Patch embed + all blocks, without the final norm: (B*(Np+1), D) f32 residual stream."""
+        steps = self.forward_tokens_steps(x)
+        while True:
+            try:
+                next(steps)
+            except StopIteration as stop:
+                return stop.value
+
+    def forward_tokens_steps(self, x):
+        """forward_tokens as a generator that yields after the patch embedding and after every
+        block (the launches of one step are all enqueued on the current stream when it yields) and
+        returns the token stream: model_vit.stream_tokens interleaves the LiDAR and map ViTs block
+        by block, so their autograd nodes interleave in creation order and the backward engine
+        (which runs the ready node created last first) feeds both HIP streams evenly instead of
+        enqueueing one stream's whole backward before the other's."""
         B, C, H, W = x.shape
         if (H, W) != self.patch_embed.img_size:
             raise ValueError(f"Input size {(H, W)} != model img_size {self.patch_embed.img_size} (timm strict size)")
@@ -162,6 +176,7 @@ class VisionTransformer(nn.Module):
         # ... and in the backward, block i+1 hands block i its DropPath-scaled bf16 gradient
         hands = [ops.GradHandoff() for _ in self.blocks] if fuse and torch.is_grad_enabled() else None
         drawn = self._draw_drop_path(B, x.device)
+        yield
         for i, blk in enumerate(self.blocks):
             nxt = self.blocks[i + 1].norm1 if fuse and i + 1 < len(self.blocks) else None
             t, nxt_ln = blk.forward_flat(t, B, N, cdt, ln_in=ln, next_norm=nxt,
@@ -169,6 +184,7 @@ class VisionTransformer(nn.Module):
                                          hand_prev=hands[i - 1] if hands and i > 0 else None,
                                          drawn=drawn[i] if drawn is not None else None)
             ln = nxt_ln if nxt is not None else None
+            yield
         return t
 
     def forward_features(self, x):
