@@ -41,6 +41,37 @@ IVIT_DEV float vmax3(float a, float b, float c) {
   return d;
 }
 
+// Per-lane LDS byte offsets of the forward's fragment reads, computed once per kernel: the 128-B-row
+// chunk swizzle makes each read's address an XOR of lane bits with the k step (not base +
+// immediate), and the compiler re-derived them inside the tile loop (~40 VALU per 64-key tile of
+// a VALU-issue-bound loop). With these in registers every read is base + immediate (the stage and
+// the row block differences are multiples that leave the swizzle bits unchanged).
+//   k[ks]     : K fragment, row lane & 31, chunk 2 ks + hl        (+ 4096 per 32-key block)
+//   v[cb][h]  : V^T transposing read, column block cb (0 / 32), row half h (+ 2048 per 16 keys)
+struct FwdLdsOff {
+  unsigned k[4], v[2][2];
+};
+IVIT_DEV FwdLdsOff fwd_lds_off(int lane) {
+  FwdLdsOff o;
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) o.k[ks] = (unsigned)t_off(lane & 31, 2 * ks + hl);
+  const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int col = 32 * cb + 16 * (G & 1) + 4 * p;
+    const int r0 = 4 * (G >> 1) + q, c = col >> 3, e = (col & 7) * 2;
+    o.v[cb][0] = (unsigned)(t_off(r0, c) + e);
+    o.v[cb][1] = (unsigned)(t_off(r0 + 8, c) + e);
+  }
+  // opaque: kept in registers, not re-derived from the lane id at every use
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) asm volatile("" : "+v"(o.k[ks]));
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) asm volatile("" : "+v"(o.v[cb][0]), "+v"(o.v[cb][1]));
+  return o;
+}
+
 template <bool MASK>
 IVIT_DEV float tile_rowmax(f32x16 (&s)[2], int kbase, int N, int lane) {
   const int hl = lane >> 5;
@@ -84,11 +115,9 @@ IVIT_DEV void qk_tile_c(const char* kimg, const bf16x8 (&qf)[4], const f32x16& i
 // next step.
 IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], const f32x16 (&cur)[2],
                                 f32x16 (&nxt)[2], f32x16& o0, f32x16& o1, f32x16& lacc, const bf16x8& ones,
-                                const f32x16& negm, int lane, int kbase, int N) {
+                                const f32x16& negm, int lane, int kbase, int N, const FwdLdsOff& lo) {
   const int hl = lane >> 5;
-  auto kfrag = [&](int i) {
-    return *(const bf16x8*)(kimg + t_off(32 * (i >> 2) + (lane & 31), 2 * (i & 3) + hl));
-  };
+  auto kfrag = [&](int i) { return *(const bf16x8*)(kimg + lo.k[i & 3] + 4096 * (i >> 2)); };
   bf16x8 p[4];
   auto ex = [&](int i) { p[i >> 3][i & 7] = (bf16)fast_exp2(cur[i >> 4][i & 15]); };
   bf16x8 ka[8];
@@ -104,7 +133,12 @@ IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8
     __builtin_amdgcn_sched_barrier(0);
   }
   bf16x8 vf[8];
-  auto vread = [&](int f) { vf[f] = tr_acc_order(vimg, 16 * (f >> 1), 32 * (f & 1), lane); };
+  auto vread = [&](int f) {
+    union { s16x4 s[2]; bf16x8 v; } u;
+    u.s[0] = ds_tr(vimg + lo.v[f & 1][0] + 2048 * (f >> 1));
+    u.s[1] = ds_tr(vimg + lo.v[f & 1][1] + 2048 * (f >> 1));
+    vf[f] = u.v;
+  };
   vread(0);
   vread(1);
   __builtin_amdgcn_sched_barrier(0);
@@ -217,6 +251,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
 #pragma unroll
   for (int r = 0; r < 16; ++r) negm[r] = -m;
   f32x16 o0 = zero16(), o1 = zero16(), lacc = zero16();
+  const FwdLdsOff lo = fwd_lds_off(lane);
 
   // after S'_{j+1} - m and its row max mt: move m lazily; the next tile is shifted with it
   auto rescale = [&](float mt, f32x16(&nxt)[2]) {
@@ -249,7 +284,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
     if (j + 2 < nt) issue1(Kb, j + 2, smem[S][0]);
     if (j + 1 < nt) issue1(Vb, j + 1, smem[S ^ 1][1]);
     rescale(fwd_step_fenced6(smem[S ^ 1][0], smem[S][1], qf, cur, nxt, o0, o1, lacc, ones, negm, lane,
-                               (j + 1) * AK, N),
+                               (j + 1) * AK, N, lo),
               nxt);
   };
   using I0 = std::integral_constant<int, 0>;
