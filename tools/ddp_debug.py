@@ -18,7 +18,7 @@ from ddp import GradBuckets  # noqa: E402
 from oracle import ivit_oracle as O  # noqa: E402
 from oracle.weights import make_state_dict, model_cfg  # noqa: E402
 
-H, W = 64, 96
+H, W = (int(v) for v in os.environ.get("GRID", "64x96").split("x"))
 sd = make_state_dict(model_cfg(img_size=(H, W)), seed=0)
 
 

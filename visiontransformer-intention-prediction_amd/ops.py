@@ -878,6 +878,65 @@ def _unit_ln_params(n, dev):
     return _UNIT_LN[key]
 
 
+NECK_FORK = os.environ.get("IVIT_NECK_FORK", "0") == "1"
+_NECK_STREAMS = {}
+
+
+class _NeckGradFork:
+    """The neck's weight gradients (head conv, fusion convs, adapter linears: none of them on the
+    path to the ViT streams' input gradient) on a side stream, so they overlap the two ViT
+    backward passes instead of delaying them by ~1 ms: each runs after the work queued so far on
+    the calling (main) stream; the gradients are delivered straight to the parameters (a gradient-
+    bucket view through ddp.GradSink, else ``.grad`` set or accumulated on the side stream) and the
+    op returns None for them, so no autograd kernel on the main stream reads them early; the main
+    stream waits for the side stream at the end of the backward pass (an engine callback). With
+    gradient buckets the side stream is their communication stream (no extra hardware queue)."""
+
+    def __init__(self, dev, params):
+        self.main = torch.cuda.current_stream(dev)
+        sink = next((getattr(p, "_ivit_sink", None) for p in params if getattr(p, "_ivit_sink", None) is not None),
+                    None)
+        if sink is not None:
+            self.side = sink.gb._comm_stream(dev)
+        else:
+            key = (dev.index, self.main.cuda_stream)
+            if key not in _NECK_STREAMS:
+                _NECK_STREAMS[key] = torch.cuda.Stream(dev)
+            self.side = _NECK_STREAMS[key]
+        self.read = []
+
+    def run(self, fn, *args):
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            out = fn(*args)
+        self.read += [a for a in args if torch.is_tensor(a)]
+        return out
+
+    def deliver(self, p, g):
+        """g (computed on the side stream) becomes / is added to p's gradient."""
+        with torch.cuda.stream(self.side):
+            sink = getattr(p, "_ivit_sink", None)
+            if sink is not None:  # gradient buckets: into the view (fresh) or added to it
+                view = sink.claim()
+                if view is not None:
+                    view.copy_(g)
+                else:
+                    p.grad.add_(g)
+                sink.done()  # the bucket waits for the side stream
+            elif p.grad is None:
+                p.grad = g
+                g.record_stream(self.main)
+            else:
+                p.grad.add_(g)
+                p.grad.record_stream(self.side)
+
+    def close(self):
+        for t in self.read:
+            t.record_stream(self.side)
+        main, side = self.main, self.side
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
+
+
 class NeckFn(torch.autograd.Function):
     """Everything after the ViT blocks (model_vit.py:116-142,179-185; heads.py):
     final ViT norm (eps 1e-6) → drop CLS → adapter LN(eps 1e-5) → Linear → GELU for each
@@ -966,6 +1025,18 @@ class NeckFn(torch.autograd.Function):
         M = B * Np
         dev = cat.device
         G = {}
+        forked = set()
+        fork = _NeckGradFork(dev, list(P.values())) if NECK_FORK and cat.is_cuda else None
+
+        def cw(n_, dy_, x_, Cin_, Cout_, k_):
+            # a fusion conv's weight gradient (+ unpack), on the fork when there is one
+            def f(dy_, x_):
+                gp_, _ = conv_wgrad(dy_, x_, B, Hf, Wf, Cin_, Cout_, k_, cdt)
+                return unpack_conv_grad(gp_, Cout_, Cin_, k_)
+            G[n_] = fork.run(f, dy_, x_) if fork is not None else f(dy_, x_)
+            if fork is not None:
+                forked.add(n_)
+
         if A == 0:
             dx = gouts[0].contiguous().float()
         else:
@@ -977,11 +1048,18 @@ class NeckFn(torch.autograd.Function):
             lib.ivit_merge_heads_grad(ptr(dcls.contiguous()), ptr(dbox.contiguous()), ptr(dint.contiguous()), M, A,
                                       K, ptr(dh), Cq, dt(dh), stream())
             Cin = x_last.shape[1]
-            gp, dbh = conv_wgrad(dh, x_last, B, Hf, Wf, Cin, Cp, 3, cdt, want_bias=True)
             Cd, Ci = A * 7, A * K
-            gw = unpack_conv_grad(gp, Cd + Ci, Cin, 3)
-            G["det_head.conv.weight"], G["intention_head.conv.weight"] = gw[:Cd], gw[Cd:]
-            G["det_head.conv.bias"], G["intention_head.conv.bias"] = dbh[:Cd].clone(), dbh[Cd:Cd + Ci].clone()
+
+            def head_wgrad(dh, x_last):
+                gp, dbh = conv_wgrad(dh, x_last, B, Hf, Wf, Cin, Cp, 3, cdt, want_bias=True)
+                gw = unpack_conv_grad(gp, Cd + Ci, Cin, 3)
+                return gw[:Cd], gw[Cd:], dbh[:Cd].clone(), dbh[Cd:Cd + Ci].clone()
+
+            hw = fork.run(head_wgrad, dh, x_last) if fork is not None else head_wgrad(dh, x_last)
+            for n_, g_ in zip(("det_head.conv.weight", "intention_head.conv.weight", "det_head.conv.bias",
+                               "intention_head.conv.bias"), hw):
+                G[n_] = g_
+                forked.add(n_) if fork is not None else None
             dx = conv_dgrad(dh, B, Hf, Wf, whp, cdt, torch.float32, w=wh, dy_zero_pad=True)
         for li in reversed(range(layers)):
             p = f"fusion_block.{li}."
@@ -990,19 +1068,16 @@ class NeckFn(torch.autograd.Function):
             dc2, dres, G[p + "bn2.weight"], G[p + "bn2.bias"] = bn_backward(c2, out, dx, s2, P[p + "bn2.weight"], True,
                                                                             cd, want_dr=True)
             Cm_ = c2.shape[1]
-            gp2, _ = conv_wgrad(dc2, r1, B, Hf, Wf, r1.shape[1], Cm_, 3, cdt)
-            G[p + "conv2.weight"] = unpack_conv_grad(gp2, Cm_, r1.shape[1], 3)
+            cw(p + "conv2.weight", dc2, r1, r1.shape[1], Cm_, 3)
             dr1 = conv_dgrad(dc2, B, Hf, Wf, packs[p + "2"], cdt, torch.float32, w=P[p + "conv2.weight"])
             dc1, _, G[p + "bn1.weight"], G[p + "bn1.bias"] = bn_backward(c1, r1, dr1, s1, P[p + "bn1.weight"], True, cd)
-            gp1, _ = conv_wgrad(dc1, x, B, Hf, Wf, x.shape[1], Cm_, 3, cdt)
-            G[p + "conv1.weight"] = unpack_conv_grad(gp1, Cm_, x.shape[1], 3)
+            cw(p + "conv1.weight", dc1, x, x.shape[1], Cm_, 3)
             dxa = conv_dgrad(dc1, B, Hf, Wf, packs[p + "1"], cdt, torch.float32, w=P[p + "conv1.weight"])
             if has_ds:
                 dd, sd, idn = bns[p + "ds"]
                 ddd, _, G[p + "downsample.1.weight"], G[p + "downsample.1.bias"] = bn_backward(
                     dd, idn, dres, sd, P[p + "downsample.1.weight"], False, cd)
-                gpd, _ = conv_wgrad(ddd, x, B, Hf, Wf, x.shape[1], Cm_, 1, cdt)
-                G[p + "downsample.0.weight"] = unpack_conv_grad(gpd, Cm_, x.shape[1], 1)
+                cw(p + "downsample.0.weight", ddd, x, x.shape[1], Cm_, 1)
                 dxb = conv_dgrad(ddd, B, Hf, Wf, packs[p + "ds"], cdt, torch.float32,
                                  w=P[p + "downsample.0.weight"])
             else:
@@ -1020,7 +1095,11 @@ class NeckFn(torch.autograd.Function):
             C = wa.shape[0]
             dp = dpre[:, c0:c0 + C]
             dz = linear_dgrad(dp, wa, cdt, torch.float32)
-            G[f"adapter_{s}.1.weight"], G[f"adapter_{s}.1.bias"] = linear_wgrad(dp, z, cdt)
+            if fork is not None:
+                G[f"adapter_{s}.1.weight"], G[f"adapter_{s}.1.bias"] = fork.run(linear_wgrad, dp, z, cdt)
+                forked.update((f"adapter_{s}.1.weight", f"adapter_{s}.1.bias"))
+            else:
+                G[f"adapter_{s}.1.weight"], G[f"adapter_{s}.1.bias"] = linear_wgrad(dp, z, cdt)
             dy, _, G[f"adapter_{s}.0.weight"], G[f"adapter_{s}.0.bias"] = layernorm_bwd(
                 y, P[f"adapter_{s}.0.weight"], ma, ra, dz)
             dt_ = torch.empty_like(t)
@@ -1028,6 +1107,10 @@ class NeckFn(torch.autograd.Function):
             _, _, G[f"vit_{s}.norm.weight"], G[f"vit_{s}.norm.bias"] = layernorm_bwd(
                 t, P[f"vit_{s}.norm.weight"], mf, rf, dy, dx=dt_, rowmap=(Np, Np + 1, 1))
             outs[s] = dt_
+        if fork is not None:
+            for n_ in forked:
+                fork.deliver(P[n_], G.pop(n_))
+            fork.close()
         grads = [G.get(n) for n in names]
         del ctx.st, ctx.P
         return (outs["lidar"], outs["map"], None) + tuple(grads)
