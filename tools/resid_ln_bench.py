@@ -46,3 +46,19 @@ for K in (384, 1536):
     fl = 2.0 * M * N * K
     print(f"K={K:5d}  GEMM+resid {t_g:6.1f} us   + LayerNorm {t2:6.1f} us   fused {t1:6.1f} us "
           f"({fl / t1 / 1e6:.0f} TF/s)", flush=True)
+
+# backward form: dgrad G = dY @ W (K = 1536: fc1's dgrad; 1152: qkv's) + LayerNorm backward, with
+# the residual-stream gradient dres added and the bf16 copy written (the in-step call shapes)
+for K in (1536, 1152):
+    dy = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16)
+    w = torch.randn(K, N, device="cuda") / K ** 0.5
+    x = torch.randn(M, N, device="cuda")
+    g = torch.ones(N, device="cuda") + 0.1 * torch.randn(N, device="cuda")
+    mean, rstd = x.mean(1), 1.0 / (x.var(1, unbiased=False) + 1e-6).sqrt()
+    dres = torch.randn(M, N, device="cuda")
+    dx = torch.empty_like(dres)
+    s = torch.ones(8, device="cuda")
+    t = timeit(lambda: ops.linear_dgrad_ln_bwd(dy, w, x, g, mean, rstd, dres=dres, dx=dx, xs_dtype=torch.bfloat16,
+                                               row_scale=s, rps=4501))
+    fl = 2.0 * M * N * K
+    print(f"bwd K={K:5d}  dgrad + LN bwd (+ colreduce) {t:6.1f} us ({fl / t / 1e6:.0f} TF/s)", flush=True)

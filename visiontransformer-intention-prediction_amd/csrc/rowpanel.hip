@@ -138,6 +138,15 @@ IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA&
 //   dXs = bf16(dX * scale[m / rps]) (optional), per-workgroup partial column sums of dY xh / dY.
 // Pointer roles in BWD: R = dres (nullable), X = X (read), Y = dXs, mean / rstd read, bias unused,
 // part = [gridDim.x][2][384] partials (reduced by colreduce_kernel).
+#ifndef RP_PF_FWD
+#define RP_PF_FWD 3
+#endif
+#ifndef RP_PF_BWD
+#define RP_PF_BWD 2
+#endif
+#ifndef RP_PFB_BWD
+#define RP_PFB_BWD 1
+#endif
 template <bool BWD, bool ST = false>
 __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
     const bf16* __restrict__ A, long lda, int M, int K, const u32x4* __restrict__ wpack,
@@ -168,7 +177,8 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
 #pragma unroll
   for (int e = 0; e < 12; ++e) { gm[e] = gamma[c0 + e]; bt[e] = BWD ? 0.f : beta[c0 + e]; }
   // row operands of block mb + 1 (residual; or X and dres) are loaded while block mb is reduced
-  struct RowIn { float4 a[3], b[3]; float s, mu, rs; };
+  struct RowIn { float4 a[3]; float s, mu, rs; };
+  struct RowB { float4 b[3]; };  // BWD: dres
   auto load_row = [&](int mb, RowIn& in) {
     const int m = min(m0 + 16 * mb + r, M - 1);
     in.s = scale ? scale[m / rps] : 1.f;
@@ -180,25 +190,43 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
       const float* xrow = X + (long)m * ldx + c0;
 #pragma unroll
       for (int e = 0; e < 3; ++e) in.a[e] = *(const float4*)(xrow + 4 * e);
-      if (R) {
-        const float* drow = R + (long)m * ldr + c0;
-#pragma unroll
-        for (int e = 0; e < 3; ++e) in.b[e] = *(const float4*)(drow + 4 * e);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 3; ++e) in.b[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
       in.mu = mean[m];
       in.rs = rstd[m];
+    }
+  };
+  auto load_b = [&](int mb, RowB& in) {
+    const int m = min(m0 + 16 * mb + r, M - 1);
+    if (R) {
+      const float* drow = R + (long)m * ldr + c0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) in.b[e] = *(const float4*)(drow + 4 * e);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 3; ++e) in.b[e] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   float pg[12], pb[12];  // BWD: this thread's partial column sums of dY xh, dY
 #pragma unroll
   for (int e = 0; e < 12; ++e) { pg[e] = 0.f; pb[e] = 0.f; }
-  RowIn in;
-  load_row(0, in);
+  // The row operands are prefetched PF blocks ahead (a ring of register sets; the loop is
+  // unrolled, so the compiler's counted waits stay exact): one block in flight per CU is 24 KiB
+  // (48 with BWD's two operands), which pulls the residual at ~10 GB/s per CU — the epilogue was
+  // bound by that latency, not by HBM bandwidth (r03 stamps: 23 us for 0.55 MB per workgroup).
+  constexpr int PF = BWD ? RP_PF_BWD : RP_PF_FWD, PFB = BWD ? RP_PFB_BWD : 1;
+  RowIn ring[PF];
+  RowB ringb[PFB];
+#pragma unroll
+  for (int i = 0; i < PF; ++i)
+    if (i < RP_MB) load_row(i, ring[i]);
+  if constexpr (BWD) {
+#pragma unroll
+    for (int i = 0; i < PFB; ++i)
+      if (i < RP_MB) load_b(i, ringb[i]);
+  }
 #pragma unroll
   for (int mb = 0; mb < RP_MB; ++mb) {
+    RowIn& in = ring[mb % PF];
+    RowB& inb = ringb[mb % PFB];
 #pragma unroll
     for (int j = 0; j < NBW; ++j)
 #pragma unroll
@@ -220,7 +248,7 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
       float x[12];
 #pragma unroll
       for (int e = 0; e < 12; ++e) x[e] = u[e] + sc * t[e];
-      if (mb + 1 < RP_MB) load_row(mb + 1, in);
+      if (mb + PF < RP_MB) load_row(mb + PF, in);
       float sum = 0.f;
 #pragma unroll
       for (int e = 0; e < 12; ++e) sum += x[e];
@@ -252,10 +280,11 @@ __global__ __launch_bounds__(512, 1) void rowpanel_ln_kernel(
       float dr[12];
 #pragma unroll
       for (int e = 0; e < 12; e += 4) {
-        const float4 q = in.b[e / 4];
+        const float4 q = inb.b[e / 4];
         dr[e] = q.x; dr[e + 1] = q.y; dr[e + 2] = q.z; dr[e + 3] = q.w;
       }
-      if (mb + 1 < RP_MB) load_row(mb + 1, in);
+      if (mb + PFB < RP_MB) load_b(mb + PFB, inb);
+      if (mb + PF < RP_MB) load_row(mb + PF, in);
       float xh[12], gy[12], s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < 12; ++e) {
