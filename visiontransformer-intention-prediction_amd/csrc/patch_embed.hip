@@ -387,16 +387,10 @@ IVIT_DEV long wg_unit_start(int w, long U) { return (long)w * U / WG_NWG; }
 // stream the same patch chunks in the same order, so a dtok chunk is fetched into that XCD's L2
 // once for the ~32 pairs being reduced there together, instead of once per pair from the
 // Infinity Cache (the persistent form moved 4 GB of dtok per LiDAR launch: 2.58x the raster).
-// SPLIT = -1 (XCD-sharded persistent form): workgroup w = 8 c + x (x = its XCD under round-robin
-// placement) takes the chunk range [J x / 8, J (x + 1) / 8) of EVERY pair, split evenly over the
-// XCD's 32 workgroups (pair-major; a range meets at most NS pairs: slab [w][NS][D][128]). The
-// token-gradient rows an XCD reads are then one eighth of dtok (3.5 MB at the bench shape), held
-// in that XCD's L2 for all its pairs instead of streamed from the Infinity Cache once per pair.
 template <int NT, int NBK, int SPLIT>
 __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restrict__ dtok,
                                                             const float* __restrict__ img, int C, int H, int W,
-                                                            int Wp, int Np, int M, int J, float* __restrict__ slab,
-                                                            int NS = 2) {
+                                                            int Wp, int Np, int M, int J, float* __restrict__ slab) {
   constexpr int D = NT * 128, NBN = 3;
   constexpr int TPW = NT;                            // dtok pieces (4 rows x 256 B) per wave per unit
   constexpr int RPW = 2;                             // raster pieces per wave per unit
@@ -413,18 +407,8 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
   const int ng = wv % NGRP, kg = wv / NGRP;
   const long U = (long)((C + 1) / 2) * J;
   const int w = blockIdx.x;
-  int g0, j0, nu, jlo = 0, jhi = J;  // jlo / jhi: the chunk range of this workgroup's pairs
-  if constexpr (SPLIT < 0) {
-    const int x = w & 7, c = w >> 3;
-    jlo = (int)((long)J * x / 8);
-    jhi = (int)((long)J * (x + 1) / 8);
-    const int Jx = jhi - jlo;
-    const long Ux = (long)((C + 1) / 2) * Jx, v0 = (long)c * Ux / 32, v1 = (long)(c + 1) * Ux / 32;
-    nu = (int)(v1 - v0);
-    g0 = Jx > 0 ? (int)(v0 / Jx) : 0;
-    j0 = jlo + (int)(v0 - (long)g0 * Jx);
-    slab += (long)w * NS * D * 128;
-  } else if constexpr (SPLIT > 0) {
+  int g0, j0, nu;
+  if constexpr (SPLIT > 0) {
     g0 = w / SPLIT;
     const int s = w - g0 * SPLIT;
     j0 = (int)((long)s * J / SPLIT);
@@ -450,7 +434,7 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
   // A cursor = (g, j) of one unit, advanced by one unit per iteration; the lane positions of
   // its 32-patch chunk advance by 32 patches with carries.
   struct Cur { int g, j; };
-  auto cnext = [&](Cur& c) { if (++c.j == jhi) { c.j = jlo; ++c.g; } };
+  auto cnext = [&](Cur& c) { if (++c.j == J) { c.j = 0; ++c.g; } };
   // raster lane position: patch (lane >> 1) of the chunk as (b, gy, gx)
   struct RPos { int b, gy, gx; };
   auto rpos_at = [&](int m) { RPos r; r.b = m / Np; const int pi = m - r.b * Np; r.gy = pi / Wp; r.gx = pi - r.gy * Wp; return r; };
@@ -461,11 +445,11 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
   // dtok lane rows: patches row_i of the chunk as (b, p), i = the wave's pieces
   struct TPos { int b, p; };
   auto tadv = [&](TPos& t) { t.p += WG_MU; while (t.p >= Np) { t.p -= Np; ++t.b; } };
-  const RPos r_first = rpos_at(min(jlo * WG_MU + (lane >> 1), M - 1));
+  const RPos r_first = rpos_at(min(lane >> 1, M - 1));
   TPos t_first[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
-    const int row = ((wv * TPW + i) & 7) * 4 + (lane >> 4), m = min(jlo * WG_MU + row, M - 1);
+    const int row = ((wv * TPW + i) & 7) * 4 + (lane >> 4), m = min(row, M - 1);
     t_first[i].b = m / Np; t_first[i].p = m - t_first[i].b * Np;
   }
   // cursors: raster issue (runs 4 ahead of compute), dtok issue (2 ahead), convert (1 ahead), compute
@@ -493,7 +477,7 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
       glds_v<true>(src, st + q * 1024);
     }
     cnext(cr);
-    if (cr.j == jlo) rp = r_first; else radv(rp);
+    if (cr.j == 0) rp = r_first; else radv(rp);
   };
   // dtok rows of the dtok cursor's unit: piece = (image ti = 128-column block, 4-row group)
   auto issue_t = [&](int k) {
@@ -510,7 +494,7 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
     cnext(ct);
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
-      if (ct.j == jlo) tp[i] = t_first[i];
+      if (ct.j == 0) tp[i] = t_first[i];
       else tadv(tp[i]);
     }
   };
@@ -673,42 +657,6 @@ __global__ __launch_bounds__(256) void patch_wgrad_reduce_split_kernel(const flo
   *o = accumulate ? *o + s : s;
 }
 
-// XCD-sharded form: dW[n][g*128 + k] (+)= sum over the XCD shards x, then over the workgroups of
-// shard x whose unit range meets pair g (fixed order: deterministic). Block-uniform pair g.
-__global__ __launch_bounds__(256) void patch_wgrad_reduce_xs_kernel(const float* __restrict__ slab, int C, int J,
-                                                                    int D, int NS, float* __restrict__ dW,
-                                                                    int accumulate) {
-  const int G = (C + 1) / 2;
-  const long per = (long)D * 128, i0 = (long)blockIdx.x * 256;
-  const int g = (int)(i0 / per);
-  if (g >= G) return;
-  const int e = (int)(i0 - (long)g * per) + threadIdx.x, n = e >> 7, k = e & 127;
-  float s = 0.f;
-  for (int x = 0; x < 8; ++x) {
-    const int Jx = (int)((long)J * (x + 1) / 8 - (long)J * x / 8);
-    if (Jx == 0) continue;
-    const long Ux = (long)G * Jx, ga = (long)g * Jx, gb = ga + Jx;
-    // first workgroup c of the shard whose range [c Ux / 32, (c + 1) Ux / 32) ends past ga
-    int c = (int)(ga * 32 / Ux);
-    while (c > 0 && (long)c * Ux / 32 > ga) --c;
-    while (c < 32 && (long)(c + 1) * Ux / 32 <= ga) ++c;
-    for (; c < 32; ++c) {
-      const long v0 = (long)c * Ux / 32, v1 = (long)(c + 1) * Ux / 32;
-      if (v0 >= gb) break;
-      if (v1 <= v0) continue;  // an empty range (tiny grids) wrote nothing
-      const int g0 = (int)(v0 / Jx);
-      s += slab[((long)(c * 8 + x) * NS + (g - g0)) * per + e];
-    }
-  }
-  if (2 * g + (k >> 6) >= C) return;
-  float* o = dW + (long)n * C * 64 + (long)g * 128 + k;
-  *o = accumulate ? *o + s : s;
-}
-
-// slab tiles per workgroup of the XCD-sharded form: a range of <= ceil(G Jx / 32) units meets at
-// most ceil(range / Jx) + 1 pairs
-long patch_wgrad_xs_ns(long C) { return ((C + 1) / 2 + 31) / 32 + 2; }
-
 // splits along the patches (an instantiated SPLIT): a multiple of 8 (one XCD per split residue)
 // giving >= ~256 workgroups
 long patch_wgrad_splits(long C) {
@@ -722,9 +670,7 @@ long patch_wgrad_raster_workspace(long D) { return (long)WG_NWG * 2 * D * 128 * 
 long patch_wgrad_raster_workspace2(long C, long D) {
   const long split = patch_wgrad_splits(C) * ((C + 1) / 2) * D * 128 * 4;
   const long pers = patch_wgrad_raster_workspace(D);
-  const long xs = (long)WG_NWG * patch_wgrad_xs_ns(C) * D * 128 * 4;
-  const long m = split > pers ? split : pers;
-  return xs > m ? xs : m;
+  return split > pers ? split : pers;
 }
 
 bool patch_wgrad_raster_ok(long B, long C, long H, long W, long D) {
@@ -744,18 +690,13 @@ int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long 
   // Default: the persistent form. The split-along-patches form (IVIT_PATCH_WGRAD_SPLIT=1) cuts the
   // dtok bytes fetched from the Infinity Cache but not the bytes each CU takes in by LDS-DMA (16 KiB
   // raster + 24 KiB dtok per unit either way), which bound both: measured in-step 1.08 vs 1.01 ms
-  // (LiDAR), 48.74-48.84 vs 48.64-48.69 ms per step.
+  // (LiDAR), 48.74-48.84 vs 48.64-48.69 ms per step. Round 4, isolated (LiDAR shape):
+  // persistent 1.116-1.121 ms, split 1.163, an XCD-sharded persistent form (each XCD's workgroups
+  // on one eighth of the patch chunks for every pair: its dtok rows L2-resident) 1.387 (removed);
+  // diagnostic builds with the dtok chunk fixed (L2-resident) 0.988 and the raster chunk fixed
+  // 1.002 ms — neither operand's source bounds the kernel by itself.
   const char* sv = getenv("IVIT_PATCH_WGRAD_SPLIT");
   const int mode = sv ? atoi(sv) : 0;
-  if (mode == 2 && J >= 8) {  // XCD-sharded persistent form
-    const int NS = (int)patch_wgrad_xs_ns(C);
-    if ((D * 128) % 256) return IVIT_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, -1>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H,
-                       (int)W, Wp, Np, M, J, slab, NS);
-    hipLaunchKernelGGL(patch_wgrad_reduce_xs_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, (int)C, J,
-                       (int)D, NS, dW, accumulate);
-    return 0;
-  }
   if (mode != 1) {
     if ((D * 128) % 256) return IVIT_ERR_UNSUPPORTED;  // the reduce's block-uniform pair
     hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, 0>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H,

@@ -138,11 +138,14 @@ IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA&
 //   dXs = bf16(dX * scale[m / rps]) (optional), per-workgroup partial column sums of dY xh / dY.
 // Pointer roles in BWD: R = dres (nullable), X = X (read), Y = dXs, mean / rstd read, bias unused,
 // part = [gridDim.x][2][384] partials (reduced by colreduce_kernel).
+#ifndef RP_WPF
+#define RP_WPF 1
+#endif
 #ifndef RP_PF_FWD
 #define RP_PF_FWD 3
 #endif
 #ifndef RP_PF_BWD
-#define RP_PF_BWD 2
+#define RP_PF_BWD 1
 #endif
 #ifndef RP_PFB_BWD
 #define RP_PFB_BWD 1
@@ -504,16 +507,24 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
     for (int j = 0; j < NBW; ++j)
       bv[j] = (!epi_reads_p(EPI) && bias) ? bias[n0 + (wv * NBW + j) * 16 + (lane & 15)] : 0.f;
     const float qs = (EPI == EPI_QS && n0 < qcols) ? qscale : 1.f;  // qcols is a multiple of 384 (of CW)
-    uint2 pv[3];
+    // P rows prefetched WPF blocks ahead (one block of a 192-column chunk is only 6 KiB: at one
+    // block in flight the epilogue waited on the read latency, ~11 us of an 18-us workgroup)
+    constexpr int WPF = RP_WPF;
+    uint2 pvr[WPF][3];
     auto load_pre = [&](int mb) {
       const int m = min(m0 + 16 * mb + r, M - 1);
       const bf16* prow = P + (long)m * ldp + n0 + c0;
 #pragma unroll
-      for (int e = 0; e < 3; ++e) pv[e] = *(const uint2*)(prow + 4 * e);
+      for (int e = 0; e < 3; ++e) pvr[mb % WPF][e] = *(const uint2*)(prow + 4 * e);
     };
-    if constexpr (epi_reads_p(EPI)) load_pre(0);
+    if constexpr (epi_reads_p(EPI)) {
+#pragma unroll
+      for (int i = 0; i < WPF; ++i)
+        if (i < RP_MB) load_pre(i);
+    }
 #pragma unroll
     for (int mb = 0; mb < RP_MB; ++mb) {
+      uint2 (&pv)[3] = pvr[mb % WPF];
 #pragma unroll
       for (int j = 0; j < NBW; ++j)
 #pragma unroll
@@ -536,7 +547,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
 #pragma unroll
           for (int k = 0; k < 4; ++k) h[4 * e + k] = (float)q.h[k];
         }
-        if (mb + 1 < RP_MB) load_pre(mb + 1);
+        if (mb + WPF < RP_MB) load_pre(mb + WPF);
       }
       if (m < M) {
         unsigned y[6], p[6];

@@ -1108,8 +1108,12 @@ class NeckFn(torch.autograd.Function):
                 t, P[f"vit_{s}.norm.weight"], mf, rf, dy, dx=dt_, rowmap=(Np, Np + 1, 1))
             outs[s] = dt_
         if fork is not None:
-            for n_ in forked:
-                fork.deliver(P[n_], G.pop(n_))
+            # in parameter order: a delivery can complete a gradient bucket and launch its collective,
+            # and every rank must launch the buckets in the same order (a set's order follows the
+            # per-process string hash)
+            for n_ in names:
+                if n_ in forked:
+                    fork.deliver(P[n_], G.pop(n_))
             fork.close()
         grads = [G.get(n) for n in names]
         del ctx.st, ctx.P
