@@ -142,7 +142,7 @@ IVIT_DEV void panel_mainloop(f32x4 (&acc)[RP_MB][NBW], char* smem, const PanelA&
 #define RP_WPF 1
 #endif
 #ifndef RP_PF_FWD
-#define RP_PF_FWD 3
+#define RP_PF_FWD 1
 #endif
 #ifndef RP_PF_BWD
 #define RP_PF_BWD 1
