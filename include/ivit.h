@@ -292,6 +292,15 @@ int ivit_adamw_guarded(long n_tensors, void* const* params, void* const* grads, 
                        void* const* exp_avg_sq, void* const* shadows, const long* sizes, long max_size, float lr,
                        double beta1, double beta2, float eps, float weight_decay, float bc1, float bc2_sqrt,
                        const float* finite, const float* steps_in, float* steps_out, void* stream);
+/* ivit_adamw_guarded's update over a flat chunk list: chunks (device int32 [n_chunks][2]) =
+ * (tensor t, chunk c) for every c < ceil(sizes[t] / ivit_adamw_chunk_elems()) of every tensor; one
+ * workgroup per chunk (no idle workgroups for the small tensors), 16-B accesses where the arrays
+ * allow. shadows may be null or hold null entries. Bit-identical to ivit_adamw_guarded. */
+long ivit_adamw_chunk_elems(void);
+int ivit_adamw_chunked(long n_tensors, void* const* params, void* const* grads, void* const* exp_avg,
+                       void* const* exp_avg_sq, void* const* shadows, const long* sizes, const int* chunks,
+                       long n_chunks, float lr, double beta1, double beta2, float eps, float weight_decay, float bc1,
+                       float bc2_sqrt, const float* finite, const float* steps_in, float* steps_out, void* stream);
 
 /* ---- Detection / intention loss (loss.py:58-206): assignment + focal + Smooth-L1 + CE. ----- */
 /* gt: [B, Gmax, 5] f32 padded, ngt[B] int32, gint[B, Gmax] int32. keep: [B, NA] f32 0/1 (dominant

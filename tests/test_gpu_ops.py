@@ -716,6 +716,53 @@ def test_adamw_matches_torch():
         assert _rel(q.detach(), p.detach()) < 1e-6
 
 
+@pytest.mark.parametrize("guard", ["host", "device"])
+def test_adamw_chunked_bit_identical_to_guarded(guard):
+    """ivit_adamw_chunked (FusedAdamW's launch: one workgroup per 4096-element chunk, 16-B
+    accesses where allowed) against the 2D-grid ivit_adamw_guarded on the same state: bit-identical
+    parameters, moments, bf16 shadows and step counts — tensors of several chunks with a ragged
+    last one, ones smaller than a chunk, 4-B-offset (scalar-path) views, shadows present / absent,
+    the host bias correction and the device step counts with finite = 1 and 0."""
+    from _lib import lib, ptr, stream
+    g0 = torch.Generator().manual_seed(3)
+    flat = [torch.randn(4 * 20000 + 7, generator=g0) for _ in range(4)]  # p, g, m, v storage
+    shapes = [(9000,), (4096,), (37, 5), (1,), (12289,), (384,)]
+    offs = [0, 9004, 13100, 13287, 13289, 25580]  # 13289, 25580 % 4 == 1 / 0: scalar / vector
+    sizes = [int(torch.tensor(sh).prod()) for sh in shapes]
+    states = []
+    for run in range(2):
+        P, G, M, V = [f.clone().to(DEV) for f in flat]
+        M.abs_().mul_(0.1)
+        V.abs_().mul_(0.01)
+        sh = [torch.zeros(n, dtype=torch.bfloat16, device=DEV) if i % 2 == 0 else None for i, n in enumerate(sizes)]
+        views = [[T[o:o + n] for o, n in zip(offs, sizes)] for T in (P, G, M, V)]
+        tab = [torch.tensor([v.data_ptr() for v in vs], dtype=torch.int64, device=DEV) for vs in views]
+        tsh = torch.tensor([x.data_ptr() if x is not None else 0 for x in sh], dtype=torch.int64, device=DEV)
+        tsz = torch.tensor(sizes, dtype=torch.int64, device=DEV)
+        steps = [torch.tensor([3.0, 0.0, 7.0, 1.0, 2.0, 5.0], device=DEV), torch.empty(6, device=DEV)]
+        for it, fin in enumerate((1.0, 0.0, 1.0)):
+            finite = torch.tensor(fin, device=DEV)
+            args_d = (ptr(finite), ptr(steps[it % 2]), ptr(steps[1 - it % 2])) if guard == "device" else \
+                (ptr(finite), 0, 0)
+            if run == 0:
+                assert lib.ivit_adamw_guarded(6, *[ptr(t) for t in tab], ptr(tsh), ptr(tsz), max(sizes), 1e-2, 0.9,
+                                              0.999, 1e-8, 1e-2, 0.271, 0.0447, *args_d, stream()) == 0
+            else:
+                ce = lib.ivit_adamw_chunk_elems()
+                rec = [(t, c) for t, n in enumerate(sizes) for c in range(-(-n // ce))]
+                ch = torch.tensor(rec, dtype=torch.int32, device=DEV)
+                assert lib.ivit_adamw_chunked(6, *[ptr(t) for t in tab], ptr(tsh), ptr(tsz), ptr(ch), len(rec), 1e-2,
+                                              0.9, 0.999, 1e-8, 1e-2, 0.271, 0.0447, *args_d, stream()) == 0
+        torch.cuda.synchronize()
+        states.append((P, M, V, [x for x in sh if x is not None], steps[1] if guard == "device" else None))
+    (P0, M0, V0, S0, st0), (P1, M1, V1, S1, st1) = states
+    assert torch.equal(P0, P1) and torch.equal(M0, M1) and torch.equal(V0, V1)
+    assert all(torch.equal(a, b) for a, b in zip(S0, S1))
+    assert not torch.equal(P0.cpu(), flat[0])  # the updates happened
+    if st0 is not None:
+        assert torch.equal(st0, st1)
+
+
 def test_adamw_device_guard_skips_step_count():
     """The sync-free guard path (Trainer with check_nan=False: step(finite=flag)): a finite = 0
     update changes nothing — weights, moments AND step counts — so the following updates match

@@ -86,7 +86,7 @@ class FusedAdamW(torch.optim.Optimizer):
         return bufs
 
     def _launch(self, group, ps, bc1, bc2s, finite, sin, sout):
-        """The update of ``ps`` through the streaming kernel (live bf16 compute copies,
+        """The update of ``ps`` through the chunked streaming kernel (live bf16 compute copies,
         ops.cast_weight, rewritten in it), then every live row-panel weight pack (ops.packed_weight /
         packed_weight_t) rebuilt from the updated f32 weights in ONE launch: the pointer-table update
         moves no version counter, so without it the packs would stay at the old weights."""
@@ -108,8 +108,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 if pack is not None:
                     jobs.append((p.data_ptr(), pack.data_ptr(), rows, cols, tr))
                     big = max(big, rows * cols)
-        lib.ivit_adamw_guarded(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(self._table_ptrs(shadows, dev)),
-                               ptr(sizes), max(p.numel() for p in ps), group["lr"], b1, b2, group["eps"],
+        chunks, nch = self._table_chunks(ps, dev)
+        lib.ivit_adamw_chunked(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(self._table_ptrs(shadows, dev)),
+                               ptr(sizes), ptr(chunks), nch, group["lr"], b1, b2, group["eps"],
                                group["weight_decay"], bc1, bc2s, ptr(finite), ptr(sin), ptr(sout), stream())
         if jobs:
             lib.ivit_weight_pack_multi(len(jobs), ptr(self._pack_jobs(jobs, dev)), big, stream())
@@ -148,6 +149,21 @@ class FusedAdamW(torch.optim.Optimizer):
             for w, wp, rows, cols, tr in jobs:
                 rec += [w, wp, rows, cols, tr]
             tab = torch.tensor(rec, dtype=torch.int64).pin_memory().to(device, non_blocking=True)
+            if len(self._tables) > 64:
+                self._tables.clear()
+            self._tables[key] = tab
+        return tab
+
+    def _table_chunks(self, ps, device):
+        """Device int32 [n][2] table of (tensor, chunk) for ivit_adamw_chunked: every
+        ivit_adamw_chunk_elems()-element chunk of every tensor of the launch."""
+        key = ("chunks",) + tuple(p.numel() for p in ps)
+        tab = self._tables.get(key)
+        if tab is None:
+            ce = lib.ivit_adamw_chunk_elems()
+            rec = [(t, c) for t, p in enumerate(ps) for c in range(-(-p.numel() // ce))]
+            tab = (torch.tensor(rec, dtype=torch.int32).reshape(-1, 2).pin_memory().to(device, non_blocking=True),
+                   len(rec))
             if len(self._tables) > 64:
                 self._tables.clear()
             self._tables[key] = tab
