@@ -126,6 +126,18 @@ __global__ void merge_heads_kernel(const float* dcls, const float* dbox, const f
 // bias correction is the one torch.optim.AdamW uses when that step never happened. The count is
 // written to a second buffer (block 0 of the tensor) so that no block reads a count another
 // block has already advanced; the caller swaps the two buffers.
+// One element of the update. Contraction off: the two launch forms below (and any vector width)
+// round identically, whatever the surrounding code lets the backend fuse.
+IVIT_DEV void adamw_elem(float gi, float& pi, float& mi, float& vi, float keep, float omb1, float b2, float omb2,
+                         float bc2s, float eps, float step) {
+#pragma clang fp contract(off)
+  pi = pi * keep;
+  mi = mi + omb1 * (gi - mi);
+  vi = vi * b2 + omb2 * gi * gi;
+  const float den = sqrtf(vi) / bc2s + eps;
+  pi = pi - step * (mi / den);
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* const* grads, void* const* ms,
                                                     void* const* vs, const long* sizes, float lr, float b1, float b2,
                                                     float eps, float wd, float bc1, float bc2s, void* const* shadows,
@@ -151,15 +163,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* c
   float* m = (float*)ms[t];
   float* v = (float*)vs[t];
   bf16* sh = shadows ? (bf16*)shadows[(long)sstride * t] : nullptr;
-  const float step = lr / bc1;
+  const float step = lr / bc1, keep = 1.f - lr * wd;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const float gi = g[i];
-    float pi = p[i] * (1.f - lr * wd);
-    float mi = m[i];
-    mi = mi + omb1 * (gi - mi);
-    float vi = v[i] * b2 + omb2 * gi * gi;
-    const float den = sqrtf(vi) / bc2s + eps;
-    pi = pi - step * (mi / den);
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(g[i], pi, mi, vi, keep, omb1, b2, omb2, bc2s, eps, step);
     p[i] = pi;
     m[i] = mi;
     v[i] = vi;
@@ -171,8 +178,8 @@ __global__ __launch_bounds__(256) void adamw_kernel(void* const* params, void* c
 // chunk of AW_CHUNK elements of one tensor (chunks[b] = (tensor, chunk index)), 16-B accesses where
 // the tensor's four arrays allow them. The 2D form above launches max_size / 256 workgroups for EVERY
 // tensor (335 k for IntentNetViT's 327 parameters, nearly all of them leaving at once), which kept
-// the update at ~3.7 TB/s; this grid has exactly the ~15.7 k chunks there are. Same arithmetic, same
-// order of operations per element (bit-identical results).
+// the update at ~3.7 TB/s; this grid has exactly the ~15.7 k chunks there are. Same element update
+// (adamw_elem): bit-identical results.
 constexpr int AW_CHUNK = 4096;
 __global__ __launch_bounds__(256) void adamw_chunk_kernel(void* const* params, void* const* grads, void* const* ms,
                                                           void* const* vs, const long* sizes, const int2* chunks,
@@ -202,11 +209,7 @@ __global__ __launch_bounds__(256) void adamw_chunk_kernel(void* const* params, v
   bf16* sh = shadows && shadows[t] ? (bf16*)shadows[t] + off : nullptr;
   const float step = lr / bc1, keep = 1.f - lr * wd;
   auto upd = [&](float gi, float& pi, float& mi, float& vi) {
-    pi = pi * keep;
-    mi = mi + omb1 * (gi - mi);
-    vi = vi * b2 + omb2 * gi * gi;
-    const float den = sqrtf(vi) / bc2s + eps;
-    pi = pi - step * (mi / den);
+    adamw_elem(gi, pi, mi, vi, keep, omb1, b2, omb2, bc2s, eps, step);
   };
   const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0) &&
                    (((uintptr_t)sh & 7) == 0) && (len & 3) == 0;
