@@ -28,6 +28,8 @@
 #include "patch_embed.h"
 #include "panel_common.h"
 
+#include <type_traits>
+
 namespace ivit {
 namespace {
 
@@ -596,15 +598,20 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
 }
 
 // dW[n][g*128 + k] (+)= sum of the partial tiles of pair g (workgroups whose unit range meets it).
-// D * 128 is a multiple of the block size, so a block's pair g, and the range of workgroups whose
-// unit range meets it, are block-uniform (scalar; one 64-bit division per block, not per element).
+// D * 128 is a multiple of the block's 256 V elements, so a block's pair g, and the range of
+// workgroups whose unit range meets it, are block-uniform (scalar; one 64-bit division per block,
+// not per element). V = 4: four consecutive k per thread with 16-B accesses (the V = 1 form's
+// 27 840 one-element-per-thread blocks at the LiDAR shape were launch-latency-bound: 58 us for 50 MB).
+// Every element is summed in the same order either way.
+template <int V>
 __global__ __launch_bounds__(256) void patch_wgrad_reduce_kernel(const float* __restrict__ slab, int C, int J, int D,
                                                                  float* __restrict__ dW, int accumulate) {
+  using VT = typename std::conditional<V == 4, float4, float>::type;
   const int G = (C + 1) / 2;
-  const long per = (long)D * 128, i0 = (long)blockIdx.x * 256;
+  const long per = (long)D * 128, i0 = (long)blockIdx.x * 256 * V;
   const int g = (int)(i0 / per);
   if (g >= G) return;
-  const int e = (int)(i0 - (long)g * per) + threadIdx.x, n = e >> 7, k = e & 127;
+  const int e = (int)(i0 - (long)g * per) + threadIdx.x * V, n = e >> 7, k = e & 127;
   const long U = (long)G * J, ga = (long)g * J, gb = ga + J;
   // the contiguous workgroup range [w0, w1) whose unit ranges meet pair g (block-uniform); only w0
   // can have begun in the previous pair (its partial tile of g is then its second slab slot)
@@ -614,31 +621,42 @@ __global__ __launch_bounds__(256) void patch_wgrad_reduce_kernel(const float* __
   int w1 = w0;
   while (w1 < WG_NWG && wg_unit_start(w1, U) < gb) ++w1;
   const int slot0 = wg_unit_start(w0, U) < ga ? 1 : 0;
-  float s = 0.f;
+  auto ld = [&](long off) { return *(const VT*)(slab + off); };
+  auto add = [](VT& s, const VT& v) {
+    if constexpr (V == 4) { s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w; }
+    else s += v;
+  };
+  VT s{};
   const long estride = 2L * D * 128;  // one workgroup's two slab slots
-  const float* base = slab + ((long)w0 * 2 * D + n) * 128 + k;
+  const long base = ((long)w0 * 2 * D + n) * 128 + k;
   if (U < WG_NWG) {  // tiny grids: some workgroups own no units (and wrote no slab): skip them
     for (int w = w0; w < w1; ++w) {
       const long a = wg_unit_start(w, U), b = wg_unit_start(w + 1, U);
       if (b <= a) continue;
-      s += slab[(((long)w * 2 + (a < ga ? 1 : 0)) * D + n) * 128 + k];
+      add(s, ld((((long)w * 2 + (a < ga ? 1 : 0)) * D + n) * 128 + k));
     }
   } else if (w0 < w1) {
-    s = base[(long)slot0 * D * 128];
+    s = ld(base + (long)slot0 * D * 128);
     // the rest start in pair g (slot 0): independent loads, eight in flight, summed in order
     int w = w0 + 1;
     for (; w + 8 <= w1; w += 8) {
-      float v[8];
+      VT v[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = base[(long)(w - w0 + q) * estride];
+      for (int q = 0; q < 8; ++q) v[q] = ld(base + (long)(w - w0 + q) * estride);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) s += v[q];
+      for (int q = 0; q < 8; ++q) add(s, v[q]);
     }
-    for (; w < w1; ++w) s += base[(long)(w - w0) * estride];
+    for (; w < w1; ++w) add(s, ld(base + (long)(w - w0) * estride));
   }
   if (2 * g + (k >> 6) >= C) return;
-  float* o = dW + (long)n * C * 64 + (long)g * 128 + k;
-  *o = accumulate ? *o + s : s;
+  VT* o = (VT*)(dW + (long)n * C * 64 + (long)g * 128 + k);
+  if (accumulate) {
+    VT t = *o;
+    add(t, s);
+    *o = t;
+  } else {
+    *o = s;
+  }
 }
 
 // split form: dW[n][g*128 + k] (+)= sum_s slab[s][g][n][k]  (fixed order: deterministic)
@@ -701,8 +719,12 @@ int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long 
     if ((D * 128) % 256) return IVIT_ERR_UNSUPPORTED;  // the reduce's block-uniform pair
     hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, 0>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H,
                        (int)W, Wp, Np, M, J, slab);
-    hipLaunchKernelGGL(patch_wgrad_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, (int)C, J, (int)D,
-                       dW, accumulate);
+    if ((D * 128) % 1024 == 0 && ((uintptr_t)dW & 15) == 0 && (C * 64) % 4 == 0)
+      hipLaunchKernelGGL(patch_wgrad_reduce_kernel<4>, dim3(ivit_cdiv(n, 1024)), dim3(256), 0, st, slab, (int)C, J,
+                         (int)D, dW, accumulate);
+    else
+      hipLaunchKernelGGL(patch_wgrad_reduce_kernel<1>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, (int)C, J,
+                         (int)D, dW, accumulate);
     return 0;
   }
   const int S = (int)patch_wgrad_splits(C);
