@@ -403,11 +403,12 @@ BF16_SLACK = 1.5
 def test_full_grid_bf16_train_step_vs_oracle():
     """BASELINE config 2 shape (400x720, real channels / depth / width), B=2, bf16, DropPath 0.1
     injected: outputs, loss and every parameter gradient vs the f32 oracle. Blocks 0..10 of both
-    ViTs take their scaled fc2-dgrad operand from the next block's backward (ops.GradHandoff)."""
+    ViTs take their scaled fc2-dgrad operand from the next block's backward, and each patch
+    embedding its bf16 token gradient from block 0's (ops.GradHandoff)."""
     import ops
     before = ops.GradHandoff.used
     _bf16_vs_oracle(400, 720, 2, 1234, 0.1, "explicit", False, BF16_SLACK)
-    assert ops.GradHandoff.used - before == 2 * 11
+    assert ops.GradHandoff.used - before == 2 * 12
 
 
 def test_full_grid_bf16_train_step_batch8_vs_oracle():

@@ -575,10 +575,15 @@ class PatchEmbedFn(torch.autograd.Function):
     img (B, C, H, W) f32 → tokens (B*(Np+1), D) f32. No input gradient (the BEV raster)."""
 
     @staticmethod
-    def forward(ctx, img, w, b, pos, cls, cdt):
+    def forward(ctx, img, w, b, pos, cls, cdt, hand=None):
         B, C, H, W = img.shape
         D = w.shape[0]
         P = w.shape[-1]
+        # hand (GradHandoff): block 0's qkv-dgrad + norm1-backward epilogue also writes bf16(dtok),
+        # the weight gradient's operand, so the backward skips its own cast pass over dtok
+        ctx.hand = hand
+        if hand is not None:
+            hand.scale, hand.g, hand.key = None, None, None
         if P != 8:
             # other patch sizes (timm vit_*_patch16_224 at model_vit.py:64,71): patch matrix in the
             # compute dtype, the linear GEMM, then the CLS / pos_embed assembly (ivit_patch_*)
@@ -635,8 +640,15 @@ class PatchEmbedFn(torch.autograd.Function):
             dcls = torch.empty((1, 1, D), dtype=torch.float32, device=src.device)
             lib.ivit_patch_tokens_bwd(ptr(dtok), dt(dtok), B, Np, D, ptr(dy), cdt, ptr(dpos), ptr(dcls), 0, stream())
             dw, db = linear_wgrad(dy, src, cdt)
-            return None, dw.reshape(wshape), db, dpos, dcls, None
-        dtok = cast(dtok.contiguous(), tdtype(cdt))
+            return None, dw.reshape(wshape), db, dpos, dcls, None, None
+        hd = ctx.hand
+        if hd is not None and hd.g is not None and hd.g.dtype == tdtype(cdt) and hd.key == GradHandoff.ident(dtok):
+            dtok = hd.g  # written by block 0's backward (unmodified dtok: same tensor and version)
+            GradHandoff.used += 1
+        else:
+            dtok = cast(dtok.contiguous(), tdtype(cdt))
+        if hd is not None:
+            hd.g = hd.key = None
         Ntok = (H // 8) * (W // 8) + 1
         dw = torch.empty(wshape, dtype=torch.float32, device=src.device)
         db = torch.empty((D,), dtype=torch.float32, device=src.device)
@@ -649,7 +661,7 @@ class PatchEmbedFn(torch.autograd.Function):
         else:
             lib.ivit_patch_embed_wgrad(cdt, ptr(dtok), ptr(src), B, C, H, W, D, ptr(dw), ptr(db), ptr(dpos),
                                        ptr(dcls), 0, ptr(ws), ws.numel(), stream())
-        return None, dw, db, dpos, dcls, None
+        return None, dw, db, dpos, dcls, None, None
 
 
 # Off by default: measured on MI355X with the two ViT streams already concurrent, the extra

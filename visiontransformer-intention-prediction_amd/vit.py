@@ -167,21 +167,23 @@ class VisionTransformer(nn.Module):
         if (H, W) != self.patch_embed.img_size:
             raise ValueError(f"Input size {(H, W)} != model img_size {self.patch_embed.img_size} (timm strict size)")
         cdt = self._cdt()
-        t = ops.PatchEmbedFn.apply(x.float().contiguous(), self.patch_embed.proj.weight, self.patch_embed.proj.bias,
-                                   self.pos_embed, self.cls_token, cdt)
-        N = self.patch_embed.num_patches + 1
         # bf16 at D = 384: block i's fc2 epilogue also produces block i+1's norm1 (ops.ViTBlockFn)
         fuse = cdt == BF16 and self.embed_dim == 384
-        ln = None
-        # ... and in the backward, block i+1 hands block i its DropPath-scaled bf16 gradient
+        # ... and in the backward, block i+1 hands block i its DropPath-scaled bf16 gradient, and
+        # block 0 hands the patch embedding its bf16 token gradient
         hands = [ops.GradHandoff() for _ in self.blocks] if fuse and torch.is_grad_enabled() else None
+        hand_pe = ops.GradHandoff() if hands else None
+        t = ops.PatchEmbedFn.apply(x.float().contiguous(), self.patch_embed.proj.weight, self.patch_embed.proj.bias,
+                                   self.pos_embed, self.cls_token, cdt, hand_pe)
+        N = self.patch_embed.num_patches + 1
+        ln = None
         drawn = self._draw_drop_path(B, x.device)
         yield
         for i, blk in enumerate(self.blocks):
             nxt = self.blocks[i + 1].norm1 if fuse and i + 1 < len(self.blocks) else None
             t, nxt_ln = blk.forward_flat(t, B, N, cdt, ln_in=ln, next_norm=nxt,
                                          hand_mine=hands[i] if hands else None,
-                                         hand_prev=hands[i - 1] if hands and i > 0 else None,
+                                         hand_prev=(hands[i - 1] if i > 0 else hand_pe) if hands else None,
                                          drawn=drawn[i] if drawn is not None else None)
             ln = nxt_ln if nxt is not None else None
             yield
