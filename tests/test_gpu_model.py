@@ -450,7 +450,7 @@ def test_full_grid_bf16_fused_adamw_step():
 def test_fused_adamw_refreshes_packed_weights():
     """FusedAdamW updates parameters through device pointer tables (no version bump), so the bf16
     shadows and the row-panel weight packs the next forward reads are rewritten in the same launch
-    (ivit_adamw_guarded). After a large-lr step, the next forward must equal a forward with every
+    (ivit_adamw_chunked). After a large-lr step, the next forward must equal a forward with every
     cached copy rebuilt from the updated f32 weights; the packs must equal freshly built ones; and a
     device finite flag of 0 must leave weights and moments bit-identical."""
     import loss as L

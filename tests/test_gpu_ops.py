@@ -802,7 +802,7 @@ def test_adamw_device_guard_skips_step_count():
 
 
 def test_adamw_refreshes_bf16_weight_shadows():
-    """ops.cast_weight's cached bf16 copy is rewritten by the AdamW launch (ivit_adamw_guarded),
+    """ops.cast_weight's cached bf16 copy is rewritten by the AdamW launch (ivit_adamw_chunked),
     so after every step it equals bf16(p) exactly; a parameter without a shadow is unaffected."""
     import ops
     from optim import FusedAdamW
@@ -847,7 +847,7 @@ def test_vit_block_wgrad_grouped(M):
 
 
 def test_adamw_packs_unaligned_grads():
-    """FusedAdamW (ivit_adamw_guarded + ivit_weight_pack_multi) on a packed weight whose gradient
+    """FusedAdamW (ivit_adamw_chunked + ivit_weight_pack_multi) on a packed weight whose gradient
     is a view at a 4-B (not 16-B) offset (a DDP bucket view): the same update as
     torch.optim.AdamW and packs equal to freshly built ones."""
     import ops

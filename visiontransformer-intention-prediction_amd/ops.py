@@ -35,7 +35,7 @@ def cast(x, dtype):
 
 
 # Compute-dtype (bf16) copies of f32 parameters, kept across steps: FusedAdamW refreshes them in
-# its own launch (ivit_adamw_guarded) when it updates the parameter, so a training step casts no
+# its own launch (ivit_adamw_chunked) when it updates the parameter, so a training step casts no
 # weights. Any other in-place change of a parameter bumps its version counter and re-casts.
 _SHADOWS = WeakIdKeyDictionary()
 
@@ -95,7 +95,7 @@ def shadow_of(p):
 
 def packs_of(p):
     """(pack, transposed pack) of parameter p that are live (built at its current version), or
-    None each. FusedAdamW rewrites them in its update launch (ivit_adamw_guarded): its pointer-table
+    None each. FusedAdamW rewrites them in its update launch (ivit_adamw_chunked): its pointer-table
     update does not move the version counter, so without that the packs would stay at the
     weights they were built from."""
     e, et = _PACKED.get(p), _PACKED_T.get(p)
