@@ -82,6 +82,8 @@ def _bucket_worker(rank, world, port, bucket_mb):
     model = Toy()
     gb = GradBuckets(model.parameters(), bucket_mb=bucket_mb)
     assert gb.numel == sum(p.numel() for p in model.parameters())
+    # every gradient view starts on a 16-B boundary (kernels store 16 B per lane into them)
+    assert all(p.grad.data_ptr() % 16 == 0 for p in model.parameters())
     if bucket_mb < 0.01:
         assert len(gb.buckets) > 2
     opt = torch.optim.SGD(model.parameters(), lr=0.1)

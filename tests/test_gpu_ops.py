@@ -497,17 +497,14 @@ def test_patch_embed_fused_exact(B, C, H, W, D):
     assert (out2.double().cpu().reshape(B, Np + 1, D) - o).abs().max().item() < 2 * err + 1e-5
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
 @pytest.mark.parametrize("B,C,H,W", [(2, 9, 32, 48), (3, 290, 24, 40), (2, 4, 400, 720), (1, 3, 16, 16),
                                      (2, 290, 64, 128), (1, 290, 160, 200)])
-def test_patch_wgrad_raster_exact(B, C, H, W, mode, monkeypatch):
+def test_patch_wgrad_raster_exact(B, C, H, W):
     """bf16 weight gradient straight from the raster (ivit_patch_embed_wgrad, D = 384: the
-    persistent channel-pair kernel + slab reduction; IVIT_PATCH_WGRAD_SPLIT=1 the split-along-
-    patches form) vs the same products in f64: odd channel
+    persistent channel-pair kernel + slab reduction) vs the same products in f64: odd channel
     counts, 32-patch chunks crossing images, workgroups spanning two / several channel pairs, tiny
     grids with idle workgroups; dbias / dpos / dcls as before."""
     from _lib import BF16, lib, ptr, stream
-    monkeypatch.setenv("IVIT_PATCH_WGRAD_SPLIT", mode)
     D = 384
     g = torch.Generator().manual_seed(7 * C + B)
     img = torch.rand(B, C, H, W, generator=g)

@@ -1,12 +1,19 @@
 #!/bin/bash
 # Build libivit_hip.so of a git revision into ab/lib_<name>.so (same-call A/B runs on the GPU box:
-# IVIT_LIB=ab/lib_<name>.so python ...).  Usage: tools/ab_build.sh <rev> <name>
+# IVIT_LIB=ab/lib_<name>.so python ...).  Usage: tools/ab_build.sh <rev> <name> [extra hipcc flags]
+# (rev WORKTREE: the working tree as it is; extra flags e.g. -DIVIT_WB_ANATOMY=1 for anatomy builds)
 set -e
-REV=$1; NAME=$2
+REV=$1; NAME=$2; EXTRA=${3:-}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d /tmp/abbuild.XXXX)
-git -C "$ROOT" archive "$REV" | tar -x -C "$T"
-make -C "$T/visiontransformer-intention-prediction_amd" -j8 > "$T/make.log" 2>&1
+if [ "$REV" = WORKTREE ]; then
+  mkdir -p "$T/visiontransformer-intention-prediction_amd" "$T/include"
+  cp -r "$ROOT/visiontransformer-intention-prediction_amd/csrc" "$ROOT/visiontransformer-intention-prediction_amd/Makefile" "$T/visiontransformer-intention-prediction_amd/"
+  cp "$ROOT/include/ivit.h" "$T/include/"
+else
+  git -C "$ROOT" archive "$REV" | tar -x -C "$T"
+fi
+make -C "$T/visiontransformer-intention-prediction_amd" -j8 EXTRA="$EXTRA" > "$T/make.log" 2>&1
 mkdir -p "$ROOT/ab"
 cp "$T/visiontransformer-intention-prediction_amd/libivit_hip.so" "$ROOT/ab/lib_$NAME.so"
 rm -rf "$T"

@@ -1,8 +1,8 @@
 set -u
-# Round-4 evidence, part 1: every -m gpu test, smoke, the default bench line (CPU baseline included),
+# Round evidence: every -m gpu test, smoke, the default bench line (CPU baseline included),
 # the DDP leg (--force-collectives), config 4 (eval B=32) and config 5 (800x1440).
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-TAG=${1:-r04_x}
+TAG=${1:-evidence}
 timeout -k 10 800 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 240 --timeout-method thread > gpurun_out/${TAG}_gpu_tests.txt 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/${TAG}_gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/${TAG}_smoke.txt 2>&1

@@ -26,10 +26,11 @@ def timeit(fn, iters):
 
 
 def main():
+    # anatomy: build libraries with -DIVIT_WB_ANATOMY=1 / 2 (tools/ab_build.sh) and run this under
+    # tools/gpu_ab_libs.sh
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=36008)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--modes", type=str, default="", help="comma list of IVIT_WB_MODE anatomy builds to time too")
     a = ap.parse_args()
     import ops
     from _lib import BF16
@@ -41,11 +42,6 @@ def main():
     grouped = timeit(lambda: ops.vit_block_wgrad(*t), a.iters)
     sep = timeit(lambda: [ops.linear_wgrad(t[2 * q], t[2 * q + 1], BF16) for q in range(4)], a.iters)
     each = [timeit(lambda q=q: ops.linear_wgrad(t[2 * q], t[2 * q + 1], BF16), a.iters) for q in range(4)]
-    for mode in [m for m in a.modes.split(",") if m]:
-        os.environ["IVIT_WB_MODE"] = mode
-        tm = timeit(lambda: ops.vit_block_wgrad(*t), a.iters)
-        print(f"  IVIT_WB_MODE={mode}: {tm:.1f} us")
-    os.environ.pop("IVIT_WB_MODE", None)
     print(f"M={M}: grouped {grouped:.1f} us ({flops / grouped / 1e6:.0f} TF/s), four engine GEMMs {sep:.1f} us "
           f"({flops / sep / 1e6:.0f} TF/s); each {[round(x, 1) for x in each]} us")
 

@@ -1012,14 +1012,6 @@ inline int gemm_big_mode() {
   const char* v = getenv("IVIT_GEMM_BIG");
   return v ? atoi(v) : 0;
 }
-// 256 x 128 LDS-DMA tiles (gemm_bf16_glds_kernel<..., 4>: 8 waves, three LDS stages, two K tiles
-// in flight) for long-K GEMMs with a K-contiguous A (the fusion convolutions' forward / dgrad):
-// IVIT_GEMM_WM4=1.
-inline int gemm_wm4_mode() {
-  const char* v = getenv("IVIT_GEMM_WM4");
-  return v ? atoi(v) : 0;
-}
-
 // dtype_bf16: which kernel. batch: number of z. splits: split-K factor (kchunk multiple
 // of the K tile). Grid: x = tiles (XCD-remapped), y = batch * splits.
 template <bool A_KC, bool B_KC, class LA, class LB, class EPI>
@@ -1053,14 +1045,6 @@ int launch_gemm(bool bf16_path, const LA& la, const LB& lb, const EPI& epi, int 
             hipLaunchKernelGGL((gemm_bf16_big_kernel<LA, LB, EPI, A_KC, B_KC, 128>), dim3(tM * tN, batch), dim3(256),
                                0, st, la, lb, epi, M, N, K, tM, tN);
           }
-          return 0;
-        }
-      }
-      if constexpr (A_KC) {
-        if (gemm_wm4_mode() && K >= 1024 && M >= 2048) {
-          const int tM = ivit_cdiv(M, 256);
-          hipLaunchKernelGGL((gemm_bf16_glds_kernel<LA, LB, EPI, A_KC, B_KC, 4>), dim3(tM * tilesN, batch * splits),
-                             dim3(512), 0, st, la, lb, epi, M, N, K, tM, tilesN, splits, kchunk);
           return 0;
         }
       }

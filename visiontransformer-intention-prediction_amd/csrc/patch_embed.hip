@@ -382,14 +382,9 @@ IVIT_DEV long wg_unit_start(int w, long U) { return (long)w * U / WG_NWG; }
 
 
 // NT = D / 128 dtok images; NBK = k-blocks (of 32) per wave (D = 384: NT = 3, NBK = 2).
-// SPLIT = 0: 256 persistent workgroups over the g-major (pair, chunk) units (a range meets at most
-// two pairs; slab [w][2][D][128]). SPLIT = S > 0 (splits along the patches): workgroup f owns
-// pair g = f / S and the chunk range of split s = f % S (slab [s][g][D][128]). With S a multiple
-// of 8 the workgroups that share a split sit on one XCD (flat ids reach the XCDs round-robin) and
-// stream the same patch chunks in the same order, so a dtok chunk is fetched into that XCD's L2
-// once for the ~32 pairs being reduced there together, instead of once per pair from the
-// Infinity Cache (the persistent form moved 4 GB of dtok per LiDAR launch: 2.58x the raster).
-template <int NT, int NBK, int SPLIT>
+// 256 persistent workgroups over the g-major (pair, chunk) units (a range meets at most two pairs;
+// slab [w][2][D][128]).
+template <int NT, int NBK>
 __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restrict__ dtok,
                                                             const float* __restrict__ img, int C, int H, int W,
                                                             int Wp, int Np, int M, int J, float* __restrict__ slab) {
@@ -409,26 +404,12 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
   const int ng = wv % NGRP, kg = wv / NGRP;
   const long U = (long)((C + 1) / 2) * J;
   const int w = blockIdx.x;
-  int g0, j0, nu;
-  if constexpr (SPLIT > 0) {
-    g0 = w / SPLIT;
-    const int s = w - g0 * SPLIT;
-    j0 = (int)((long)s * J / SPLIT);
-    nu = (int)((long)(s + 1) * J / SPLIT) - j0;
-    slab += (long)(s * ((C + 1) / 2) + g0) * D * 128;
-  } else {
-    const long u0 = wg_unit_start(w, U), u1 = wg_unit_start(w + 1, U);
-    nu = (int)(u1 - u0);
-    g0 = (int)(u0 / J);
-    j0 = (int)(u0 - (long)g0 * J);
-    slab += (long)w * 2 * D * 128;
-  }
-  if (nu <= 0) {
-    if constexpr (SPLIT > 0) {  // an empty split still owns its slab tile: zeros
-      for (int i = threadIdx.x; i < D * 128; i += 512) slab[i] = 0.f;
-    }
-    return;
-  }
+  const long u0 = wg_unit_start(w, U), u1 = wg_unit_start(w + 1, U);
+  const int nu = (int)(u1 - u0);
+  const int g0 = (int)(u0 / J);
+  const int j0 = (int)(u0 - (long)g0 * J);
+  slab += (long)w * 2 * D * 128;
+  if (nu <= 0) return;
   const int Hp = H / 8, Bn = M / Np;
 
   // Per-unit addressing is incremental (no integer division in the loop: a runtime-divisor
@@ -659,36 +640,12 @@ __global__ __launch_bounds__(256) void patch_wgrad_reduce_kernel(const float* __
   }
 }
 
-// split form: dW[n][g*128 + k] (+)= sum_s slab[s][g][n][k]  (fixed order: deterministic)
-__global__ __launch_bounds__(256) void patch_wgrad_reduce_split_kernel(const float* __restrict__ slab, int C, int D,
-                                                                       int S, float* __restrict__ dW, int accumulate) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  const int G = (C + 1) / 2;
-  const long per = (long)G * D * 128;
-  if (i >= per) return;
-  const int g = (int)(i / ((long)D * 128));
-  const int e = (int)(i - (long)g * D * 128), n = e >> 7, k = e & 127;
-  if (2 * g + (k >> 6) >= C) return;
-  float s = 0.f;
-  for (int q = 0; q < S; ++q) s += slab[(long)q * per + i];
-  float* o = dW + (long)n * C * 64 + (long)g * 128 + k;
-  *o = accumulate ? *o + s : s;
-}
-
-// splits along the patches (an instantiated SPLIT): a multiple of 8 (one XCD per split residue)
-// giving >= ~256 workgroups
-long patch_wgrad_splits(long C) {
-  const long G = (C + 1) / 2;
-  return G >= 32 ? 8 : G >= 16 ? 16 : G >= 4 ? 64 : 256;
-}
-
 }  // namespace
 
 long patch_wgrad_raster_workspace(long D) { return (long)WG_NWG * 2 * D * 128 * 4; }
 long patch_wgrad_raster_workspace2(long C, long D) {
-  const long split = patch_wgrad_splits(C) * ((C + 1) / 2) * D * 128 * 4;
-  const long pers = patch_wgrad_raster_workspace(D);
-  return split > pers ? split : pers;
+  (void)C;
+  return patch_wgrad_raster_workspace(D);
 }
 
 bool patch_wgrad_raster_ok(long B, long C, long H, long W, long D) {
@@ -705,44 +662,19 @@ int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long 
   const int Wp = (int)(W / 8), Np = (int)((H / 8) * Wp), M = (int)(B * Np), J = ivit_cdiv(M, WG_MU);
   float* slab = (float*)work;
   const long n = (long)((C + 1) / 2) * D * 128;
-  // Default: the persistent form. The split-along-patches form (IVIT_PATCH_WGRAD_SPLIT=1) cuts the
-  // dtok bytes fetched from the Infinity Cache but not the bytes each CU takes in by LDS-DMA (16 KiB
-  // raster + 24 KiB dtok per unit either way), which bound both: measured in-step 1.08 vs 1.01 ms
-  // (LiDAR), 48.74-48.84 vs 48.64-48.69 ms per step. Round 4, isolated (LiDAR shape):
-  // persistent 1.116-1.121 ms, split 1.163, an XCD-sharded persistent form (each XCD's workgroups
-  // on one eighth of the patch chunks for every pair: its dtok rows L2-resident) 1.387 (removed);
+  // The persistent form. Measured and removed: a split-along-patches form (in-step
+  // 1.08 vs 1.01 ms, LiDAR) and an XCD-sharded persistent form (1.387 vs 1.116 ms isolated);
   // diagnostic builds with the dtok chunk fixed (L2-resident) 0.988 and the raster chunk fixed
   // 1.002 ms — neither operand's source bounds the kernel by itself.
-  const char* sv = getenv("IVIT_PATCH_WGRAD_SPLIT");
-  const int mode = sv ? atoi(sv) : 0;
-  if (mode != 1) {
-    if ((D * 128) % 256) return IVIT_ERR_UNSUPPORTED;  // the reduce's block-uniform pair
-    hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, 0>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H,
-                       (int)W, Wp, Np, M, J, slab);
-    if ((D * 128) % 1024 == 0 && ((uintptr_t)dW & 15) == 0 && (C * 64) % 4 == 0)
-      hipLaunchKernelGGL(patch_wgrad_reduce_kernel<4>, dim3(ivit_cdiv(n, 1024)), dim3(256), 0, st, slab, (int)C, J,
-                         (int)D, dW, accumulate);
-    else
-      hipLaunchKernelGGL(patch_wgrad_reduce_kernel<1>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, (int)C, J,
-                         (int)D, dW, accumulate);
-    return 0;
-  }
-  const int S = (int)patch_wgrad_splits(C);
-  const int G = (int)((C + 1) / 2);
-  if (S == 8)
-    hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, 8>), dim3(G * 8), dim3(512), 0, st, dtok, img, (int)C, (int)H, (int)W,
-                       Wp, Np, M, J, slab);
-  else if (S == 16)
-    hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, 16>), dim3(G * 16), dim3(512), 0, st, dtok, img, (int)C, (int)H,
-                       (int)W, Wp, Np, M, J, slab);
-  else if (S == 64)
-    hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, 64>), dim3(G * 64), dim3(512), 0, st, dtok, img, (int)C, (int)H,
-                       (int)W, Wp, Np, M, J, slab);
+  if ((D * 128) % 256) return IVIT_ERR_UNSUPPORTED;  // the reduce's block-uniform pair
+  hipLaunchKernelGGL((patch_wgrad_kernel<3, 2>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H, (int)W, Wp,
+                     Np, M, J, slab);
+  if ((D * 128) % 1024 == 0 && ((uintptr_t)dW & 15) == 0 && (C * 64) % 4 == 0)
+    hipLaunchKernelGGL(patch_wgrad_reduce_kernel<4>, dim3(ivit_cdiv(n, 1024)), dim3(256), 0, st, slab, (int)C, J,
+                       (int)D, dW, accumulate);
   else
-    hipLaunchKernelGGL((patch_wgrad_kernel<3, 2, 256>), dim3(G * 256), dim3(512), 0, st, dtok, img, (int)C, (int)H,
-                       (int)W, Wp, Np, M, J, slab);
-  hipLaunchKernelGGL(patch_wgrad_reduce_split_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, (int)C, (int)D,
-                     S, dW, accumulate);
+    hipLaunchKernelGGL(patch_wgrad_reduce_kernel<1>, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, (int)C, J,
+                       (int)D, dW, accumulate);
   return 0;
 }
 

@@ -53,9 +53,12 @@ struct WbArgs {
 // cycles beside MFMAs (MI355X_MICROARCH.md cycle constants), and with every wave issuing its own
 // pieces the DMA and MFMA phases ran nearly serialised (anatomy: DMA skeleton 112 us + MFMA-only
 // 105 us -> 206 us together). Both roles pass exactly one barrier per step.
-// MODE (anatomy builds, tools/wgrad_bench.py --modes): 0 product, 1 no MFMAs (the DMA / barrier
+// MODE (anatomy builds: -DIVIT_WB_ANATOMY=MODE via tools/ab_build.sh): 0 product, 1 no MFMAs (the DMA / barrier
 // skeleton), 2 no DMA after the prologue (MFMAs on stale stages).
 constexpr int WB_CW = 8, WB_LW = 4;  // compute / loader waves
+#ifndef IVIT_WB_ANATOMY
+#define IVIT_WB_ANATOMY 0
+#endif
 template <int MODE>
 __global__ __launch_bounds__(64 * (WB_CW + WB_LW), 1) void wgrad_block_kernel(const WbArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[WB_NS * WB_STAGE];
@@ -256,6 +259,10 @@ extern "C" int ivit_vit_block_wgrad(long M, long D, long Hd, const void* dy2, co
   IVIT_CHECK_ARG(work_bytes >= ivit_vit_block_wgrad_workspace(M, D, Hd), "ivit_vit_block_wgrad: workspace too small");
   const void* ops[8] = {dy2, a, dh, x2, dyp, o, dyq, x1};
   for (int i = 0; i < 8; ++i) IVIT_CHECK_ARG(((uintptr_t)ops[i] & 15) == 0, "ivit_vit_block_wgrad: operand not 16-B aligned");
+  // the reduce stores 16 B per thread into every output (ddp.GradBuckets aligns its views)
+  const void* outs[8] = {dw2, db2, dw1, db1, dwp, dbp, dwq, dbq};
+  for (int i = 0; i < 8; ++i)
+    IVIT_CHECK_ARG(((uintptr_t)outs[i] & 15) == 0, "ivit_vit_block_wgrad: output %d not 16-B aligned", i);
   const int S = wb_splits(M);
   const long steps = (M + WB_BK - 1) / WB_BK;
   const int kchunk = (int)((steps + S - 1) / S) * WB_BK;
@@ -298,14 +305,9 @@ extern "C" int ivit_vit_block_wgrad(long M, long D, long Hd, const void* dy2, co
   args.slab = (float*)w;
   args.bslab = args.slab + (long)S * off;
   hipStream_t st = ivit_stream(stream);
-  const char* mv = getenv("IVIT_WB_MODE");
-  const int mode = mv ? atoi(mv) : 0;
-  if (mode == 1)
-    hipLaunchKernelGGL(wgrad_block_kernel<1>, dim3(args.tile_base[4] * S), dim3(64 * (WB_CW + WB_LW)), 0, st, args);
-  else if (mode == 2)
-    hipLaunchKernelGGL(wgrad_block_kernel<2>, dim3(args.tile_base[4] * S), dim3(64 * (WB_CW + WB_LW)), 0, st, args);
-  else
-    hipLaunchKernelGGL(wgrad_block_kernel<0>, dim3(args.tile_base[4] * S), dim3(64 * (WB_CW + WB_LW)), 0, st, args);
+  // anatomy builds (tools/ab_build.sh -DIVIT_WB_ANATOMY=1 / 2) compile a diagnostic body instead
+  hipLaunchKernelGGL(wgrad_block_kernel<IVIT_WB_ANATOMY>, dim3(args.tile_base[4] * S), dim3(64 * (WB_CW + WB_LW)), 0,
+                     st, args);
   IVIT_LAUNCH_CHECK();
   hipLaunchKernelGGL(wgrad_block_reduce_kernel, dim3(ivit_cdiv((off + boff) / 4, 256)), dim3(256), 0, st, args.slab,
                      args.bslab, out, S);

@@ -52,12 +52,27 @@ def init_distributed(backend: str | None = None, force_group: bool = False):
     return rank, local, world, dev
 
 
-class _Bucket:
-    __slots__ = ("params", "flat", "ready", "work", "events", "streams")
+# Each parameter's view starts on a 16-byte boundary of its bucket: kernels that write a gradient
+# straight into its view (GradSink: the grouped ViT weight gradient's reduce stores 16 B per lane)
+# need aligned destinations, and a 35-element bias (the detection head) would otherwise leave every
+# later view 4-byte aligned. The padding floats stay zero (all-reduced with the rest, harmless).
+_ALIGN = 4  # floats
 
-    def __init__(self, params, flat):
+
+def _aligned(n: int) -> int:
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+_ON_COMM = object()  # a bucket whose collective was enqueued on the comm stream itself
+
+
+class _Bucket:
+    __slots__ = ("params", "flat", "offs", "ready", "work", "events", "streams")
+
+    def __init__(self, params, flat, offs):
         self.params = params
         self.flat = flat
+        self.offs = offs
         self.ready = 0
         self.work = None
         self.events = []
@@ -124,6 +139,9 @@ class GradBuckets:
         self._direct = set()  # ids of parameters written through their GradSink in this backward
         self.direct = os.environ.get("IVIT_DDP_DIRECT", "1") == "1"
         self.per_param_events = os.environ.get("IVIT_DDP_EVENTS", "stream") == "param"
+        # IVIT_DDP_PG_STREAM=1: asynchronous collectives on the process group's own stream (a fifth
+        # stream beside the step's four; kept for the A/B against the comm-stream form)
+        self.pg_stream = os.environ.get("IVIT_DDP_PG_STREAM", "0") == "1"
         cur, cur_bytes = [], 0
         for p in reversed(ps):
             nb = p.numel() * p.element_size()
@@ -137,21 +155,23 @@ class GradBuckets:
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in ps]
 
     def _add(self, params):
-        n = sum(p.numel() for p in params)
-        flat = torch.zeros(n, dtype=params[0].dtype, device=params[0].device)
-        b = _Bucket(params, flat)
-        off = 0
+        offs, n = [], 0
         for p in params:
+            offs.append(n)
+            n += _aligned(p.numel())
+        flat = torch.zeros(n, dtype=params[0].dtype, device=params[0].device)
+        b = _Bucket(params, flat, offs)
+        for p, off in zip(params, offs):
             p.grad = flat[off:off + p.numel()].view_as(p)
             self._of[p] = b
             self._ptr[p] = p.grad.data_ptr()
             p._ivit_sink = GradSink(self, p, p.grad)
-            off += p.numel()
         self.buckets.append(b)
 
     @property
     def numel(self):
-        return sum(b.flat.numel() for b in self.buckets)
+        """Gradient elements held (the buckets' alignment padding not counted)."""
+        return sum(p.numel() for b in self.buckets for p in b.params)
 
     def zero_grad(self):
         for b in self.buckets:
@@ -160,12 +180,10 @@ class GradBuckets:
             b.flat.zero_()
             b.ready = 0
             b.streams = {}
-            off = 0
-            for p in b.params:  # re-attach views if something replaced .grad
+            for p, off in zip(b.params, b.offs):  # re-attach views if something replaced .grad
                 view = b.flat[off:off + p.numel()]
                 if p.grad is None or p.grad.data_ptr() != view.data_ptr():
                     p.grad = view.view_as(p)
-                off += p.numel()
         self._fresh = {id(p) for b in self.buckets for p in b.params}
         self._seen = set()
         self._direct = set()
@@ -211,7 +229,16 @@ class GradBuckets:
             b.events = []
             b.streams = {}
             with torch.cuda.stream(comm):
-                b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+                if self.pg_stream:
+                    b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
+                else:
+                    # a synchronous-op collective is enqueued on the CURRENT stream (torch >= 2.8
+                    # ProcessGroupNCCL, asyncOp = false): the RCCL kernel runs on `comm` itself, not
+                    # on the process group's internal stream, so the step stays at four streams
+                    # (default, the two ViT streams, comm) = GPU_MAX_HW_QUEUES. The host does not
+                    # block: the op only orders `comm` behind its own end event.
+                    dist.all_reduce(b.flat, group=self.group, async_op=False)
+                    b.work = _ON_COMM
         else:
             b.work = dist.all_reduce(b.flat, group=self.group, async_op=True)
         GradBuckets.launched += 1
@@ -237,7 +264,8 @@ class GradBuckets:
                 self._launch(b)
         inv = 1.0 / self.world
         for b in self.buckets:
-            b.work.wait()
+            if b.work is not _ON_COMM:
+                b.work.wait()
             b.work = None
             b.ready = 0
             b.events = []

@@ -155,8 +155,13 @@ class TwoStreamViTBackbone(nn.Module):
             # backward engine (newest node first) runs the LiDAR stream k blocks ahead and its long
             # patch-embedding weight gradient overlaps the map stream's last blocks
             with torch.cuda.stream(s2):
-                for _ in range(LEAD):
-                    next(live[1][2])
+                for _ in range(LEAD):  # a lead past the map ViT's depth finishes it here
+                    try:
+                        next(live[1][2])
+                    except StopIteration as stop:
+                        out["m"] = stop.value
+                        live.pop(1)
+                        break
         while live:
             for item in list(live):
                 st, key, gen = item
@@ -251,7 +256,7 @@ class TwoStreamViTBackbone(nn.Module):
 
 _SIDE_STREAMS = {}
 INTERLEAVE = os.environ.get("IVIT_STREAM_INTERLEAVE", "1") == "1"
-LEAD = int(os.environ.get("IVIT_STREAM_LEAD", "1"))  # 44.53-44.64 vs 44.65-44.67 ms (lead 0), same call
+LEAD = max(0, int(os.environ.get("IVIT_STREAM_LEAD", "1")))  # 44.53-44.64 vs 44.65-44.67 ms (lead 0), same call
 
 
 def _side_streams(device):

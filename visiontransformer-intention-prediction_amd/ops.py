@@ -664,48 +664,9 @@ class PatchEmbedFn(torch.autograd.Function):
         return None, dw, db, dpos, dcls, None, None
 
 
-# Off by default: measured on MI355X with the two ViT streams already concurrent, the extra
-# fork costs 7 % (65.0 -> 69.5 ms/step, bench.py A/B in one call). IVIT_WGRAD_FORK=1 enables it.
-WGRAD_FORK = os.environ.get("IVIT_WGRAD_FORK", "0") == "1"
 # bf16 row-panel ViT blocks: the four weight gradients as one grouped launch (ivit_vit_block_wgrad)
 # instead of four split-K engine GEMMs; IVIT_GROUP_WGRAD=0 selects the per-GEMM path (A/B runs).
 GROUP_WGRAD = os.environ.get("IVIT_GROUP_WGRAD", "1") == "1"
-_FORK_STREAMS = {}
-
-
-class _WgradFork:
-    """A side stream (one per calling stream) for weight-gradient GEMMs: each call waits for
-    the work queued so far on the calling stream, runs on the side stream, and join() makes the
-    calling stream wait for all of it. Tensors crossing streams are record_stream()-ed so the
-    caching allocator never hands their memory out early."""
-
-    def __init__(self, device):
-        self.cur = torch.cuda.current_stream(device)
-        key = (device.index, self.cur.cuda_stream)
-        if key not in _FORK_STREAMS:
-            _FORK_STREAMS[key] = torch.cuda.Stream(device)
-        self.side = _FORK_STREAMS[key]
-        self.outs = []
-
-    def run(self, fn, *args):
-        self.side.wait_stream(self.cur)
-        with torch.cuda.stream(self.side):
-            out = fn(*args)
-        self.outs += [t for t in out if t is not None]
-        return out
-
-    def join(self, inputs):
-        self.cur.wait_stream(self.side)
-        for t in inputs:
-            t.record_stream(self.side)
-        for t in self.outs:
-            t.record_stream(self.cur)
-
-
-def _wgrad(fork, dy, x, cdt):
-    return linear_wgrad(dy, x, cdt) if fork is None else fork.run(linear_wgrad, dy, x, cdt)
-
-
 class GradHandoff:
     """Backward hand-off between consecutive fused ViT blocks: block i+1's qkv-dgrad + norm1-backward
     kernel also writes bf16(dx * s2_i) — block i's DropPath-scaled MLP-branch gradient, the fc2
@@ -822,9 +783,6 @@ class ViTBlockFn(torch.autograd.Function):
         cd = tdtype(cdt)
         dx2 = torch.zeros_like(x) if dx2 is None else dx2.contiguous()
         D = x.shape[1]
-        # The weight gradients are off the critical path: they run on a forked stream and
-        # overlap the dgrad chain (notably the attention backward); joined before returning.
-        fork = _WgradFork(dx2.device) if dx2.is_cuda and WGRAD_FORK else None
         hm, hp = ctx.hand_mine, ctx.hand_prev
         dx2s = None
         if hm is not None:
@@ -836,11 +794,11 @@ class ViTBlockFn(torch.autograd.Function):
             dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
         dh = panel_dgrad_mul(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
         # bf16 row-panel blocks: the four weight gradients in one grouped launch after the dgrads
-        group = ctx.panel and GROUP_WGRAD and fork is None
+        group = ctx.panel and GROUP_WGRAD
         # DDP: the twelve parameter gradients straight into their bucket views (no autograd add)
         direct = grad_sinks(ctx.params) if group else None
         dv = direct[1] if direct is not None else [None] * 12
-        g2 = None if group else _wgrad(fork, dx2s, a, cdt)
+        g2 = None if group else linear_wgrad(dx2s, a, cdt)
         if ctx.panel:  # fc1 dgrad with norm2's backward in the epilogue
             dx1, dx1s, dg2, dbe2 = linear_dgrad_ln_bwd(dh, f1w, x1, n2w, m2, r2, dres=dx2, dx=torch.empty_like(dx2),
                                                        xs_dtype=cd, row_scale=s1, rps=N, dg=dv[6], db=dv[7])
@@ -848,9 +806,9 @@ class ViTBlockFn(torch.autograd.Function):
             dln2 = linear_dgrad(dh, w1, cdt, torch.float32)
             dx1, dx1s, dg2, dbe2 = layernorm_bwd(x1, n2w, m2, r2, dln2, dres=dx2, dx=torch.empty_like(dx2),
                                                  xs_dtype=cd, row_scale=s1, rps=N)
-        g1 = None if group else _wgrad(fork, dh, ln2, cdt)
+        g1 = None if group else linear_wgrad(dh, ln2, cdt)
         do = panel_dgrad(dx1s, pw) if ctx.panel else linear_dgrad(dx1s, wp, cdt, cd)
-        gp = None if group else _wgrad(fork, dx1s, o, cdt)
+        gp = None if group else linear_wgrad(dx1s, o, cdt)
         dqkv = attn_bwd_q2(qkv, o, do, lse, B, N, H) if ctx.q2 else attn_bwd(qkv, o, do, lse, B, N, H, cdt)
         if ctx.panel:  # qkv dgrad with norm1's backward in the epilogue
             if hp is not None:  # also the previous block's bf16(dx0 * s2) (GradHandoff)
@@ -867,9 +825,7 @@ class ViTBlockFn(torch.autograd.Function):
             outs = None if direct is None else (dv[10], dv[11], dv[8], dv[9], dv[4], dv[5], dv[2], dv[3])
             g2, g1, gp, gq = vit_block_wgrad(dx2s, a, dh, ln2, dx1s, o, dqkv, ln1, outs=outs)
         else:
-            gq = _wgrad(fork, dqkv, ln1, cdt)
-        if fork is not None:
-            fork.join((dx2s, dh, dx1s, dqkv, a, ln2, o, ln1))
+            gq = linear_wgrad(dqkv, ln1, cdt)
         if direct is not None:  # written into the buckets: nothing for autograd to accumulate
             for sk in direct[0]:
                 sk.done()
@@ -888,65 +844,6 @@ def _unit_ln_params(n, dev):
     if key not in _UNIT_LN:
         _UNIT_LN[key] = (torch.ones(n, device=dev), torch.zeros(n, device=dev))
     return _UNIT_LN[key]
-
-
-NECK_FORK = os.environ.get("IVIT_NECK_FORK", "0") == "1"
-_NECK_STREAMS = {}
-
-
-class _NeckGradFork:
-    """The neck's weight gradients (head conv, fusion convs, adapter linears: none of them on the
-    path to the ViT streams' input gradient) on a side stream, so they overlap the two ViT
-    backward passes instead of delaying them by ~1 ms: each runs after the work queued so far on
-    the calling (main) stream; the gradients are delivered straight to the parameters (a gradient-
-    bucket view through ddp.GradSink, else ``.grad`` set or accumulated on the side stream) and the
-    op returns None for them, so no autograd kernel on the main stream reads them early; the main
-    stream waits for the side stream at the end of the backward pass (an engine callback). With
-    gradient buckets the side stream is their communication stream (no extra hardware queue)."""
-
-    def __init__(self, dev, params):
-        self.main = torch.cuda.current_stream(dev)
-        sink = next((getattr(p, "_ivit_sink", None) for p in params if getattr(p, "_ivit_sink", None) is not None),
-                    None)
-        if sink is not None:
-            self.side = sink.gb._comm_stream(dev)
-        else:
-            key = (dev.index, self.main.cuda_stream)
-            if key not in _NECK_STREAMS:
-                _NECK_STREAMS[key] = torch.cuda.Stream(dev)
-            self.side = _NECK_STREAMS[key]
-        self.read = []
-
-    def run(self, fn, *args):
-        self.side.wait_stream(self.main)
-        with torch.cuda.stream(self.side):
-            out = fn(*args)
-        self.read += [a for a in args if torch.is_tensor(a)]
-        return out
-
-    def deliver(self, p, g):
-        """g (computed on the side stream) becomes / is added to p's gradient."""
-        with torch.cuda.stream(self.side):
-            sink = getattr(p, "_ivit_sink", None)
-            if sink is not None:  # gradient buckets: into the view (fresh) or added to it
-                view = sink.claim()
-                if view is not None:
-                    view.copy_(g)
-                else:
-                    p.grad.add_(g)
-                sink.done()  # the bucket waits for the side stream
-            elif p.grad is None:
-                p.grad = g
-                g.record_stream(self.main)
-            else:
-                p.grad.add_(g)
-                p.grad.record_stream(self.side)
-
-    def close(self):
-        for t in self.read:
-            t.record_stream(self.side)
-        main, side = self.main, self.side
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: main.wait_stream(side))
 
 
 class NeckFn(torch.autograd.Function):
@@ -1037,17 +934,11 @@ class NeckFn(torch.autograd.Function):
         M = B * Np
         dev = cat.device
         G = {}
-        forked = set()
-        fork = _NeckGradFork(dev, list(P.values())) if NECK_FORK and cat.is_cuda else None
 
         def cw(n_, dy_, x_, Cin_, Cout_, k_):
-            # a fusion conv's weight gradient (+ unpack), on the fork when there is one
-            def f(dy_, x_):
-                gp_, _ = conv_wgrad(dy_, x_, B, Hf, Wf, Cin_, Cout_, k_, cdt)
-                return unpack_conv_grad(gp_, Cout_, Cin_, k_)
-            G[n_] = fork.run(f, dy_, x_) if fork is not None else f(dy_, x_)
-            if fork is not None:
-                forked.add(n_)
+            # a fusion conv's weight gradient (+ unpack)
+            gp_, _ = conv_wgrad(dy_, x_, B, Hf, Wf, Cin_, Cout_, k_, cdt)
+            G[n_] = unpack_conv_grad(gp_, Cout_, Cin_, k_)
 
         if A == 0:
             dx = gouts[0].contiguous().float()
@@ -1067,11 +958,9 @@ class NeckFn(torch.autograd.Function):
                 gw = unpack_conv_grad(gp, Cd + Ci, Cin, 3)
                 return gw[:Cd], gw[Cd:], dbh[:Cd].clone(), dbh[Cd:Cd + Ci].clone()
 
-            hw = fork.run(head_wgrad, dh, x_last) if fork is not None else head_wgrad(dh, x_last)
             for n_, g_ in zip(("det_head.conv.weight", "intention_head.conv.weight", "det_head.conv.bias",
-                               "intention_head.conv.bias"), hw):
+                               "intention_head.conv.bias"), head_wgrad(dh, x_last)):
                 G[n_] = g_
-                forked.add(n_) if fork is not None else None
             dx = conv_dgrad(dh, B, Hf, Wf, whp, cdt, torch.float32, w=wh, dy_zero_pad=True)
         for li in reversed(range(layers)):
             p = f"fusion_block.{li}."
@@ -1107,11 +996,7 @@ class NeckFn(torch.autograd.Function):
             C = wa.shape[0]
             dp = dpre[:, c0:c0 + C]
             dz = linear_dgrad(dp, wa, cdt, torch.float32)
-            if fork is not None:
-                G[f"adapter_{s}.1.weight"], G[f"adapter_{s}.1.bias"] = fork.run(linear_wgrad, dp, z, cdt)
-                forked.update((f"adapter_{s}.1.weight", f"adapter_{s}.1.bias"))
-            else:
-                G[f"adapter_{s}.1.weight"], G[f"adapter_{s}.1.bias"] = linear_wgrad(dp, z, cdt)
+            G[f"adapter_{s}.1.weight"], G[f"adapter_{s}.1.bias"] = linear_wgrad(dp, z, cdt)
             dy, _, G[f"adapter_{s}.0.weight"], G[f"adapter_{s}.0.bias"] = layernorm_bwd(
                 y, P[f"adapter_{s}.0.weight"], ma, ra, dz)
             dt_ = torch.empty_like(t)
@@ -1119,14 +1004,6 @@ class NeckFn(torch.autograd.Function):
             _, _, G[f"vit_{s}.norm.weight"], G[f"vit_{s}.norm.bias"] = layernorm_bwd(
                 t, P[f"vit_{s}.norm.weight"], mf, rf, dy, dx=dt_, rowmap=(Np, Np + 1, 1))
             outs[s] = dt_
-        if fork is not None:
-            # in parameter order: a delivery can complete a gradient bucket and launch its collective,
-            # and every rank must launch the buckets in the same order (a set's order follows the
-            # per-process string hash)
-            for n_ in names:
-                if n_ in forked:
-                    fork.deliver(P[n_], G.pop(n_))
-            fork.close()
         grads = [G.get(n) for n in names]
         del ctx.st, ctx.P
         return (outs["lidar"], outs["map"], None) + tuple(grads)

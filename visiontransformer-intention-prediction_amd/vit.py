@@ -135,7 +135,8 @@ class VisionTransformer(nn.Module):
         branch, the same Bernoulli(1-p)/(1-p) law, a different stream). None when no block drops."""
         if not self.training or all(b.drop_path_rate <= 0.0 for b in self.blocks):
             return None
-        key = (device, B)
+        # the per-block rates are part of the key: a drop-path schedule that changes them rebuilds it
+        key = (device, B, tuple(float(b.drop_path_rate) for b in self.blocks))
         cache = getattr(self, "_keep_cache", None)
         if cache is None or cache[0] != key:
             keep = torch.tensor([1.0 - b.drop_path_rate for b in self.blocks], dtype=torch.float32)
@@ -172,7 +173,8 @@ class VisionTransformer(nn.Module):
         # ... and in the backward, block i+1 hands block i its DropPath-scaled bf16 gradient, and
         # block 0 hands the patch embedding its bf16 token gradient
         hands = [ops.GradHandoff() for _ in self.blocks] if fuse and torch.is_grad_enabled() else None
-        hand_pe = ops.GradHandoff() if hands else None
+        # (only the fused patch-8 embedding reads it; the generic patch path takes its f32 dtok)
+        hand_pe = ops.GradHandoff() if hands and self.patch_embed.proj.weight.shape[-1] == 8 else None
         t = ops.PatchEmbedFn.apply(x.float().contiguous(), self.patch_embed.proj.weight, self.patch_embed.proj.bias,
                                    self.pos_embed, self.cls_token, cdt, hand_pe)
         N = self.patch_embed.num_patches + 1
