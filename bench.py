@@ -80,6 +80,39 @@ def kernel_exec_ms(ops, name):
     return ops.busy_ms(iv) / n0, sum(b - a for a, b in iv) / n0, n0
 
 
+def write_intervals(ops, path):
+    """The attention kernels' execution intervals recorded in the timed region (ivit_ktime_read),
+    as a rocprofv3-kernel-trace-shaped CSV (Kernel_Name, Start_Timestamp, End_Timestamp in ns from
+    the first recorded launch, Launch = index within the kernel): the input of tools/kunion.py."""
+    import csv
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["Kernel_Name", "Launch", "Start_Timestamp", "End_Timestamp"])
+        for name in ATTN:
+            for tag, kern in zip(ATTN[name]["tags"], ATTN[name]["kernels"]):
+                for i, (a, b) in enumerate(ops.ktime_read(tag)):
+                    w.writerow([kern, i, int(round(a * 1e6)), int(round(b * 1e6))])
+
+
+def rocprof_union(name):
+    """(us per launch, source) of the newest committed rocprofv3-trace union of an ATTN entry's
+    kernels (profiles/*_<name>_union.json, written by tools/kunion.py --json from the kernel trace of
+    a profiled bench command), or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", f"*_{name}_union.json")),
+                   key=lambda p: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(p))])
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+            if d.get("source_kind") == "rocprofv3":
+                return float(d["union_us_per_launch"]), os.path.relpath(f, HERE)
+        except (OSError, ValueError, KeyError):
+            continue
+    return None, None
+
+
 def attn_flops(name, B, N, H, Dh=64):
     return (8.0 if name == "attn_bwd" else 4.0) * B * H * N * N * Dh
 
@@ -303,6 +336,9 @@ def main():
     ap.add_argument("--augment", action="store_true",
                     help="train mode: run the training-time augment_bev (dataset.py:352-353) on the batch "
                          "inside every timed step (ivit_bev_augment passes)")
+    ap.add_argument("--intervals-out", type=str, default=None,
+                    help="write the attention kernels' recorded execution intervals of the timed region (the "
+                         "roofline's device time) as a kernel-trace CSV; tools/kunion.py recomputes the union")
     ap.add_argument("--bucket-mb", type=float, default=64)
     ap.add_argument("--ddp", choices=["buckets", "torch"], default="buckets",
                     help="gradient exchange: ddp.GradBuckets (default) or torch DistributedDataParallel")
@@ -422,6 +458,8 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     ops.ktime_arm(False)
+    if args.intervals_out and timing:
+        write_intervals(ops, args.intervals_out)
     span_ms = {k: ops.KernelTimer.mean_ms(k) for k in ATTN}
     kexec = {k: kernel_exec_ms(ops, k) for k in ATTN}
     attn_ms = {k: kexec[k][0] for k in ATTN}
@@ -499,6 +537,18 @@ def main():
                       "frac": round(fl_step / (el / args.steps) / 1e12 / peak, 4),
                       "flops_per_step_per_gpu": fl_step},
     }
+    if default_cfg:
+        # the same launches' device time from a committed rocprofv3 kernel trace of the profiled
+        # bench command (tools/kunion.py --json): the figure the profile files reproduce
+        us, src = rocprof_union(roof)
+        if us is not None:
+            out["roofline"]["frac_rocprof"] = round(afl / (us * 1e-6) / 1e12 / peak, 4)
+            out["roofline"]["frac_rocprof_note"] = (f"{us:.1f} us per launch = the union of the kernels' intervals in "
+                                                    f"the rocprofv3 kernel trace summarised in {src} (profiled "
+                                                    f"command: the profiler lowers the clock, MI355X_MICROARCH.md "
+                                                    f"DVFS item 2)")
+    if args.intervals_out and timing:
+        out["roofline"]["intervals_file"] = os.path.relpath(os.path.abspath(args.intervals_out), HERE)
     if default_cfg and world == 1:
         # the same kernel(s) alone on the same shape (outside the timed region): the frac without the
         # other ViT stream's kernels sharing the CUs

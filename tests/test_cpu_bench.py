@@ -45,3 +45,46 @@ def test_visible_gpus_does_not_initialise_hip():
     import torch
     n = bench.visible_gpus()
     assert n >= 0 and not torch.cuda.is_initialized()
+
+
+class _FakeOps:
+    """ops.ktime_read stand-in: per tag, (start_ms, stop_ms) relative to the first launch."""
+    rec = {0: [(0.0, 0.3)], 1: [(1.0, 1.5), (1.2, 1.6)], 2: [(1.5, 2.1), (1.6, 2.4)]}
+
+    def ktime_read(self, tag):
+        return self.rec.get(tag, [])
+
+
+def test_intervals_file_reproduces_the_roofline_union(tmp_path):
+    """bench.py --intervals-out writes the timed region's attention intervals; tools/kunion.py
+    recomputes the union per launch from that file alone (the line's roofline time), and --json
+    carries flop / frac."""
+    import json
+    import subprocess
+    path = tmp_path / "iv.csv"
+    bench.write_intervals(_FakeOps(), str(path))
+    # union of the bwd pair: [1.0, 2.4] = 1.4 ms over 2 launches = 700 us per launch
+    iv = _FakeOps.rec[1] + _FakeOps.rec[2]
+    assert abs(sum(b - a for a, b in [(1.0, 2.4)]) - 1.4) < 1e-12 and len(iv) == 4
+    out = tmp_path / "u.json"
+    subprocess.run([sys.executable, os.path.join(HERE, "..", "tools", "kunion.py"), str(path), "attn_bwd_dq_v3",
+                    "attn_bwd_dkv_v3", "--flops", "7e8", "--json", str(out)], check=True, capture_output=True)
+    d = json.loads(out.read_text())
+    assert d["source_kind"] == "bench_intervals" and d["launches"] == 2
+    assert abs(d["union_us_per_launch"] - 700.0) < 1e-6
+    assert abs(d["tflops"] - 1.0) < 1e-6  # 7e8 flop / 700 us
+
+
+def test_rocprof_union_reads_newest_trace_summary(tmp_path, monkeypatch):
+    import json
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    (prof / "r05_a_attn_bwd_union.json").write_text(json.dumps({"source_kind": "rocprofv3",
+                                                                "union_us_per_launch": 900.0}))
+    (prof / "r05_b_attn_bwd_union.json").write_text(json.dumps({"source_kind": "rocprofv3",
+                                                                "union_us_per_launch": 850.0}))
+    (prof / "r05_c_attn_bwd_union.json").write_text(json.dumps({"source_kind": "bench_intervals",
+                                                                "union_us_per_launch": 700.0}))
+    monkeypatch.setattr(bench, "HERE", str(tmp_path))
+    us, src = bench.rocprof_union("attn_bwd")
+    assert us == 850.0 and src.endswith("r05_b_attn_bwd_union.json")

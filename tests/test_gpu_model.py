@@ -548,6 +548,49 @@ def test_full_grid_fp32_forward_vs_oracle():
     assert _rel(c, rc) < 1e-3 and _rel(b, rb) < 1e-3 and _rel(i, ri) < 1e-3
 
 
+def test_config1_fp32_full_grid_train_step_vs_oracle():
+    """BASELINE config 1's workload on the HIP f32 path: IntentNetViT fp32, B = 1, the constants.py
+    grid (400x720, N = 4501 tokens per stream), train mode with the reference's DropPath 0.1
+    (factors injected into both), forward + DetectionIntentionLoss (downsampling keep mask
+    injected) + backward (train_vit.py:29,151-173) against the oracle's f32 step (plain PyTorch f32,
+    explicit attention, run on the GPU with torch's kernels: the CPU oracle step takes minutes).
+    Bars: outputs and loss terms 1e-3 relative (north_star); every parameter gradient 1e-3
+    relative L2 where it holds, 5e-3 for any (the train-mode BN + ReLU kink argument of
+    test_medium_grid_fp32_vs_oracle)."""
+    import loss as L
+    import utils
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    H, W, B, seed = 400, 720, 1, 2024
+    cfg = model_cfg(img_size=(H, W))
+    m = _model(cfg, torch.float32, dp=0.1).train()
+    sc = (_dp_scales(B, seed=5), _dp_scales(B, seed=6))
+    _set_dp(m, *sc)
+    lidar, mp, gts = O.synthetic_batch(B, (H, W), seed=seed)
+    anchors = utils.generate_anchors(H, W, 8, device=DEV)
+    keep = (torch.rand((B, anchors.shape[0]), generator=torch.Generator().manual_seed(seed)) < 0.15).float()
+    c, b, i = m(lidar.to(DEV), mp.to(DEV))
+    d = L.DetectionIntentionLoss()(c, b, i, anchors, gts, intent_keep=keep)
+    d["loss"].backward()
+    ours = {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()}
+    outs = (c.detach(), b.detach(), i.detach())
+    del m
+    (rc, rb, ri), rd, rg = _oracle_step(cfg, lidar, mp, gts, keep, sc, "explicit", False, autocast=False)
+    e_out = {k: _rel(x, y) for k, x, y in zip(("cls", "box", "int"), outs, (rc, rb, ri))}
+    for k in ("loss", "cls_loss", "box_loss", "intent_loss"):
+        e_out[k] = abs(float(d[k]) - float(rd[k])) / max(abs(float(rd[k])), 1e-12)
+    assert int(d["num_pos_anchors"]) == int(rd["num_pos_anchors"])
+    worst = sorted(((float((ours[k] - r.double().cpu()).norm() / (r.double().norm() + 1e-30)), k)
+                    for k, r in rg.items()), reverse=True)
+    n_strict = sum(1 for e, _ in worst if e < 1e-3)
+    print("config 1 fp32 400x720 B=1: outputs / losses", e_out, "\n  worst grad rel-L2:", worst[:6],
+          f"\n  {n_strict} of {len(worst)} parameter gradients within 1e-3")
+    assert len(worst) == len(ours)
+    for k, e in e_out.items():
+        assert e < 1e-3, (k, e_out)
+    assert worst[0][0] < 5e-3, worst[:6]
+
+
 def test_config4_eval_batch32_full_grid_vs_oracle():
     """BASELINE config 4 end to end (eval_vit.py:136-187): B = 32 full-grid bf16 inference, then
     sigmoid >= 0.1, decode, NMS(0.2), intention argmax for all 32 samples through the batched

@@ -443,6 +443,7 @@ bool conv_panel_ok(long M, long N, long Cin, long lda, long ks) {
 }
 
 int conv_wgrad_panel_splits(long M, long Cout, long N) {
+  if (M <= 0 || Cout <= 0 || N <= 0) return 1;
   const long tiles = (long)ivit_cdiv(Cout, 256) * ivit_cdiv(N, 256);
   long s = 256 / tiles;
   const long steps = (M + CW_BK - 1) / CW_BK;

@@ -490,6 +490,8 @@ static int patch_wgrad_t(const void* dtok, const float* img, long B, long C, lon
 extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* img, long B, long C, long H, long W,
                                       long D, float* dW, float* dbias, float* dpos, float* dcls, int accumulate,
                                       void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(B > 0 && C > 0 && H >= 8 && W >= 8 && D > 0, "patch wgrad: bad sizes (B %ld, C %ld, H %ld, W %ld, D %ld)",
+                 B, C, H, W, D);
   IVIT_CHECK_ARG(work_bytes >= ivit_patch_embed_wgrad_workspace(B, C, H, W, D), "patch wgrad: workspace too small");
   hipStream_t st = ivit_stream(stream);
   const bool bf = dtype == IVIT_BF16;
@@ -648,6 +650,7 @@ extern "C" int ivit_conv_dgrad(int dtype, const void* dY, long lddy, long B, lon
 }
 
 extern "C" long ivit_conv_wgrad_workspace(long B, long H, long W, long Cin, long Cout, long ks) {
+  if (B <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || ks <= 0) return 0;
   const long M = B * H * W, Kc = ks * ks * Cin;
   long s = wgrad_splits(Cout, Kc, M, false);
   const long s2 = wgrad_splits(Cout, Kc, M, true);
@@ -672,6 +675,9 @@ static int conv_wgrad_t(const void* dY, long lddy, const void* X, long B, long H
 extern "C" int ivit_conv_wgrad(int dtype, const void* dY, long lddy, const void* X, long B, long H, long W, long Cin,
                                long Cout, long ks, float* dWp, float* dbias, int accumulate, void* work,
                                long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(B > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && ks > 0 && lddy >= Cout,
+                 "ivit_conv_wgrad: bad sizes (B %ld, H %ld, W %ld, Cin %ld, Cout %ld, k %ld, lddy %ld)", B, H, W, Cin,
+                 Cout, ks, lddy);
   IVIT_CHECK_ARG(Cout % 8 == 0 && Cin % 8 == 0 && lddy % 8 == 0, "ivit_conv_wgrad: channel counts %% 8");
   IVIT_CHECK_ARG(work_bytes >= ivit_conv_wgrad_workspace(B, H, W, Cin, Cout, ks), "conv wgrad: workspace too small");
   hipStream_t st = ivit_stream(stream);

@@ -312,6 +312,8 @@ __global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long lon
 
 extern "C" int ivit_generate_anchors(long bev_h, long bev_w, long stride, const float* cfgs, long A, float voxel,
                                      float off_x, float off_y, float* out, void* stream) {
+  IVIT_CHECK_ARG(stride > 0 && bev_h >= 0 && bev_w >= 0 && A >= 0, "ivit_generate_anchors: bad sizes (stride %ld)",
+                 stride);
   const int fh = (int)(bev_h / stride), fw = (int)(bev_w / stride);
   const long n = (long)fh * fw * A;
   if (n <= 0) return 0;
