@@ -361,7 +361,9 @@ int ivit_lidar_bev(const void* points, int points_f64, long ld, const float* int
 /* Batched NMS (eval_vit.py:170 for every sample of a batch, one launch per stage): sample s
  * owns rows seg[s] .. seg[s+1]-1 (int64 device offsets) of boxes / scores / keep and the mask
  * words mask_off[s] .. + n_s * ceil(n_s / 64); keep receives LOCAL kept indices in score order,
- * count[s] their number. work >= 24 * total + 8 * mask_words + 64 bytes.                     */
+ * count[s] their number; the score order is a stable descending segmented radix sort.
+ * work >= ivit_nms_batched_workspace(n_samples, total, mask_words) bytes.                      */
+long ivit_nms_batched_workspace(long n_samples, long total, long mask_words);
 int ivit_nms_batched(const float* boxes_xywha, const float* scores, const long* seg, const long* mask_off,
                      long n_samples, long total, long max_n, long mask_words, double iou_thr, long* keep,
                      long* count, void* work, long work_bytes, void* stream);

@@ -153,14 +153,17 @@ def test_attention(B, N, H, cd):
         assert _rel(d[:, i], g[:, i]) < (1e-4 if cdt == F32 else 3e-2), ("qkv"[i], _rel(d[:, i], g[:, i]))
 
 
+@pytest.mark.parametrize("dkv16", ["0", "1"])
 @pytest.mark.parametrize("B,N,H", [(1, 64, 1), (2, 257, 3), (1, 4501, 2), (1, 1, 1), (1, 33, 1), (1, 128, 2),
                                    (1, 130, 1), (1, 200, 1), (1, 320, 2), (3, 449, 1)])
-def test_attention_q2_prescaled_path(B, N, H):
+def test_attention_q2_prescaled_path(B, N, H, dkv16, monkeypatch):
     """bf16 ViT-block path: the qkv projection stores q * log2(e)/8 (ivit_linear_fwd_qs) and the
     attention kernels run on it (ivit_attn_fwd_q2 / _bwd_q2). Outputs, lse and the gradient w.r.t.
-    the UNSCALED q, k, v against the f64 reference on the unscaled q (bf16 tolerances)."""
+    the UNSCALED q, k, v against the f64 reference on the unscaled q (bf16 tolerances). dkv16: the
+    dK/dV kernel in its v_mfma_f32_16x16x32_bf16 form (IVIT_ATTN_DKV16=1)."""
     import ops
     from _lib import BF16
+    monkeypatch.setenv("IVIT_ATTN_DKV16", dkv16)
     D = H * 64
     M, K = B * N, 96
     x = torch.randn(M, K)
@@ -923,17 +926,27 @@ def test_nms_batched_equals_per_sample_golden_and_oracle():
         assert np.array_equal(k.cpu().numpy(), w), i
 
 
-def test_nms_random_vs_oracle():
+@pytest.mark.parametrize("thr", [0.2, 0.0, -0.5])
+def test_nms_random_vs_oracle(thr):
+    """Single-sample and batched NMS vs the oracle; thr <= 0 takes the exact IoU path for disjoint
+    boxes too (the kernel skips the division only when it cannot change the decision)."""
     from oracle import ivit_oracle as O
     import utils
     g = torch.Generator().manual_seed(3)
+    bl, sl, want = [], [], []
     for n in (1, 63, 64, 65, 500, 4097):
         b = torch.stack([10 * torch.rand(n, generator=g), 10 * torch.rand(n, generator=g),
                          0.5 + 2 * torch.rand(n, generator=g), 0.5 + 2 * torch.rand(n, generator=g),
                          torch.zeros(n)], 1)
         s = torch.round(torch.rand(n, generator=g) * 8) / 8
-        keep = utils.apply_nms(b.to(DEV), s.to(DEV), 0.2).cpu().numpy()
-        assert np.array_equal(keep, O.nms_numpy(b.numpy(), s.numpy(), 0.2)), n
+        keep = utils.apply_nms(b.to(DEV), s.to(DEV), thr).cpu().numpy()
+        ref = O.nms_numpy(b.numpy(), s.numpy(), thr)
+        assert np.array_equal(keep, ref), n
+        bl.append(b.to(DEV))
+        sl.append(s.to(DEV))
+        want.append(ref)
+    for i, (k, w) in enumerate(zip(utils.nms_batched(bl, sl, thr), want)):
+        assert np.array_equal(k.cpu().numpy(), w), i
 
 
 def test_standalone_activation_and_head_modules():

@@ -39,6 +39,33 @@ d = ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H)
 ms = timeit(lambda: ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H))
 print(f"bwd q2: {ms:.4f} ms  {2 * fl / ms / 1e9:.1f} TF/s algorithmic (dQ, dK, dV, dP: 8*B*H*N^2*64)")
 
+
+def kernel_ms(fn, tags, it=20):
+    """mean execution interval per kernel (ivit_ktime_*: events bound to the kernel commands)"""
+    fn()
+    torch.cuda.synchronize()
+    ops.ktime_arm(True)
+    for _ in range(it):
+        fn()
+    torch.cuda.synchronize()
+    ops.ktime_arm(False)
+    return [sum(b - a for a, b in ops.ktime_read(t)) / it for t in tags]
+
+
+VARIANTS = [v for v in os.environ.get("ATTN_VARIANTS", "").split(";") if v]  # e.g. "IVIT_ATTN_DKV16=0;IVIT_ATTN_DKV16=1"
+for rep in range(2 if VARIANTS else 1):
+    for var in VARIANTS or [""]:
+        if var:
+            k_, v_ = var.split("=")
+            os.environ[k_] = v_
+        f_ms, = kernel_ms(lambda: ops.attn_fwd_q2(qkv, B, N, H), [0])
+        dq_ms, dkv_ms = kernel_ms(lambda: ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H), [1, 2])
+        pair = timeit(lambda: ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H))
+        print(f"[{var or 'default'}] kernels: fwd {f_ms:.4f} ms ({fl / f_ms / 1e9:.0f} TF/s), dQ {dq_ms:.4f} ms, "
+              f"dK/dV {dkv_ms:.4f} ms; bwd pair back-to-back {pair:.4f} ms ({2 * fl / pair / 1e9:.0f} TF/s, "
+              f"frac {2 * fl / pair / 1e9 / 2516.6:.4f})")
+d = ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H)
+
 # reference: f32 autograd of softmax(q k^T / 8) v on the same (unscaled) bf16 values
 q = (qkv[:, : H * 64].float() / ops.Q2_SCALE).view(B, N, H, 64).transpose(1, 2)
 k = qkv[:, H * 64: 2 * H * 64].float().view(B, N, H, 64).transpose(1, 2)

@@ -832,6 +832,271 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
   }
 }
 
+// ------------------------------------------------------------------------- backward v4 (16x16x32)
+// The dK/dV kernel with every product as v_mfma_f32_16x16x32_bf16 (MI355X_MICROARCH.md DVFS item 7:
+// at equal cycles per flop the 16x16x32 loops held a higher clock than 32x32x16). Same algorithm,
+// data flow, LDS stages and barrier cadence as v3; per wave 32 keys = 2 key blocks j of 16, per
+// 32-row query unit 2 query blocks i of 16:
+//   S_ij  = Q_i K_j^T  (C layout: lane (g = l >> 4, c = l & 15) holds rows 4g..4g+3 of q-block i,
+//                       key 16j + c),  dP_ij = dO_i V_j^T  — 16 MFMA per unit, K_j / V_j in registers
+//   dV_je += P_.j^T dO_.e,  dK_je += dS_.j^T Q_.e  (e = 16-column d block) — 16 MFMA per unit: the A
+//     operand of key block j is (S_0j, S_1j) packed as they stand (k slot 8g + jj <-> query
+//     4g + jj, jj < 4, else 16 + 4g + jj - 4), the B operand two transposing reads of 4 rows each.
+// The row constants enter as the S / dP chains' initial accumulators (4 rows per lane instead of
+// 16). Q / dO images: chunk c of row r at c ^ (r & 6) — conflict-free for the 16x16x32 row reads
+// (16 rows x one chunk per 16-lane group) and for the transposed reads (8 rows x 2 chunks per
+// half-wave); the 32x32 images' swz128 leaves the latter 2-way.
+IVIT_DEV int t16_off(int r, int c) { return r * 128 + ((c ^ (r & 6)) << 4); }
+
+template <int W>
+IVIT_DEV int dma_off16(int i, int wv, int lane, long ld) {
+  const int piece = wv * (8 / W) + i;
+  const int row = piece * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ (row & 6);
+  return (int)(row * ld) + c * 8;
+}
+
+IVIT_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf16* __restrict__ qkv,
+                                                                 const bf16* __restrict__ dout,
+                                                                 const float* __restrict__ nlse2p,
+                                                                 const float* __restrict__ ndeltap, int N, int Npad,
+                                                                 int H, bf16* __restrict__ dqkv, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][Q|dO]
+  __shared__ __attribute__((aligned(16))) float srow[BNS][2][AK];  // [stage][-lse2|-delta]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const bf16* Gb = dout + (long)b * N * D + h * 64;
+  const char* Ls = uniform_ptr(nlse2p + (long)z * Npad);
+  const char* Ds = uniform_ptr(ndeltap + (long)z * Npad);
+  constexpr int PW = 8 / W;
+  const int kw = bid.x * (32 * W) + wv * 32;
+  // B operands of S / dP: lane holds K[key 16j + c][dims 32s + 8g .. +7]
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int key = kw + 16 * j + c16;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Pack8 pk, pv;
+      pk.u = key < N ? *(const uint4*)(Kb + (long)key * ld + 32 * s + 8 * g) : make_uint4(0, 0, 0, 0);
+      pv.u = key < N ? *(const uint4*)(Vb + (long)key * ld + 32 * s + 8 * g) : make_uint4(0, 0, 0, 0);
+      kf[j][s] = pk.v;
+      vf[j][s] = pv.v;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) asm volatile("" ::"v"(kf[j][0]), "v"(kf[j][1]), "v"(vf[j][0]), "v"(vf[j][1]));
+  f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dk[j][e] = dv[j][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  unsigned offq[PW], offg[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    offq[i] = 2u * dma_off16<W>(i, wv, lane, ld);
+    offg[i] = 2u * dma_off16<W>(i, wv, lane, D);
+  }
+  auto issue = [&](int qt, int S) {
+    char* qimg = smem[S][0];
+    char* gimg = smem[S][1];
+    const char* qb = uniform_ptr(Qb + (long)qt * AK * ld);
+    const char* gb = uniform_ptr(Gb + (long)qt * AK * D);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int piece = wv * PW + i;
+      unsigned oq = offq[i], og = offg[i];
+      if (qt >= nfull) {
+        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ (row & 6);
+        const int r = min(qt * AK + row, N - 1) - qt * AK;
+        oq = 2u * (unsigned)(r * ld + c * 8);
+        og = 2u * (unsigned)(r * D + c * 8);
+      }
+      glds_s<false>(oq, qb, qimg + piece * 1024);
+      glds_s<false>(og, gb, gimg + piece * 1024);
+    }
+    if (wv == 0) {
+      glds4_s(4u * (lane + qt * AK), Ls, &srow[S][0][0]);
+      glds4_s(4u * (lane + qt * AK), Ds, &srow[S][1][0]);
+    }
+  };
+  // per-lane LDS offsets (the unit / block offsets 4096 t, 2048 i leave (r & 6) unchanged: immediates)
+  unsigned ro[2], tro[4];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) ro[s] = (unsigned)t16_off(c16, 4 * s + g);
+  {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tro[e] = (unsigned)(t16_off(4 * g + q, 2 * e + (p >> 1)) + 8 * (p & 1));
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) asm volatile("" : "+v"(ro[s]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(tro[e]));
+
+  bf16x8 qa[2][2], ga[2][2];   // A(u) fragments [i][s]
+  f32x4 sn[2], dn[2];          // A(u+1)'s initial accumulators (-lse2 / -delta of its rows), [i]
+  f32x4 sc[2][2], dc[2][2];    // A(u) results [i][j]: S' - lse2, dP - delta
+  unsigned up[2][4], ud[2][4];  // packed P / dS of the pending B, [j][word]
+  bf16x8 tg[4], tq[4];         // transposed dO / Q fragments of the pending B, [e]
+  auto read_frag = [&](const char* qimg, const char* gimg, int t, int i, int s) {
+    qa[i][s] = *(const bf16x8*)(qimg + ro[s] + 4096 * t + 2048 * i);
+    ga[i][s] = *(const bf16x8*)(gimg + ro[s] + 4096 * t + 2048 * i);
+  };
+  auto read_rows = [&](const float* lr, const float* dr, int t, int i) {
+    sn[i] = *(const f32x4*)(lr + 32 * t + 16 * i + 4 * g);
+    dn[i] = *(const f32x4*)(dr + 32 * t + 16 * i + 4 * g);
+  };
+  // E pair k (j = k >> 2, i = (k >> 1) & 1, half hh = k & 1): word 2i + hh of up[j] / ud[j]
+  auto e_pair = [&](int k) {
+    const int j = k >> 2, i = (k >> 1) & 1, hh = k & 1;
+    const float p0 = fast_exp2(sc[i][j][2 * hh]), p1 = fast_exp2(sc[i][j][2 * hh + 1]);
+    up[j][2 * i + hh] = pk_bf16(p0, p1);
+    ud[j][2 * i + hh] = pk_bf16(p0 * dc[i][j][2 * hh], p1 * dc[i][j][2 * hh + 1]);
+  };
+  auto word8 = [&](const unsigned (&w)[4]) { return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3])); };
+  auto read_b = [&](const char* qimg, const char* gimg, int t, int e) {
+    union { s16x4 s[2]; bf16x8 v; } a, c;
+    a.s[0] = ds_tr(gimg + tro[e] + 4096 * t);
+    a.s[1] = ds_tr(gimg + tro[e] + 4096 * t + 2048);
+    c.s[0] = ds_tr(qimg + tro[e] + 4096 * t);
+    c.s[1] = ds_tr(qimg + tro[e] + 4096 * t + 2048);
+    tg[e] = a.v;
+    tq[e] = c.v;
+  };
+  // body: A(u) on (SA, tA) || E(u-1); B(u-1) on (SB, tB) || reads of A(u+1) on (SN, tN).
+  auto body = [&](auto sa, auto ta, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
+    constexpr int SA = decltype(sa)::value, TA = decltype(ta)::value, SB = decltype(sb)::value;
+    constexpr int TB = decltype(tb)::value, SN = decltype(sn_)::value, TN = decltype(tn)::value;
+    constexpr bool BAR = decltype(bar)::value;
+    f32x4 s[2][2], dp[2][2];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int ks = m >> 3, i = (m >> 2) & 1, j = (m >> 1) & 1;
+      if ((m & 1) == 0) s[i][j] = mfma16(qa[i][ks], kf[j][ks], ks == 0 ? sn[i] : s[i][j]);
+      else dp[i][j] = mfma16(ga[i][ks], vf[j][ks], ks == 0 ? dn[i] : dp[i][j]);
+      if (m == 0) read_frag(smem[SA][0], smem[SA][1], TA, 0, 1);
+      if (m == 2) read_frag(smem[SA][0], smem[SA][1], TA, 1, 1);
+      if ((m & 1) == 0) e_pair(m >> 1);
+      if (m == 9) read_b(smem[SB][0], smem[SB][1], TB, 0);
+      if (m == 12) read_b(smem[SB][0], smem[SB][1], TB, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (BAR) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (jn < nt) issue(jn, jn % BNS);
+    }
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int e = m >> 2, j = (m >> 1) & 1;
+      if (m == 0) read_b(smem[SB][0], smem[SB][1], TB, 2);
+      if (m == 2) read_b(smem[SB][0], smem[SB][1], TB, 3);
+      if ((m & 1) == 0) dv[j][e] = mfma16(word8(up[j]), tg[e], dv[j][e]);
+      else dk[j][e] = mfma16(word8(ud[j]), tq[e], dk[j][e]);
+      if (more) {
+        if (m == 5) read_rows(srow[SN][0], srow[SN][1], TN, 0);
+        if (m == 7) read_rows(srow[SN][0], srow[SN][1], TN, 1);
+        if (m == 9) read_frag(smem[SN][0], smem[SN][1], TN, 0, 0);
+        if (m == 11) read_frag(smem[SN][0], smem[SN][1], TN, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        sc[i][j] = s[i][j];
+        dc[i][j] = dp[i][j];
+      }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using F = std::false_type;
+  using T = std::true_type;
+
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  {
+    uint4* z2 = (uint4*)&smem[2][0][0];  // B(-1)'s stage: finite zeros
+    for (int i = tid; i < 2 * 8192 / 16; i += 64 * W) z2[i] = make_uint4(0, 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    read_rows(srow[0][0], srow[0][1], 0, i);
+    read_frag(smem[0][0], smem[0][1], 0, i, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      sc[i][j] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};  // exp2 -> 0
+      dc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  auto tile = [&](auto st, int j) {
+    constexpr int S = decltype(st)::value;
+    using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
+    using SNX = std::integral_constant<int, (S + 1) % BNS>;
+    using SC = std::integral_constant<int, S>;
+    body(SC{}, I0{}, SP{}, I1{}, SC{}, I1{}, F{}, 0, true);
+    body(SC{}, I1{}, SC{}, I0{}, SNX{}, I0{}, T{}, j + 2, j + 1 < nt);
+  };
+  int j = 0;
+  for (; j + 3 <= nt; j += 3) {
+    tile(I0{}, j);
+    tile(I1{}, j + 1);
+    tile(I2{}, j + 2);
+  }
+  if (j < nt) tile(I0{}, j);
+  if (j + 1 < nt) tile(I1{}, j + 1);
+  {  // drain: E and B of the last unit (tile nt-1, rows 32..63)
+    const int S = (nt - 1) % BNS;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e_pair(k);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) read_b(smem[S][0], smem[S][1], 1, e);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        dv[jj][e] = mfma16(word8(up[jj]), tg[e], dv[jj][e]);
+        dk[jj][e] = mfma16(word8(ud[jj]), tq[e], dk[jj][e]);
+      }
+  }
+  // lane holds rows key 16j + 4g + r, column d = 16e + c16
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kk = kw + 16 * jj + 4 * g + r;
+      if (kk < N) {
+        bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          row[D + 16 * e + c16] = (bf16)(dk[jj][e][r] * scale);
+          row[2 * D + 16 * e + c16] = (bf16)dv[jj][e][r];
+        }
+      }
+    }
+}
+
 // dQ: 4 waves x 32 queries (prescaled Q and dO fragments in registers), key tiles of 64 rows;
 // also forms the queries' row constants (as attn_bwd_dq_v2_kernel<true, true>) and writes them
 // negated for the dK/dV kernel. The pipeline runs over the full key tiles; a ragged last tile
@@ -1306,8 +1571,14 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
   kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
             (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
-  kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
+  const char* dv16 = getenv("IVIT_ATTN_DKV16");  // A/B switch (read per launch: tests flip it)
+  const bool dkv16 = dv16 && atoi(dv16) == 1;
+  if (dkv16)
+    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
+  else
+    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -2,6 +2,8 @@
 // torchvision-CPU-exact non-maximum suppression.
 #include "geom.h"
 
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
 #pragma clang fp contract(off)
 
 using namespace ivit;
@@ -83,6 +85,20 @@ __global__ void nms_sorted_boxes_kernel(const float* __restrict__ b, const int* 
   sb[p * 5 + 4] = (x2 - x1) * (y2 - y1);
 }
 
+// torchvision's test, bit for bit: (double)(inter / (area_i + area_j - inter)) > thr in f32. Disjoint
+// boxes (inter = 0, most pairs) give 0 / union = +-0 or NaN, never > a threshold >= 0: the f32
+// division (a ~10-instruction VALU sequence) runs only for overlapping pairs or a negative threshold.
+IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float ia, const float (&c)[5], double thr,
+                             bool thr_nonneg) {
+  const float xx1 = fmaxf(ix1, c[0]), yy1 = fmaxf(iy1, c[1]);
+  const float xx2 = fminf(ix2, c[2]), yy2 = fminf(iy2, c[3]);
+  const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+  const float inter = w * h;
+  if (thr_nonneg && !(inter > 0.f)) return false;
+  const float ovr = inter / ((ia + c[4]) - inter);
+  return (double)ovr > thr;
+}
+
 // mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr.
 __global__ void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, double thr,
                                 unsigned long long* __restrict__ mask) {
@@ -99,28 +115,30 @@ __global__ void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, do
   const float ix1 = sb[i * 5 + 0], iy1 = sb[i * 5 + 1], ix2 = sb[i * 5 + 2], iy2 = sb[i * 5 + 3],
               ia = sb[i * 5 + 4];
   unsigned long long bits = 0;
+  const bool thr_nonneg = thr >= 0.0;
   const int lim = (int)min((long)64, n - (long)cb * 64);
   for (int k = 0; k < lim; ++k) {
     const long j = (long)cb * 64 + k;
     if (j <= i) continue;
-    const float xx1 = fmaxf(ix1, cbx[k][0]), yy1 = fmaxf(iy1, cbx[k][1]);
-    const float xx2 = fminf(ix2, cbx[k][2]), yy2 = fminf(iy2, cbx[k][3]);
-    const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
-    const float inter = w * h;
-    const float ovr = inter / ((ia + cbx[k][4]) - inter);
-    if ((double)ovr > thr) bits |= 1ull << k;
+    if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cbx[k], thr, thr_nonneg)) bits |= 1ull << k;
   }
   mask[i * nw + cb] = bits;
 }
 
 constexpr int NMS_MAXW = 1024;  // n <= 65536
 
-__global__ __launch_bounds__(256) void nms_scan_kernel(const unsigned long long* __restrict__ mask, long n, int nw,
-                                                       const int* __restrict__ order, long* __restrict__ keep,
-                                                       long* __restrict__ count) {
+// The greedy walk of torchvision's nms over the suppression mask (one workgroup per sample):
+// column block c (64 sorted boxes) is settled by wave 0 on SCALAR registers (each diagonal word
+// read by v_readlane; the serial 64-step chain runs on the scalar unit), then the kept boxes'
+// mask rows are OR-ed into the removed words of the later columns by all 256 threads, 32 word
+// lanes x 8 kept-box groups, with 64-bit LDS atomic ORs: a column's loads are independent
+// (the earlier per-word loop over the kept bits waited for each load in turn).
+IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n, int nw, const int* __restrict__ order,
+                            long* __restrict__ keep, long* __restrict__ count_out) {
   __shared__ unsigned long long removed[NMS_MAXW];
   __shared__ unsigned long long kept_s;
   __shared__ long cnt_s;
+  __shared__ int kbit[64];
   for (int w = threadIdx.x; w < nw; w += 256) removed[w] = 0ull;
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
@@ -129,20 +147,23 @@ __global__ __launch_bounds__(256) void nms_scan_kernel(const unsigned long long*
     if (threadIdx.x < 64) {
       const long row = (long)c * 64 + lane;
       const unsigned long long diag = row < n ? mask[row * nw + c] : 0ull;
-      unsigned long long w = removed[c];
+      const unsigned dlo = (unsigned)diag, dhi = (unsigned)(diag >> 32);
+      const unsigned long long r0 = removed[c];
+      unsigned long long w = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(r0 >> 32)) << 32) |
+                             __builtin_amdgcn_readfirstlane((unsigned)r0);
       unsigned long long kept = 0ull;
       const int lim = (int)min((long)64, n - (long)c * 64);
       for (int i = 0; i < lim; ++i) {
-        const unsigned long long d = __shfl(diag, i, 64);
         if (!((w >> i) & 1ull)) {
           kept |= 1ull << i;
-          w |= d;
+          w |= ((unsigned long long)__builtin_amdgcn_readlane(dhi, i) << 32) | __builtin_amdgcn_readlane(dlo, i);
         }
       }
       const long base = cnt_s;
       if ((kept >> lane) & 1ull) {
-        const unsigned long long below = lane ? (kept & ((1ull << lane) - 1ull)) : 0ull;
-        keep[base + __popcll(below)] = order[row];
+        const int rk = __popcll(lane ? (kept & ((1ull << lane) - 1ull)) : 0ull);
+        keep[base + rk] = order[row];
+        kbit[rk] = lane;
       }
       if (lane == 0) {
         kept_s = kept;
@@ -150,50 +171,40 @@ __global__ __launch_bounds__(256) void nms_scan_kernel(const unsigned long long*
       }
     }
     __syncthreads();
-    const unsigned long long kept = kept_s;
-    if (kept) {
-      for (int wc = c + 1 + threadIdx.x; wc < nw; wc += 256) {
-        unsigned long long acc = removed[wc];
-        unsigned long long kb = kept;
-        while (kb) {
-          const int i = __ffsll((long long)kb) - 1;
-          kb &= kb - 1;
-          acc |= mask[((long)c * 64 + i) * nw + wc];
-        }
-        removed[wc] = acc;
+    const int K = __popcll(kept_s);
+    if (K) {
+      const int wl = threadIdx.x & 31, bg = threadIdx.x >> 5;
+      for (int wc = c + 1 + wl; wc < nw; wc += 32) {
+        unsigned long long acc = 0ull;
+        for (int b = bg; b < K; b += 8) acc |= mask[((long)c * 64 + kbit[b]) * nw + wc];
+        if (acc) atomicOr(&removed[wc], acc);
       }
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *count = cnt_s;
+  if (threadIdx.x == 0) *count_out = cnt_s;
+}
+
+__global__ __launch_bounds__(256) void nms_scan_kernel(const unsigned long long* __restrict__ mask, long n, int nw,
+                                                       const int* __restrict__ order, long* __restrict__ keep,
+                                                       long* __restrict__ count) {
+  nms_scan_body(mask, n, nw, order, keep, count);
 }
 
 // ---- batched NMS: sample s owns rows seg[s] .. seg[s+1]-1 of every per-row array and the
 // mask words mask_off[s] .. ; blockIdx.y (rank / sorted boxes / scan) or blockIdx.z (mask)
 // selects the sample, so all samples' kernels run in one launch each (the single-workgroup
 // scan of one sample no longer serialises the batch).
-__global__ void nms_rank_b_kernel(const float* __restrict__ scores, const long* __restrict__ seg,
-                                  int* __restrict__ order) {
-  __shared__ float tile[256];
+// keys / values of the segmented sort: the score (+0.0f: a -0 score ties with +0 as in torch's
+// comparison sort) and the row's local index.
+__global__ void nms_keys_b_kernel(const float* __restrict__ scores, const long* __restrict__ seg, float* __restrict__ key,
+                                  int* __restrict__ idx) {
   const int sm = blockIdx.y;
   const long o = seg[sm], n = seg[sm + 1] - o;
-  if ((long)blockIdx.x * 256 >= n) return;
-  const float* s = scores + o;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  const float si = i < n ? s[i] : 0.f;
-  long rank = 0;
-  for (long j0 = 0; j0 < n; j0 += 256) {
-    __syncthreads();
-    if (j0 + threadIdx.x < n) tile[threadIdx.x] = s[j0 + threadIdx.x];
-    __syncthreads();
-    const int lim = (int)min((long)256, n - j0);
-    for (int k = 0; k < lim; ++k) {
-      const float sj = tile[k];
-      const long j = j0 + k;
-      rank += (sj > si) || (sj == si && j < i);
-    }
-  }
-  if (i < n) order[o + rank] = (int)i;
+  if (i >= n) return;
+  key[o + i] = scores[o + i] + 0.0f;
+  idx[o + i] = (int)i;
 }
 
 __global__ void nms_sorted_boxes_b_kernel(const float* __restrict__ b, const int* __restrict__ order,
@@ -233,16 +244,12 @@ __global__ void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* 
   const float ix1 = sb[i * 5 + 0], iy1 = sb[i * 5 + 1], ix2 = sb[i * 5 + 2], iy2 = sb[i * 5 + 3],
               ia = sb[i * 5 + 4];
   unsigned long long bits = 0;
+  const bool thr_nonneg = thr >= 0.0;
   const int lim = (int)min((long)64, n - (long)cb * 64);
   for (int k = 0; k < lim; ++k) {
     const long j = (long)cb * 64 + k;
     if (j <= i) continue;
-    const float xx1 = fmaxf(ix1, cbx[k][0]), yy1 = fmaxf(iy1, cbx[k][1]);
-    const float xx2 = fminf(ix2, cbx[k][2]), yy2 = fminf(iy2, cbx[k][3]);
-    const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
-    const float inter = w * h;
-    const float ovr = inter / ((ia + cbx[k][4]) - inter);
-    if ((double)ovr > thr) bits |= 1ull << k;
+    if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cbx[k], thr, thr_nonneg)) bits |= 1ull << k;
   }
   mask[i * nw + cb] = bits;
 }
@@ -254,58 +261,7 @@ __global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long lon
                                                          long* __restrict__ keep_all, long* __restrict__ count) {
   const int sm = blockIdx.x;
   const long o = seg[sm], n = seg[sm + 1] - o;
-  const int nw = (int)((n + 63) / 64);
-  const unsigned long long* mask = mask_all + mask_off[sm];
-  const int* order = order_all + o;
-  long* keep = keep_all + o;
-  __shared__ unsigned long long removed[NMS_MAXW];
-  __shared__ unsigned long long kept_s;
-  __shared__ long cnt_s;
-  for (int w = threadIdx.x; w < nw; w += 256) removed[w] = 0ull;
-  if (threadIdx.x == 0) cnt_s = 0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  for (int c = 0; c < nw; ++c) {
-    if (threadIdx.x < 64) {
-      const long row = (long)c * 64 + lane;
-      const unsigned long long diag = row < n ? mask[row * nw + c] : 0ull;
-      unsigned long long w = removed[c];
-      unsigned long long kept = 0ull;
-      const int lim = (int)min((long)64, n - (long)c * 64);
-      for (int i = 0; i < lim; ++i) {
-        const unsigned long long d = __shfl(diag, i, 64);
-        if (!((w >> i) & 1ull)) {
-          kept |= 1ull << i;
-          w |= d;
-        }
-      }
-      const long base = cnt_s;
-      if ((kept >> lane) & 1ull) {
-        const unsigned long long below = lane ? (kept & ((1ull << lane) - 1ull)) : 0ull;
-        keep[base + __popcll(below)] = order[row];
-      }
-      if (lane == 0) {
-        kept_s = kept;
-        cnt_s = base + __popcll(kept);
-      }
-    }
-    __syncthreads();
-    const unsigned long long kept = kept_s;
-    if (kept) {
-      for (int wc = c + 1 + threadIdx.x; wc < nw; wc += 256) {
-        unsigned long long acc = removed[wc];
-        unsigned long long kb = kept;
-        while (kb) {
-          const int i = __ffsll((long long)kb) - 1;
-          kb &= kb - 1;
-          acc |= mask[((long)c * 64 + i) * nw + wc];
-        }
-        removed[wc] = acc;
-      }
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) count[sm] = cnt_s;
+  nms_scan_body(mask_all + mask_off[sm], n, (int)((n + 63) / 64), order_all + o, keep_all + o, count + sm);
 }
 
 }  // namespace
@@ -381,14 +337,36 @@ extern "C" int ivit_nms(const float* boxes_xywha, const float* scores, long n, d
 // Batched torchvision-CPU-exact NMS (eval_vit.py:170 per sample, all samples in one launch per
 // stage). seg: [S+1] int64 row offsets (device); mask_off: [S] int64 word offsets of each
 // sample's [n_s, ceil(n_s/64)] suppression mask (device). keep[seg[s] ..] receives sample s's kept
-// LOCAL indices in score order, count[s] their number. Workspace (bytes) >= 24 * total + 8 *
-// mask_words + 64.
+// LOCAL indices in score order, count[s] their number. The score order is a stable descending
+// segmented radix sort (rocPRIM; ties keep the row order, as torch's stable sort). Workspace:
+// ivit_nms_batched_workspace(n_samples, total, mask_words) bytes.
+namespace {
+size_t nms_sort_temp_bytes(long n_samples, long total) {
+  size_t bytes = 0;
+  if (rocprim::segmented_radix_sort_pairs_desc(nullptr, bytes, (const float*)nullptr, (float*)nullptr,
+                                               (const int*)nullptr, (int*)nullptr, (unsigned)total,
+                                               (unsigned)n_samples, (const long*)nullptr, (const long*)nullptr) !=
+      hipSuccess)
+    return 0;
+  return bytes;
+}
+long al16(long b) { return (b + 15) / 16 * 16; }
+}  // namespace
+
+extern "C" long ivit_nms_batched_workspace(long n_samples, long total, long mask_words) {
+  if (n_samples <= 0 || total <= 0) return 64;
+  return al16(4 * total) + al16(20 * total) + al16(8 * mask_words) + 2 * al16(4 * total) + al16(4 * total) +
+         al16((long)nms_sort_temp_bytes(n_samples, total)) + 256 + 64;
+}
+
 extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, const long* seg, const long* mask_off,
                                 long n_samples, long total, long max_n, long mask_words, double iou_thr, long* keep,
                                 long* count, void* work, long work_bytes, void* stream) {
   IVIT_CHECK_ARG(max_n <= 64L * NMS_MAXW, "ivit_nms_batched: n=%ld exceeds %d", max_n, 64 * NMS_MAXW);
-  IVIT_CHECK_ARG(n_samples < 65536, "ivit_nms_batched: too many samples (%ld)", n_samples);
-  IVIT_CHECK_ARG(work_bytes >= 24 * total + 8 * mask_words + 64, "ivit_nms_batched: workspace too small");
+  IVIT_CHECK_ARG(n_samples < 65536 && total < (1L << 31), "ivit_nms_batched: too many samples / rows (%ld, %ld)",
+                 n_samples, total);
+  IVIT_CHECK_ARG(work_bytes >= ivit_nms_batched_workspace(n_samples, total, mask_words),
+                 "ivit_nms_batched: workspace too small");
   hipStream_t st = ivit_stream(stream);
   if (n_samples <= 0) return 0;
   if (max_n <= 0) {
@@ -397,14 +375,29 @@ extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, c
     return 0;
   }
   const int nwmax = (int)((max_n + 63) / 64);
-  char* w = (char*)work;
+  char* w = (char*)(((uintptr_t)work + 15) & ~(uintptr_t)15);
   int* order = (int*)w;
-  w += (total * 4 + 15) / 16 * 16;
+  w += al16(4 * total);
   float* sb = (float*)w;
-  w += (total * 20 + 15) / 16 * 16;
+  w += al16(20 * total);
   unsigned long long* mask = (unsigned long long*)w;
+  w += al16(8 * mask_words);
+  float* key = (float*)w;
+  w += al16(4 * total);
+  float* key_sorted = (float*)w;
+  w += al16(4 * total);
+  int* idx = (int*)w;
+  w += al16(4 * total);
+  w = (char*)(((uintptr_t)w + 255) & ~(uintptr_t)255);
+  size_t tb = nms_sort_temp_bytes(n_samples, total);
   const int gx = ivit_cdiv(max_n, 256);
-  hipLaunchKernelGGL(nms_rank_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, scores, seg, order);
+  hipLaunchKernelGGL(nms_keys_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, scores, seg, key, idx);
+  const hipError_t e = rocprim::segmented_radix_sort_pairs_desc(w, tb, key, key_sorted, idx, order, (unsigned)total,
+                                                               (unsigned)n_samples, seg, seg + 1, 0, 32, st);
+  if (e != hipSuccess) {
+    ivit_set_error("ivit_nms_batched: segmented sort: %s", hipGetErrorString(e));
+    return (int)e;
+  }
   hipLaunchKernelGGL(nms_sorted_boxes_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, boxes_xywha, order, seg, sb);
   hipLaunchKernelGGL(nms_mask_b_kernel, dim3(nwmax, nwmax, n_samples), dim3(64), 0, st, sb, seg, mask_off, iou_thr,
                      mask);

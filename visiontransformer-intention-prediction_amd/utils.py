@@ -111,7 +111,7 @@ def nms_batched(boxes_list, scores_list, iou_threshold: float = 0.2):
     d_moff = torch.from_numpy(moff).to(dev, non_blocking=True)
     keep = torch.empty((total,), dtype=torch.int64, device=dev)
     count = torch.empty((S,), dtype=torch.int64, device=dev)
-    ws = workspace(24 * total + 8 * sum(words) + 64, dev)
+    ws = workspace(lib.ivit_nms_batched_workspace(S, total, sum(words)), dev)
     lib.ivit_nms_batched(ptr(b), ptr(sc), ptr(d_seg), ptr(d_moff), S, total, max(ns), sum(words),
                          float(iou_threshold), ptr(keep), ptr(count), ptr(ws), ws.numel(), stream())
     cnt = count.cpu().tolist()
