@@ -75,6 +75,17 @@ rows = [
      M * 3 * D * B2 + M * D * (F4 + F4 + F4) + 8 * M, 2.0 * M * D * 3 * D),
     ("bwd qkv wgrad", lambda: ops.linear_wgrad(dqkv, ln, BF16), M * 4 * D * B2, 2.0 * M * 3 * D * D),
 ]
+# WIDE_AB="ENV=V;ENV=V;...": only the wide row-panel kernels, once per variant, twice over (same-call A/B)
+if os.environ.get("WIDE_AB"):
+    wide = [r for r in rows if r[0].startswith(("fwd qkv", "fwd fc1 + GELU (+GELU')", "bwd fc2 dgrad x G"))]
+    for rep in range(2):
+        for var in os.environ["WIDE_AB"].split(";"):
+            for kv in var.split(","):
+                k_, v_ = kv.split("=")
+                os.environ[k_] = v_
+            res = [(name, timeit(fn) * 1e3, max(by / 6.3e12, fl / 2516.6e12) * 1e6) for name, fn, by, fl in wide]
+            print(f"[{var}] " + "; ".join(f"{n}: {t:.1f} us ({t / f:.2f}x floor)" for n, t, f in res))
+    sys.exit(0)
 tot = tot_floor = 0.0
 print(f"{'kernel':32s} {'us':>8s} {'TF/s':>7s} {'GB/s':>7s} {'hbm-floor':>9s} {'mfma-floor':>10s}  ratio")
 for name, fn, by, fl in rows:
