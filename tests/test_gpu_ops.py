@@ -600,9 +600,6 @@ def test_linear_dgrad_ln_bwd_fused(M, K, xs):
         assert _rel(dxs.float(), r2) < 4e-3
 
 
-@pytest.mark.parametrize("M,N,K,mode", [(36008, 1152, 384, "qs"), (36008, 1536, 384, "gelu"), (300, 768, 128, "gelu"),
-                                        (145, 1536, 384, "dgelu"), (36008, 1536, 384, "dgelu"), (1, 384, 64, "qs"),
-                                        (36008, 384, 384, "dgrad"), (77, 384, 384, "dgrad")])
 def _wide_env(epi, monkeypatch):
     """epi "0" / "1" / "2": IVIT_WIDE_EPI; "pK": the LDS-tile form as the persistent, staggered
     grid (IVIT_WIDE_PERSIST=K)."""
@@ -614,6 +611,9 @@ def _wide_env(epi, monkeypatch):
         monkeypatch.setenv("IVIT_WIDE_PERSIST", "0")
 
 
+@pytest.mark.parametrize("M,N,K,mode", [(36008, 1152, 384, "qs"), (36008, 1536, 384, "gelu"), (300, 768, 128, "gelu"),
+                                        (145, 1536, 384, "dgelu"), (36008, 1536, 384, "dgelu"), (1, 384, 64, "qs"),
+                                        (36008, 384, 384, "dgrad"), (77, 384, 384, "dgrad")])
 @pytest.mark.parametrize("epi", ["0", "2", "p2"])
 def test_panel_wide(M, N, K, mode, epi, monkeypatch):
     """Row-panel wide GEMMs (ivit_linear_fwd_panel / ivit_linear_dgrad_gelu_panel) vs the generic

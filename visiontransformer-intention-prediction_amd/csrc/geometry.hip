@@ -149,14 +149,17 @@ IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n,
       const unsigned long long diag = row < n ? mask[row * nw + c] : 0ull;
       const unsigned dlo = (unsigned)diag, dhi = (unsigned)(diag >> 32);
       const unsigned long long r0 = removed[c];
-      unsigned long long w = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(r0 >> 32)) << 32) |
-                             __builtin_amdgcn_readfirstlane((unsigned)r0);
+      // (the builtins return int: widen through unsigned, or the low word sign-extends)
+      unsigned long long w =
+          ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(r0 >> 32)) << 32) |
+          (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)r0);
       unsigned long long kept = 0ull;
       const int lim = (int)min((long)64, n - (long)c * 64);
       for (int i = 0; i < lim; ++i) {
         if (!((w >> i) & 1ull)) {
           kept |= 1ull << i;
-          w |= ((unsigned long long)__builtin_amdgcn_readlane(dhi, i) << 32) | __builtin_amdgcn_readlane(dlo, i);
+          w |= ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(dhi, i) << 32) |
+               (unsigned long long)(unsigned)__builtin_amdgcn_readlane(dlo, i);
         }
       }
       const long base = cnt_s;
