@@ -177,9 +177,17 @@ IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n,
     const int K = __popcll(kept_s);
     if (K) {
       const int wl = threadIdx.x & 31, bg = threadIdx.x >> 5;
+      const unsigned long long* blk = mask + (long)c * 64 * nw;
       for (int wc = c + 1 + wl; wc < nw; wc += 32) {
+        unsigned long long v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {  // up to 8 independent loads in flight per thread
+          const int b = bg + 8 * q;
+          v[q] = b < K ? blk[(long)kbit[b] * nw + wc] : 0ull;
+        }
         unsigned long long acc = 0ull;
-        for (int b = bg; b < K; b += 8) acc |= mask[((long)c * 64 + kbit[b]) * nw + wc];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc |= v[q];
         if (acc) atomicOr(&removed[wc], acc);
       }
     }
