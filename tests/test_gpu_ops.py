@@ -600,28 +600,16 @@ def test_linear_dgrad_ln_bwd_fused(M, K, xs):
         assert _rel(dxs.float(), r2) < 4e-3
 
 
-def _wide_env(epi, monkeypatch):
-    """epi "0" / "1" / "2": IVIT_WIDE_EPI; "pK": the LDS-tile form as the persistent, staggered
-    grid (IVIT_WIDE_PERSIST=K)."""
-    if epi.startswith("p"):
-        monkeypatch.setenv("IVIT_WIDE_EPI", "0")
-        monkeypatch.setenv("IVIT_WIDE_PERSIST", epi[1:])
-    else:
-        monkeypatch.setenv("IVIT_WIDE_EPI", epi)
-        monkeypatch.setenv("IVIT_WIDE_PERSIST", "0")
-
-
 @pytest.mark.parametrize("M,N,K,mode", [(36008, 1152, 384, "qs"), (36008, 1536, 384, "gelu"), (300, 768, 128, "gelu"),
                                         (145, 1536, 384, "dgelu"), (36008, 1536, 384, "dgelu"), (1, 384, 64, "qs"),
                                         (36008, 384, 384, "dgrad"), (77, 384, 384, "dgrad")])
-@pytest.mark.parametrize("epi", ["0", "2", "p2"])
+@pytest.mark.parametrize("epi", ["0", "2"])
 def test_panel_wide(M, N, K, mode, epi, monkeypatch):
     """Row-panel wide GEMMs (ivit_linear_fwd_panel / ivit_linear_dgrad_gelu_panel) vs the generic
     engine on the same bf16 operands (qkv with the prescaled Q block, fc1 + GELU + pre-activation,
     fc2 dgrad x GELU'): equal up to f32 summation order and the bf16 rounding of the output. Both
-    epilogue forms: IVIT_WIDE_EPI=0 (the default LDS-tile form), 2 (transposed accumulators), and the
-    persistent staggered grid (p2)."""
-    _wide_env(epi, monkeypatch)
+    epilogue forms: IVIT_WIDE_EPI=0 (the default LDS-tile form), 2 (transposed accumulators)."""
+    monkeypatch.setenv("IVIT_WIDE_EPI", epi)
     import ops
     from _lib import ACT_GELU, BF16
     g = torch.Generator().manual_seed(M + N + K)
@@ -652,14 +640,13 @@ def test_panel_wide(M, N, K, mode, epi, monkeypatch):
 
 
 @pytest.mark.parametrize("M,N,K", [(36008, 1536, 384), (300, 768, 128), (145, 1536, 384), (1, 384, 64)])
-@pytest.mark.parametrize("epi", ["0", "1", "2", "p2"])
+@pytest.mark.parametrize("epi", ["0", "1", "2"])
 def test_panel_gelu_derivative_pair(M, N, K, epi, monkeypatch):
     """fc1 with GELU' as its second output (act GELU_D: y = gelu(z), g = gelu'(z) from the f32 z =
     x W^T + b) and the fc2 dgrad that multiplies by it (ivit_linear_dgrad_mul_panel), vs torch on
     the same bf16 operands: z in f64, exact-erf GELU / GELU' (bf16-output tolerance); every
-    epilogue form (IVIT_WIDE_EPI 0: LDS tile, 1: transposed GELU_D, 2: transposed for both; p2: the
-    LDS tile on the persistent staggered grid)."""
-    _wide_env(epi, monkeypatch)
+    epilogue form (IVIT_WIDE_EPI 0: LDS tile, 1: transposed GELU_D, 2: transposed for both)."""
+    monkeypatch.setenv("IVIT_WIDE_EPI", epi)
     import ops
     from _lib import ACT_GELU_D, BF16
     g = torch.Generator().manual_seed(7 * M + N + K)

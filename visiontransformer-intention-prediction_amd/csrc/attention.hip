@@ -1571,8 +1571,10 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
   kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
             (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
-  const char* dv16 = getenv("IVIT_ATTN_DKV16");  // A/B switch (read per launch: tests flip it)
-  const bool dkv16 = dv16 && atoi(dv16) == 1;
+  // dK/dV: the 16x16x32 form (v4) by default — isolated 0.441-0.445 -> 0.406 ms, same call
+  // (profiles/r05_b_attn_dkv16_ab.txt); IVIT_ATTN_DKV16=0 restores v3 (A/B, read per launch)
+  const char* dv16 = getenv("IVIT_ATTN_DKV16");
+  const bool dkv16 = !(dv16 && atoi(dv16) == 0);
   if (dkv16)
     kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
               (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);

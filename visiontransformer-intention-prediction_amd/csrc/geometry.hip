@@ -88,41 +88,60 @@ __global__ void nms_sorted_boxes_kernel(const float* __restrict__ b, const int* 
 // torchvision's test, bit for bit: (double)(inter / (area_i + area_j - inter)) > thr in f32. Disjoint
 // boxes (inter = 0, most pairs) give 0 / union = +-0 or NaN, never > a threshold >= 0: the f32
 // division (a ~10-instruction VALU sequence) runs only for overlapping pairs or a negative threshold.
-IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float ia, const float (&c)[5], double thr,
+IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float ia, float4 c, float ca, double thr,
                              bool thr_nonneg) {
-  const float xx1 = fmaxf(ix1, c[0]), yy1 = fmaxf(iy1, c[1]);
-  const float xx2 = fminf(ix2, c[2]), yy2 = fminf(iy2, c[3]);
+  const float xx1 = fmaxf(ix1, c.x), yy1 = fmaxf(iy1, c.y);
+  const float xx2 = fminf(ix2, c.z), yy2 = fminf(iy2, c.w);
   const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
   const float inter = w * h;
   if (thr_nonneg && !(inter > 0.f)) return false;
-  const float ovr = inter / ((ia + c[4]) - inter);
+  const float ovr = inter / ((ia + ca) - inter);
   return (double)ovr > thr;
 }
 
-// mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr.
-__global__ void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, double thr,
-                                unsigned long long* __restrict__ mask) {
-  const int cb = blockIdx.x, rb = blockIdx.y;
-  if (cb < rb) return;
-  __shared__ float cbx[64][5];
+// One 64-thread workgroup per (row block rb, chunk of NMS_CB column blocks): rows rb*64 + t against
+// the column blocks cb >= rb of its chunk, each staged through LDS as corners (one ds_read_b128)
+// and area (ds_read_b32) — NMS_CB times fewer workgroups than one per (rb, cb), most of which had
+// nothing to do (cb < rb) or one short loop.
+constexpr int NMS_CB = 8;
+IVIT_DEV void nms_mask_body(const float* __restrict__ sb, long n, int nw, double thr,
+                            unsigned long long* __restrict__ mask, int rb, int cb0) {
+  __shared__ float4 cxy[64];
+  __shared__ float car[64];
   const int t = threadIdx.x;
-  const long cj = (long)cb * 64 + t;
-  if (cj < n)
-    for (int k = 0; k < 5; ++k) cbx[t][k] = sb[cj * 5 + k];
-  __syncthreads();
   const long i = (long)rb * 64 + t;
-  if (i >= n) return;
-  const float ix1 = sb[i * 5 + 0], iy1 = sb[i * 5 + 1], ix2 = sb[i * 5 + 2], iy2 = sb[i * 5 + 3],
-              ia = sb[i * 5 + 4];
-  unsigned long long bits = 0;
-  const bool thr_nonneg = thr >= 0.0;
-  const int lim = (int)min((long)64, n - (long)cb * 64);
-  for (int k = 0; k < lim; ++k) {
-    const long j = (long)cb * 64 + k;
-    if (j <= i) continue;
-    if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cbx[k], thr, thr_nonneg)) bits |= 1ull << k;
+  float ix1 = 0.f, iy1 = 0.f, ix2 = 0.f, iy2 = 0.f, ia = 0.f;
+  if (i < n) {
+    ix1 = sb[i * 5 + 0]; iy1 = sb[i * 5 + 1]; ix2 = sb[i * 5 + 2]; iy2 = sb[i * 5 + 3]; ia = sb[i * 5 + 4];
   }
-  mask[i * nw + cb] = bits;
+  const bool thr_nonneg = thr >= 0.0;
+  const int cb1 = min(cb0 + NMS_CB, nw);
+  for (int cb = max(cb0, rb); cb < cb1; ++cb) {
+    __syncthreads();  // the previous block's reads of cxy / car are done
+    const long cj = (long)cb * 64 + t;
+    if (cj < n) {
+      cxy[t] = make_float4(sb[cj * 5 + 0], sb[cj * 5 + 1], sb[cj * 5 + 2], sb[cj * 5 + 3]);
+      car[t] = sb[cj * 5 + 4];
+    }
+    __syncthreads();
+    if (i < n) {
+      unsigned long long bits = 0;
+      const int lim = (int)min((long)64, n - (long)cb * 64);
+      const int k0 = cb == rb ? t + 1 : 0;  // the diagonal block: only boxes after this one
+      for (int k = k0; k < lim; ++k)
+        if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cxy[k], car[k], thr, thr_nonneg)) bits |= 1ull << k;
+      mask[i * nw + cb] = bits;
+    }
+  }
+}
+
+// mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr.
+// grid (ceil(nw / NMS_CB), nw)
+__global__ __launch_bounds__(64) void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, double thr,
+                                                      unsigned long long* __restrict__ mask) {
+  const int cb0 = blockIdx.x * NMS_CB, rb = blockIdx.y;
+  if (cb0 + NMS_CB <= rb) return;
+  nms_mask_body(sb, n, nw, thr, mask, rb, cb0);
 }
 
 constexpr int NMS_MAXW = 1024;  // n <= 65536
@@ -143,10 +162,19 @@ IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n,
   if (threadIdx.x == 0) cnt_s = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
+  // wave 0 holds the next column's diagonal word and sorted index, loaded during the current
+  // column's update (neither depends on it): the walk does not wait on a global load
+  unsigned long long diag_n = 0ull;
+  int ord_n = 0;
+  if (threadIdx.x < 64 && lane < n) {
+    diag_n = mask[(long)lane * nw];
+    ord_n = order[lane];
+  }
   for (int c = 0; c < nw; ++c) {
     if (threadIdx.x < 64) {
       const long row = (long)c * 64 + lane;
-      const unsigned long long diag = row < n ? mask[row * nw + c] : 0ull;
+      const unsigned long long diag = diag_n;
+      const int ord = ord_n;
       const unsigned dlo = (unsigned)diag, dhi = (unsigned)(diag >> 32);
       const unsigned long long r0 = removed[c];
       // (the builtins return int: widen through unsigned, or the low word sign-extends)
@@ -165,7 +193,7 @@ IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n,
       const long base = cnt_s;
       if ((kept >> lane) & 1ull) {
         const int rk = __popcll(lane ? (kept & ((1ull << lane) - 1ull)) : 0ull);
-        keep[base + rk] = order[row];
+        keep[base + rk] = ord;
         kbit[rk] = lane;
       }
       if (lane == 0) {
@@ -174,6 +202,11 @@ IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n,
       }
     }
     __syncthreads();
+    if (threadIdx.x < 64 && c + 1 < nw) {
+      const long row = (long)(c + 1) * 64 + lane;
+      diag_n = row < n ? mask[row * nw + c + 1] : 0ull;
+      ord_n = row < n ? order[row] : 0;
+    }
     const int K = __popcll(kept_s);
     if (K) {
       const int wl = threadIdx.x & 31, bg = threadIdx.x >> 5;
@@ -234,35 +267,16 @@ __global__ void nms_sorted_boxes_b_kernel(const float* __restrict__ b, const int
   d[4] = (x2 - x1) * (y2 - y1);
 }
 
-__global__ void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
-                                  const long* __restrict__ mask_off, double thr,
-                                  unsigned long long* __restrict__ mask_all) {
+// grid (ceil(nwmax / NMS_CB), nwmax, samples)
+__global__ __launch_bounds__(64) void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
+                                                        const long* __restrict__ mask_off, double thr,
+                                                        unsigned long long* __restrict__ mask_all) {
   const int sm = blockIdx.z;
   const long o = seg[sm], n = seg[sm + 1] - o;
   const int nw = (int)((n + 63) / 64);
-  const int cb = blockIdx.x, rb = blockIdx.y;
-  if (cb >= nw || rb >= nw || cb < rb) return;
-  const float* sb = sb_all + o * 5;
-  unsigned long long* mask = mask_all + mask_off[sm];
-  __shared__ float cbx[64][5];
-  const int t = threadIdx.x;
-  const long cj = (long)cb * 64 + t;
-  if (cj < n)
-    for (int k = 0; k < 5; ++k) cbx[t][k] = sb[cj * 5 + k];
-  __syncthreads();
-  const long i = (long)rb * 64 + t;
-  if (i >= n) return;
-  const float ix1 = sb[i * 5 + 0], iy1 = sb[i * 5 + 1], ix2 = sb[i * 5 + 2], iy2 = sb[i * 5 + 3],
-              ia = sb[i * 5 + 4];
-  unsigned long long bits = 0;
-  const bool thr_nonneg = thr >= 0.0;
-  const int lim = (int)min((long)64, n - (long)cb * 64);
-  for (int k = 0; k < lim; ++k) {
-    const long j = (long)cb * 64 + k;
-    if (j <= i) continue;
-    if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cbx[k], thr, thr_nonneg)) bits |= 1ull << k;
-  }
-  mask[i * nw + cb] = bits;
+  const int cb0 = blockIdx.x * NMS_CB, rb = blockIdx.y;
+  if (cb0 >= nw || rb >= nw || cb0 + NMS_CB <= rb) return;
+  nms_mask_body(sb_all + o * 5, n, nw, thr, mask_all + mask_off[sm], rb, cb0);
 }
 
 __global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long long* __restrict__ mask_all,
@@ -339,7 +353,7 @@ extern "C" int ivit_nms(const float* boxes_xywha, const float* scores, long n, d
   unsigned long long* mask = (unsigned long long*)w;
   hipLaunchKernelGGL(nms_rank_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, scores, n, order);
   hipLaunchKernelGGL(nms_sorted_boxes_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, boxes_xywha, order, n, sb);
-  hipLaunchKernelGGL(nms_mask_kernel, dim3(nw, nw), dim3(64), 0, st, sb, n, nw, iou_thr, mask);
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(ivit_cdiv(nw, NMS_CB), nw), dim3(64), 0, st, sb, n, nw, iou_thr, mask);
   hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(256), 0, st, mask, n, nw, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;
@@ -410,8 +424,8 @@ extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, c
     return (int)e;
   }
   hipLaunchKernelGGL(nms_sorted_boxes_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, boxes_xywha, order, seg, sb);
-  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(nwmax, nwmax, n_samples), dim3(64), 0, st, sb, seg, mask_off, iou_thr,
-                     mask);
+  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(ivit_cdiv(nwmax, NMS_CB), nwmax, n_samples), dim3(64), 0, st, sb, seg,
+                     mask_off, iou_thr, mask);
   hipLaunchKernelGGL(nms_scan_b_kernel, dim3(n_samples), dim3(256), 0, st, mask, seg, mask_off, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;

@@ -461,18 +461,12 @@ IVIT_DEV void wide_epilogue_tr(const f32x4 (&acc)[RP_MB][NBW], int nw, int m0, i
 // (16 B, 32 contiguous bytes per row per instruction): no LDS round trip, no barriers. The
 // round-2 form (EV = 0: through an f32 LDS tile, 8-B stores, two barriers per 16-row block)
 // measured 4.2 us of a 12.5-us workgroup on the qkv projection (tools/panel_stamps.py).
-// PS > 0 (W = 4): persistent — gridDim.x workgroups (two per CU) walk the nitems (panel, chunk)
-// items with stride gridDim.x (the XCD of an item is kept: the stride is a multiple of 8), and the
-// second half of the grid starts PS x 4096 cycles late, so the two workgroups of a CU run out of
-// phase: one's epilogue (VALU + stores) beside the other's main loop (MFMA + LDS), which the
-// lock-stepped one-item-per-workgroup grid never overlapped.
-template <int EPI, int W, bool ST = false, int EV = 0, int PS = 0>
+template <int EPI, int W, bool ST = false, int EV = 0>
 __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16* __restrict__ A, long lda, int M,
                                                                       int K, const u32x4* __restrict__ wpack, int N,
                                                                       const float* __restrict__ bias, int qcols,
                                                                       float qscale, bf16* __restrict__ Y, long ldy,
-                                                                      bf16* __restrict__ P, long ldp, u64* stamps,
-                                                                      int nitems) {
+                                                                      bf16* __restrict__ P, long ldp, u64* stamps) {
   Stamps stp;
   if constexpr (ST) stp.begin();
   constexpr int CW = 48 * W, TLD = CW + 4, LPR = CW / 12;  // chunk width, T row stride, lanes per row
@@ -480,22 +474,13 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nch = N / CW;
-  if constexpr (PS > 0) {
-    if (blockIdx.x >= gridDim.x / 2) {
-#pragma unroll 1
-      for (int i = 0; i < PS; ++i) __builtin_amdgcn_s_sleep(64);
-    }
-  }
-  const int item_step = PS > 0 ? (int)gridDim.x : nitems;
-#pragma unroll 1
-  for (int item = blockIdx.x; item < nitems; item += item_step) {
   int rp, nc_begin, nc_end;
   if constexpr (W == 8) {
-    rp = xcd_remap(item, nitems);
+    rp = xcd_remap(blockIdx.x, gridDim.x);
     nc_begin = 0;
     nc_end = nch;
   } else {  // (panel, chunk) with the chunks of a panel adjacent: one XCD, the A panel in one L2
-    const int id = xcd_remap(item, nitems);
+    const int id = xcd_remap(blockIdx.x, gridDim.x);
     rp = id / nch;
     nc_begin = id - rp * nch;
     nc_end = nc_begin + 1;
@@ -504,7 +489,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
   const PanelA pa = panel_a_setup<W>(A, lda, M, m0, wv, lane);
   const int r = tid / LPR, c0 = (tid % LPR) * 12;  // row phase: LPR lanes per row, 12 columns each
   float* T = (float*)smem;                          // [16][TLD] after the main loop
-  if (PS > 0 && item != (int)blockIdx.x) __builtin_amdgcn_s_barrier();  // the last item's epilogue read T
 #pragma unroll 1
   for (int nc = nc_begin; nc < nc_end; ++nc) {
     f32x4 acc[RP_MB][NBW];
@@ -601,7 +585,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void rowpanel_wide_kernel(const bf16
       __builtin_amdgcn_s_barrier();  // T is rewritten by the next block (or the next chunk's ring)
     }
   }
-  }
   if constexpr (ST) stp.end(stamps);
 }
 
@@ -629,22 +612,9 @@ void launch_wide(dim3 g, hipStream_t st, bool ev1, u64* sb, const bf16* A, long 
   const int mode = env ? atoi(env) : 0;
   const bool off = mode == 0;
   ev1 = ev1 && !off && (EPI == EPI_QS || EPI == EPI_GELUD || mode == 2);
-  const int nitems = (int)g.x;
-  // IVIT_WIDE_PERSIST=k (A/B): the persistent, half-grid-staggered form (LDS-tile epilogue), k x 4096
-  // cycles of stagger, 512 workgroups
-  const char* pe = getenv("IVIT_WIDE_PERSIST");
-  const int ps = pe ? atoi(pe) : 0;
-  if (ps > 0 && !ev1 && !sb) {
-    const dim3 gp(nitems < 512 ? nitems : 512);
-    auto kp = ps <= 1 ? rowpanel_wide_kernel<EPI, 4, false, 0, 1>
-                      : ps == 2 ? rowpanel_wide_kernel<EPI, 4, false, 0, 2>
-                                : ps == 3 ? rowpanel_wide_kernel<EPI, 4, false, 0, 3> : rowpanel_wide_kernel<EPI, 4, false, 0, 5>;
-    hipLaunchKernelGGL(kp, gp, dim3(256), 0, st, A, lda, M, K, wp, N, bias, qcols, qscale, Y, ldy, P, ldp, sb, nitems);
-    return;
-  }
   auto k = ev1 ? (sb ? rowpanel_wide_kernel<EPI, 4, true, 1> : rowpanel_wide_kernel<EPI, 4, false, 1>)
                : (sb ? rowpanel_wide_kernel<EPI, 4, true, 0> : rowpanel_wide_kernel<EPI, 4, false, 0>);
-  hipLaunchKernelGGL(k, g, dim3(256), 0, st, A, lda, M, K, wp, N, bias, qcols, qscale, Y, ldy, P, ldp, sb, nitems);
+  hipLaunchKernelGGL(k, g, dim3(256), 0, st, A, lda, M, K, wp, N, bias, qcols, qscale, Y, ldy, P, ldp, sb);
 }
 bool al16_rows(const void* p, long ld) { return p == nullptr || (((uintptr_t)p & 15) == 0 && ld % 8 == 0); }
 }  // namespace
