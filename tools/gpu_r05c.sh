@@ -4,6 +4,8 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${1:-r05_c}
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_entry.py -x -q -k "attention or nms or postprocess or panel" -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/${T}_tests.txt 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/${T}_tests.txt; [ $rc -eq 0 ] || exit $rc
+ATTN_VARIANTS="IVIT_ATTN_DQ16=0;IVIT_ATTN_DQ16=1" TORCH_SDPA=0 timeout -k 10 300 python tools/attn_bench.py > gpurun_out/${T}_attn_bench.txt 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/${T}_attn_bench.txt; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do
   for v in 1 0; do
     IVIT_ATTN_DKV16=$v timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_ab_dkv16_${v}_$rep.json 2>/dev/null

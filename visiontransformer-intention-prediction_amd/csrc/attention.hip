@@ -1294,6 +1294,292 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v3_kernel(const bf1
   }
 }
 
+// ------------------------------------------------------------------------- dQ v4 (16x16x32)
+// The dQ kernel in the 16x16x32 form of attn_bwd_dkv_v4_kernel: per wave 32 queries = 2 query
+// blocks i of 16 (Q_i, dO_i as the B operands, in registers), per 32-key unit 2 key blocks j:
+//   S^T_ji = K_j Q_i^T, dP^T_ji = V_j dO_i^T  (C layout: lane (g, c) holds keys 4g..4g+3 of block
+//   j, query 16i + c; initial accumulators -lse2 / -delta of the lane's query)     16 MFMA per unit
+//   dQ_ie += dS_i K_.e  (A operand (dS^T_0i, dS^T_1i) as they stand, B operand two transposing
+//   reads of the K image: keys 4g.. and 16 + 4g.., columns 16e..)                    8 MFMA per unit
+// The ragged last key tile (keys past N masked) runs through dq16_tile_masked afterwards.
+IVIT_DEV void dq16_tile_masked(const char* kimg, const char* vimg, const bf16x8 (&qf)[2][2], const bf16x8 (&gf)[2][2],
+                               const f32x4 (&nl)[2], const f32x4 (&nd)[2], f32x4 (&dq)[2][4], int kbase, int N,
+                               int lane) {
+  const int g = lane >> 4, c16 = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    f32x4 s[2][2], dp[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        s[j][i] = nl[i];
+        dp[j][i] = nd[i];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 ka = *(const bf16x8*)(kimg + t16_off(32 * t + 16 * j + c16, 4 * ks + g));
+          const bf16x8 va = *(const bf16x8*)(vimg + t16_off(32 * t + 16 * j + c16, 4 * ks + g));
+          s[j][i] = mfma16(ka, qf[i][ks], s[j][i]);
+          dp[j][i] = mfma16(va, gf[i][ks], dp[j][i]);
+        }
+      }
+    unsigned w[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          float d0 = fast_exp2(s[j][i][2 * hh]) * dp[j][i][2 * hh];
+          float d1 = fast_exp2(s[j][i][2 * hh + 1]) * dp[j][i][2 * hh + 1];
+          const int key = kbase + 32 * t + 16 * j + 4 * g + 2 * hh;
+          if (key >= N) d0 = 0.f;
+          if (key + 1 >= N) d1 = 0.f;
+          w[i][2 * j + hh] = pk_bf16(d0, d1);
+        }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int off = t16_off(32 * t + 4 * g + q, 2 * e + (p >> 1)) + 8 * (p & 1);
+      union { s16x4 s[2]; bf16x8 v; } u;
+      u.s[0] = ds_tr(kimg + off);
+      u.s[1] = ds_tr(kimg + off + 2048);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        dq[i][e] = mfma16(__builtin_bit_cast(bf16x8, make_uint4(w[i][0], w[i][1], w[i][2], w[i][3])), u.v, dq[i][e]);
+    }
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf16* __restrict__ qkv,
+                                                                const bf16* __restrict__ dout,
+                                                                float* __restrict__ nlse2p,
+                                                                float* __restrict__ ndeltap, int N, int Npad, int H,
+                                                                bf16* __restrict__ dqkv, float scale,
+                                                                const bf16* __restrict__ out,
+                                                                const float* __restrict__ lse) {
+  __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  constexpr int PW = 8 / W;
+  const int qw = bid.x * (32 * W) + wv * 32;
+  // B operands: lane (g, c) holds Q / dO of query qw + 16i + c, dims 32s + 8g .. +7
+  bf16x8 qf[2][2], gf[2][2];
+  f32x4 nl[2], nd[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = qw + 16 * i + c16;
+    const bool qv = q < N;
+    bf16x8 of[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Pack8 pq, pg, po;
+      const long orow = ((long)b * N + q) * D + h * 64 + 32 * s + 8 * g;
+      pq.u = qv ? *(const uint4*)(Qb + (long)q * ld + 32 * s + 8 * g) : make_uint4(0, 0, 0, 0);
+      pg.u = qv ? *(const uint4*)(dout + orow) : make_uint4(0, 0, 0, 0);
+      po.u = qv ? *(const uint4*)(out + orow) : make_uint4(0, 0, 0, 0);
+      qf[i][s] = pq.v;
+      gf[i][s] = pg.v;
+      of[s] = po.v;
+    }
+    float d = 0.f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf((float)of[s][e], (float)gf[i][s][e], d);
+    d += __shfl_xor(d, 16, 64);  // the query's 64 dims sit in lanes c, c + 16, c + 32, c + 48
+    d += __shfl_xor(d, 32, 64);
+    const float lse2 = qv ? lse[(long)z * N + q] * LOG2E : 1e30f;
+    const float dlt = qv ? d : 0.f;
+    if (g == 0 && q < Npad) {
+      nlse2p[(long)z * Npad + q] = -lse2;
+      ndeltap[(long)z * Npad + q] = -dlt;
+    }
+    nl[i] = f32x4{-lse2, -lse2, -lse2, -lse2};
+    nd[i] = f32x4{-dlt, -dlt, -dlt, -dlt};
+  }
+  f32x4 dq[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dq[i][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  unsigned off[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) off[i] = 2u * dma_off16<W>(i, wv, lane, ld);
+  auto issue = [&](int kt, int S) {  // keys past N (ragged tile) are clamped to row N-1 and masked
+    char* kimg = smem[S][0];
+    char* vimg = smem[S][1];
+    const char* kb = uniform_ptr(Kb + (long)kt * AK * ld);
+    const char* vb = uniform_ptr(Vb + (long)kt * AK * ld);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int piece = wv * PW + i;
+      unsigned o = off[i];
+      if (kt >= nfull) {
+        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ (row & 6);
+        o = 2u * (unsigned)((min(kt * AK + row, N - 1) - kt * AK) * ld + c * 8);
+      }
+      glds_s<false>(o, kb, kimg + piece * 1024);
+      glds_s<false>(o, vb, vimg + piece * 1024);
+    }
+  };
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  {
+    uint4* z2 = (uint4*)&smem[2][0][0];
+    for (int i = tid; i < 2 * 8192 / 16; i += 64 * W) z2[i] = make_uint4(0, 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  if (nfull > 0) {
+    unsigned ro[2], tro[4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) ro[s] = (unsigned)t16_off(c16, 4 * s + g);
+    {
+      const int q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) tro[e] = (unsigned)(t16_off(4 * g + q, 2 * e + (p >> 1)) + 8 * (p & 1));
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) asm volatile("" : "+v"(ro[s]));
+#pragma unroll
+    for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(tro[e]));
+    bf16x8 ka[2][2], va[2][2];  // A(u) fragments [j][ks]
+    f32x4 sc[2][2], dc[2][2];   // A(u) results [j][i]
+    unsigned pdq[2][4];         // packed dS of the pending B, [i][word]
+    bf16x8 tk[4];               // transposed K fragments of the pending B, [e]
+    auto read_a = [&](const char* kimg, const char* vimg, int t, int j, int ks) {
+      ka[j][ks] = *(const bf16x8*)(kimg + ro[ks] + 4096 * t + 2048 * j);
+      va[j][ks] = *(const bf16x8*)(vimg + ro[ks] + 4096 * t + 2048 * j);
+    };
+    // E pair k (i = k >> 2, j = (k >> 1) & 1, half hh = k & 1): word 2j + hh of pdq[i]
+    auto e_pair = [&](int k) {
+      const int i = k >> 2, j = (k >> 1) & 1, hh = k & 1;
+      const float d0 = fast_exp2(sc[j][i][2 * hh]) * dc[j][i][2 * hh];
+      const float d1 = fast_exp2(sc[j][i][2 * hh + 1]) * dc[j][i][2 * hh + 1];
+      pdq[i][2 * j + hh] = pk_bf16(d0, d1);
+    };
+    auto read_b = [&](const char* kimg, int t, int e) {
+      union { s16x4 s[2]; bf16x8 v; } u;
+      u.s[0] = ds_tr(kimg + tro[e] + 4096 * t);
+      u.s[1] = ds_tr(kimg + tro[e] + 4096 * t + 2048);
+      tk[e] = u.v;
+    };
+    auto word8 = [&](const unsigned (&w)[4]) { return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3])); };
+    auto body = [&](auto sa, auto ta, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
+      constexpr int SA = decltype(sa)::value, TA = decltype(ta)::value, SB = decltype(sb)::value;
+      constexpr int TB = decltype(tb)::value, SN = decltype(sn_)::value, TN = decltype(tn)::value;
+      constexpr bool BAR = decltype(bar)::value;
+      f32x4 s[2][2], dp[2][2];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        const int ks = m >> 3, j = (m >> 2) & 1, i = (m >> 1) & 1;
+        if ((m & 1) == 0) s[j][i] = mfma16(ka[j][ks], qf[i][ks], ks == 0 ? nl[i] : s[j][i]);
+        else dp[j][i] = mfma16(va[j][ks], gf[i][ks], ks == 0 ? nd[i] : dp[j][i]);
+        if (m == 0) read_a(smem[SA][0], smem[SA][1], TA, 0, 1);
+        if (m == 2) read_a(smem[SA][0], smem[SA][1], TA, 1, 1);
+        if ((m & 1) == 0) e_pair(m >> 1);
+        if (m == 8) read_b(smem[SB][0], TB, 0);
+        if (m == 10) read_b(smem[SB][0], TB, 1);
+        if (m == 12) read_b(smem[SB][0], TB, 2);
+        if (m == 14) read_b(smem[SB][0], TB, 3);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (BAR) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (jn < nt) issue(jn, jn % BNS);
+      }
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int e = m >> 1, i = m & 1;
+        dq[i][e] = mfma16(word8(pdq[i]), tk[e], dq[i][e]);
+        if (more) {
+          if (m == 1) read_a(smem[SN][0], smem[SN][1], TN, 0, 0);
+          if (m == 3) read_a(smem[SN][0], smem[SN][1], TN, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          sc[j][i] = s[j][i];
+          dc[j][i] = dp[j][i];
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using F = std::false_type;
+    using T = std::true_type;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) read_a(smem[0][0], smem[0][1], 0, j, 0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        sc[j][i] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};
+        dc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    auto tile = [&](auto st, int j) {
+      constexpr int S = decltype(st)::value;
+      using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
+      using SNX = std::integral_constant<int, (S + 1) % BNS>;
+      using SC = std::integral_constant<int, S>;
+      body(SC{}, I0{}, SP{}, I1{}, SC{}, I1{}, F{}, 0, true);
+      body(SC{}, I1{}, SC{}, I0{}, SNX{}, I0{}, T{}, j + 2, j + 1 < nfull);
+    };
+    int j = 0;
+    for (; j + 3 <= nfull; j += 3) {
+      tile(I0{}, j);
+      tile(I1{}, j + 1);
+      tile(I2{}, j + 2);
+    }
+    if (j < nfull) tile(I0{}, j);
+    if (j + 1 < nfull) tile(I1{}, j + 1);
+    {  // drain: E and B of the last unit (tile nfull-1, keys 32..63)
+      const int S = (nfull - 1) % BNS;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e_pair(k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) read_b(smem[S][0], 1, e);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dq[i][e] = mfma16(word8(pdq[i]), tk[e], dq[i][e]);
+    }
+  }
+  if (nt > nfull) {  // ragged last key tile (DMA issued one tile ahead, or in the prologue)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int S = nfull % BNS;
+    dq16_tile_masked(smem[S][0], smem[S][1], qf, gf, nl, nd, dq, nfull * AK, N, lane);
+  }
+  // lane holds rows q = qw + 16i + 4g + r, column d = 16e + c16
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qq = qw + 16 * i + 4 * g + r;
+      if (qq < N) {
+        bf16* row = dqkv + ((long)b * N + qq) * ld + h * 64;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) row[16 * e + c16] = (bf16)(dq[i][e][r] * scale);
+      }
+    }
+}
+
 // ------------------------------------------------------------------------- f32 row kernels
 // S rows (already scaled) -> P = softmax, zero padding columns; lse = max + log(sum).
 __global__ void softmax_rows_kernel(float* __restrict__ S, long ldS, int N, float* __restrict__ lse) {
@@ -1569,8 +1855,13 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   // independent workgroup to fill its gaps)
   constexpr int BW = 4;
   const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
-  kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
+  const char* dq16e = getenv("IVIT_ATTN_DQ16");  // A/B switch: dQ in the 16x16x32 form (read per launch)
+  if (dq16e && atoi(dq16e) == 1)
+    kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
+  else
+    kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
   // dK/dV: the 16x16x32 form (v4) by default — isolated 0.441-0.445 -> 0.406 ms, same call
   // (profiles/r05_b_attn_dkv16_ab.txt); IVIT_ATTN_DKV16=0 restores v3 (A/B, read per launch)
   const char* dv16 = getenv("IVIT_ATTN_DKV16");
