@@ -4,13 +4,13 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 T=${1:-r05_c}
 timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_entry.py -x -q -k "attention or nms or postprocess or panel" -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/${T}_tests.txt 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/${T}_tests.txt; [ $rc -eq 0 ] || exit $rc
-ATTN_VARIANTS="IVIT_ATTN_DQ16=0;IVIT_ATTN_DQ16=1" TORCH_SDPA=0 timeout -k 10 300 python tools/attn_bench.py > gpurun_out/${T}_attn_bench.txt 2>&1
+ATTN_VARIANTS="IVIT_ATTN_FWD16=0;IVIT_ATTN_FWD16=1" TORCH_SDPA=0 timeout -k 10 300 python tools/attn_bench.py > gpurun_out/${T}_attn_bench.txt 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/${T}_attn_bench.txt; [ $rc -eq 0 ] || exit $rc
 for rep in 1 2; do
   for v in 1 0; do
-    IVIT_ATTN_DKV16=$v timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_ab_dkv16_${v}_$rep.json 2>/dev/null
+    IVIT_ATTN_FWD16=$v timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${T}_ab_fwd16_${v}_$rep.json 2>/dev/null
     rc=$?; [ $rc -eq 0 ] || exit $rc
-    python -c "import json; d=json.load(open('gpurun_out/${T}_ab_dkv16_${v}_$rep.json')); r=d['roofline']; print('DKV16=$v', d['ms_per_step'], d['value'], r['frac'], r.get('isolated',{}).get('frac'), r['per_step_ms'])"
+    python -c "import json; d=json.load(open('gpurun_out/${T}_ab_fwd16_${v}_$rep.json')); r=d['roofline']; print('FWD16=$v', d['ms_per_step'], d['value'], r['frac'], r.get('isolated',{}).get('frac'), r['per_step_ms'])"
   done
 done
 timeout -k 10 300 python bench.py --mode eval --steps 10 --warmup 2 > gpurun_out/${T}_bench_eval.json 2>gpurun_out/${T}_eval.err

@@ -319,6 +319,255 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
   if (q < N && hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
 }
 
+// ------------------------------------------------------------------------- forward v7 (16x16x32)
+// v6's algorithm (prescaled Q, -m as the S chains' initial accumulator, lazy rescale, one barrier
+// per key tile, K two tiles ahead and V one by LDS-DMA) with every product as
+// v_mfma_f32_16x16x32_bf16. Per wave 32 queries = 2 query blocks i; per 64-key tile 4 key blocks kb:
+//   S'^T_{kb,i} = K_kb Q_i^T - m_i        (C layout: lane (g, c) holds keys 16kb + 4g + r of query
+//                                          16i + c)                                  16 MFMA
+//   O^T_{e,i} += V^T_{e,.} P^T_{.,i}     (B operand of k step s = (P_{2s,i}, P_{2s+1,i}) packed as
+//                                          they stand; A operand two transposing reads of V)   16 MFMA
+//   l_i += 1^T P^T_{.,i}                                                                          4 MFMA
+// A query's row max spans the four lanes c, c + 16, c + 32, c + 48 (quad_max: two permlane swaps).
+template <int W, bool PRE>
+__global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v7_kernel(const bf16* __restrict__ qkv, int N, int H,
+                                                                        bf16* __restrict__ out,
+                                                                        float* __restrict__ lse, float c2) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int2 bid = attn_block_id();
+  const int z = bid.y, b = z / H, h = z - b * H;
+  const int D = H * 64;
+  const long ld = 3L * D;
+  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
+  const bf16* Kb = Qb + D;
+  const bf16* Vb = Qb + 2 * D;
+  const int qw = bid.x * (32 * W) + wv * 32;
+  bf16x8 qf[2][2];  // B operand: Q[qw + 16i + c][dims 32s + 8g .. +7]
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = qw + 16 * i + c16;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      Pack8 pq;
+      pq.u = q < N ? *(const uint4*)(Qb + (long)q * ld + 32 * s + 8 * g) : make_uint4(0, 0, 0, 0);
+      qf[i][s] = pq.v;
+      if constexpr (PRE) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) qf[i][s][e] = (bf16)((float)qf[i][s][e] * c2);
+      }
+    }
+  }
+  const int nt = (N + AK - 1) / AK, nfull = N / AK;
+  unsigned off[8 / W];
+#pragma unroll
+  for (int i = 0; i < 8 / W; ++i) off[i] = 2u * dma_off16<W>(i, wv, lane, ld);
+  auto issue1 = [&](const bf16* base, int kt, char* img) {
+    const char* sb = uniform_ptr(base + (long)kt * AK * ld);
+#pragma unroll
+    for (int i = 0; i < 8 / W; ++i) {
+      const int piece = wv * (8 / W) + i;
+      unsigned o = off[i];
+      if (kt >= nfull) {  // keys past N: row N-1 (finite V; their scores are masked)
+        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ (row & 6);
+        o = 2u * (unsigned)((min(kt * AK + row, N - 1) - kt * AK) * ld + c * 8);
+      }
+      glds_s<false>(o, sb, img + piece * 1024);
+    }
+  };
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
+  // per-lane LDS offsets: K row reads (+ 2048 kb), V transposed reads (+ 4096 s, + 2048 second half)
+  unsigned kro[2], vtr[4];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) kro[s] = (unsigned)t16_off(c16, 4 * s + g);
+  {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) vtr[e] = (unsigned)(t16_off(4 * g + q, 2 * e + (p >> 1)) + 8 * (p & 1));
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s) asm volatile("" : "+v"(kro[s]));
+#pragma unroll
+  for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(vtr[e]));
+  auto kfrag = [&](const char* kimg, int kb, int s) { return *(const bf16x8*)(kimg + kro[s] + 2048 * kb); };
+  auto vfrag = [&](const char* vimg, int e, int s) {
+    union { s16x4 s[2]; bf16x8 v; } u;
+    u.s[0] = ds_tr(vimg + vtr[e] + 4096 * s);
+    u.s[1] = ds_tr(vimg + vtr[e] + 4096 * s + 2048);
+    return u.v;
+  };
+  auto mask_tile = [&](f32x4 (&t)[4][2], int kbase) {  // keys >= N -> NEG_BIG (ragged tile only)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool dead = kbase + 16 * kb + 4 * g + r >= N;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) t[kb][i][r] = dead ? NEG_BIG : t[kb][i][r];
+      }
+  };
+  auto tile_max = [&](const f32x4 (&t)[4][2], int i) {
+    float a = NEG_BIG, bm = NEG_BIG;
+#pragma unroll
+    for (int kb = 0; kb < 4; kb += 2) {
+      a = vmax3(a, t[kb][i][0], t[kb][i][1]);
+      a = vmax3(a, t[kb][i][2], t[kb][i][3]);
+      bm = vmax3(bm, t[kb + 1][i][0], t[kb + 1][i][1]);
+      bm = vmax3(bm, t[kb + 1][i][2], t[kb + 1][i][3]);
+    }
+    return quad_max(fmaxf(a, bm));
+  };
+
+  // prologue: S'_0 (from a zero accumulator), m = its row max, then S'_0 - m; K_1 in flight
+  issue1(Kb, 0, smem[0][0]);
+  issue1(Vb, 0, smem[0][1]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (nt > 1) issue1(Kb, 1, smem[1][0]);
+  f32x4 sc[4][2], sn[4][2];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      sc[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) sc[kb][i] = mfma16(kfrag(smem[0][0], kb, s), qf[i][s], sc[kb][i]);
+    }
+  if (nfull == 0) mask_tile(sc, 0);
+  float m[2];
+  f32x4 negm[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    m[i] = tile_max(sc, i);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sc[kb][i][r] -= m[i];
+    negm[i] = f32x4{-m[i], -m[i], -m[i], -m[i]};
+  }
+  f32x4 o[4][2], lacc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    lacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  // one tile step: S'_{j+1} = K_{j+1} Q^T - m (16 MFMA) beside P_j = exp2(S'_j) (VALU), then
+  // O^T += V_j^T P_j^T, l += 1^T P_j^T (20 MFMA) beside the row max of S'_{j+1}
+  auto step = [&](const char* kimg, const char* vimg, f32x4 (&cur)[4][2], f32x4 (&nxt)[4][2], int kbase,
+                  float (&mt)[2]) {
+    unsigned pw[2][2][4];  // [i][s][word]: B operand of PV k step s for query block i
+    auto ex = [&](int k) {  // k = 0..15: (i, s, word): two exps, one packed word
+      const int i = k >> 3, s = (k >> 2) & 1, w = k & 3;
+      const int kb = 2 * s + (w >> 1), r = 2 * (w & 1);
+      pw[i][s][w] = pk_bf16(fast_exp2(cur[kb][i][r]), fast_exp2(cur[kb][i][r + 1]));
+    };
+    bf16x8 kf[3];
+    kf[0] = kfrag(kimg, 0, 0);
+    kf[1] = kfrag(kimg, 1, 0);
+#pragma unroll
+    for (int mi = 0; mi < 16; ++mi) {
+      const int s = mi >> 3, kb = (mi >> 1) & 3, i = mi & 1;
+      const int f = mi >> 1;  // fragment (s, kb) index, used by i = 0 and 1
+      if (i == 0 && f + 2 < 8) kf[(f + 2) % 3] = kfrag(kimg, ((f + 2) & 3), (f + 2) >> 2);
+      nxt[kb][i] = mfma16(kf[f % 3], qf[i][s], s == 0 ? negm[i] : nxt[kb][i]);
+      ex(mi);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    bf16x8 vf[3];
+    vf[0] = vfrag(vimg, 0, 0);
+    vf[1] = vfrag(vimg, 1, 0);
+    if (kbase + AK > N) mask_tile(nxt, kbase);
+    float a[2] = {NEG_BIG, NEG_BIG};
+#pragma unroll
+    for (int mi = 0; mi < 20; ++mi) {
+      // 8 V fragments (s, e), each feeding two MFMAs (i = 0, 1); the l MFMAs after each k step
+      if (mi < 16) {
+        const int s = mi >> 3, e = (mi >> 1) & 3, i = mi & 1, f = mi >> 1;
+        if (i == 0 && f + 2 < 8) vf[(f + 2) % 3] = vfrag(vimg, (f + 2) & 3, (f + 2) >> 2);
+        o[e][i] = mfma16(vf[f % 3], __builtin_bit_cast(bf16x8, make_uint4(pw[i][s][0], pw[i][s][1], pw[i][s][2],
+                                                                            pw[i][s][3])),
+                         o[e][i]);
+      } else {
+        const int s = (mi - 16) >> 1, i = (mi - 16) & 1;
+        lacc[i] = mfma16(ones, __builtin_bit_cast(bf16x8, make_uint4(pw[i][s][0], pw[i][s][1], pw[i][s][2],
+                                                                       pw[i][s][3])),
+                         lacc[i]);
+      }
+      if (mi >= 4 && mi < 12) {  // row max of S'_{j+1}: block kb = mi - 4 (two per i)
+        const int kb = (mi - 4) >> 1, i = (mi - 4) & 1;
+        a[i] = vmax3(a[i], nxt[kb][i][0], nxt[kb][i][1]);
+        a[i] = vmax3(a[i], nxt[kb][i][2], nxt[kb][i][3]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    mt[0] = quad_max(a[0]);
+    mt[1] = quad_max(a[1]);
+  };
+  // after S'_{j+1} - m and its row max mt: move m lazily; the next tile is shifted with it
+  auto rescale = [&](const float (&mt)[2], f32x4(&nxt)[4][2]) {
+    const bool moved0 = mt[0] > TAU, moved1 = mt[1] > TAU;
+    if (__any(moved0 || moved1)) {
+      const float d[2] = {moved0 ? mt[0] : 0.f, moved1 ? mt[1] : 0.f};
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float alpha = fast_exp2(-d[i]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[e][i][r] *= alpha;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lacc[i][r] *= alpha;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) nxt[kb][i][r] -= d[i];
+        m[i] += d[i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("v_sub_f32 %0, %0, %1" : "+v"(negm[i][r]) : "v"(d[i]));
+      }
+    }
+  };
+  auto body = [&](auto stage, int j, f32x4(&cur)[4][2], f32x4(&nxt)[4][2]) {
+    constexpr int S = decltype(stage)::value;  // V_j in smem[S][1], K_{j+1} in smem[S^1][0]
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (j + 2 < nt) issue1(Kb, j + 2, smem[S][0]);
+    if (j + 1 < nt) issue1(Vb, j + 1, smem[S ^ 1][1]);
+    float mt[2];
+    step(smem[S ^ 1][0], smem[S][1], cur, nxt, (j + 1) * AK, mt);
+    rescale(mt, nxt);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  int j = 0;
+  for (; j + 1 < nt; j += 2) {
+    body(I0{}, j, sc, sn);
+    body(I1{}, j + 1, sn, sc);
+  }
+  if (j < nt) body(I0{}, j, sc, sn);
+  // epilogue: lane (g, c) holds O[q = qw + 16i + c][d = 16e + 4g + r]: 8-B stores
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = qw + 16 * i + c16;
+    const float l = lacc[i][0];
+    const float inv = 1.f / l;
+    if (q < N) {
+      bf16* orow = out + ((long)b * N + q) * D + h * 64 + 4 * g;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        *(uint2*)(orow + 16 * e) = make_uint2(pk_bf16(o[e][i][0] * inv, o[e][i][1] * inv),
+                                              pk_bf16(o[e][i][2] * inv, o[e][i][3] * inv));
+      if (g == 0) lse[(long)z * N + q] = (m[i] + log2f(l)) * 0.69314718055994531f;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- backward v2 (bf16)
 // Row constants for the backward in a padded layout [z][Npad] (Npad = N rounded up to 64):
 // lse2 = lse * log2(e) (+1e30 on padding rows, so their probabilities are exactly 0) and
@@ -846,20 +1095,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf
 // 16). Q / dO images: chunk c of row r at c ^ (r & 6) — conflict-free for the 16x16x32 row reads
 // (16 rows x one chunk per 16-lane group) and for the transposed reads (8 rows x 2 chunks per
 // half-wave); the 32x32 images' swz128 leaves the latter 2-way.
-IVIT_DEV int t16_off(int r, int c) { return r * 128 + ((c ^ (r & 6)) << 4); }
-
-template <int W>
-IVIT_DEV int dma_off16(int i, int wv, int lane, long ld) {
-  const int piece = wv * (8 / W) + i;
-  const int row = piece * 8 + (lane >> 3);
-  const int c = (lane & 7) ^ (row & 6);
-  return (int)(row * ld) + c * 8;
-}
-
-IVIT_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
 template <int W>
 __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf16* __restrict__ qkv,
                                                                  const bf16* __restrict__ dout,
@@ -1831,8 +2066,13 @@ extern "C" int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh
   (void)work_bytes;
   if (B * N * H == 0) return 0;
   dim3 g(ivit_cdiv(N, 128), B * H);
-  kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream), (const bf16*)qkv,
-            (int)N, (int)H, (bf16*)out, lse, 1.0f);
+  const char* f16 = getenv("IVIT_ATTN_FWD16");  // A/B switch: the 16x16x32 forward (read per launch)
+  if (f16 && atoi(f16) == 1)
+    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v7_kernel<4, false>, g, dim3(256), ivit_stream(stream),
+              (const bf16*)qkv, (int)N, (int)H, (bf16*)out, lse, 1.0f);
+  else
+    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream),
+              (const bf16*)qkv, (int)N, (int)H, (bf16*)out, lse, 1.0f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -1855,8 +2095,10 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   // independent workgroup to fill its gaps)
   constexpr int BW = 4;
   const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
-  const char* dq16e = getenv("IVIT_ATTN_DQ16");  // A/B switch: dQ in the 16x16x32 form (read per launch)
-  if (dq16e && atoi(dq16e) == 1)
+  // dQ: the 16x16x32 form (v4) by default — isolated 0.332-0.334 -> 0.316 ms, same call
+  // (profiles/r05_c_attn_dq16_ab.txt); IVIT_ATTN_DQ16=0 restores v3 (A/B, read per launch)
+  const char* dq16e = getenv("IVIT_ATTN_DQ16");
+  if (!(dq16e && atoi(dq16e) == 0))
     kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
               (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
   else

@@ -136,4 +136,27 @@ IVIT_DEV void retire_loads(bf16x8 (&a)[4], bf16x8 (&b)[4]) {
   for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(a[i]), "v"(b[i]));
 }
 
+// 16x16x32 forms (attention.hip v4 backward, v7 forward): 64-row x 128-B tile images with chunk c of
+// row r at c ^ (r & 6) — conflict-free for the 16x16x32 row reads (16 rows x one chunk per 16-lane
+// group) and the transposed reads of 8 rows x 2 chunks per half-wave.
+IVIT_DEV int t16_off(int r, int c) { return r * 128 + ((c ^ (r & 6)) << 4); }
+
+template <int W>
+IVIT_DEV int dma_off16(int i, int wv, int lane, long ld) {
+  const int piece = wv * (8 / W) + i;
+  const int row = piece * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ (row & 6);
+  return (int)(row * ld) + c * 8;
+}
+
+IVIT_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// max over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (the 16x16 C layout's row groups)
+IVIT_DEV float quad_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return half_swap_max(fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1])));
+}
+
 }  // namespace

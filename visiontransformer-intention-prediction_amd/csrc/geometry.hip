@@ -99,49 +99,62 @@ IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float i
   return (double)ovr > thr;
 }
 
-// One 64-thread workgroup per (row block rb, chunk of NMS_CB column blocks): rows rb*64 + t against
-// the column blocks cb >= rb of its chunk, each staged through LDS as corners (one ds_read_b128)
-// and area (ds_read_b32) — NMS_CB times fewer workgroups than one per (rb, cb), most of which had
-// nothing to do (cb < rb) or one short loop.
-constexpr int NMS_CB = 8;
+// One 256-thread workgroup per (NMS_RW = 4 row blocks, chunk of NMS_CB column blocks): wave w takes
+// rows (rb0 + w) * 64 + t against the column blocks cb >= rb of the chunk. Wave 0 stages each column
+// block in LDS (corners as one float4, the area) double-buffered, and loads the next block's boxes
+// while the current one is compared (one barrier per column block); the earlier one-wave-per-(rb, cb)
+// grid launched ~4 M mostly empty workgroups per eval batch.
+constexpr int NMS_CB = 8, NMS_RW = 4;
 IVIT_DEV void nms_mask_body(const float* __restrict__ sb, long n, int nw, double thr,
-                            unsigned long long* __restrict__ mask, int rb, int cb0) {
-  __shared__ float4 cxy[64];
-  __shared__ float car[64];
-  const int t = threadIdx.x;
+                            unsigned long long* __restrict__ mask, int rb0, int cb0) {
+  __shared__ float4 cxy[2][64];
+  __shared__ float car[2][64];
+  const int t = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int rb = rb0 + w;
   const long i = (long)rb * 64 + t;
+  const bool row_ok = rb < nw && i < n;
   float ix1 = 0.f, iy1 = 0.f, ix2 = 0.f, iy2 = 0.f, ia = 0.f;
-  if (i < n) {
+  if (row_ok) {
     ix1 = sb[i * 5 + 0]; iy1 = sb[i * 5 + 1]; ix2 = sb[i * 5 + 2]; iy2 = sb[i * 5 + 3]; ia = sb[i * 5 + 4];
   }
   const bool thr_nonneg = thr >= 0.0;
-  const int cb1 = min(cb0 + NMS_CB, nw);
-  for (int cb = max(cb0, rb); cb < cb1; ++cb) {
-    __syncthreads();  // the previous block's reads of cxy / car are done
+  const int cbs = max(cb0, rb0), cb1 = min(cb0 + NMS_CB, nw);
+  float4 pxy = make_float4(0.f, 0.f, 0.f, 0.f);
+  float pa = 0.f;
+  auto fetch = [&](int cb) {
     const long cj = (long)cb * 64 + t;
     if (cj < n) {
-      cxy[t] = make_float4(sb[cj * 5 + 0], sb[cj * 5 + 1], sb[cj * 5 + 2], sb[cj * 5 + 3]);
-      car[t] = sb[cj * 5 + 4];
+      pxy = make_float4(sb[cj * 5 + 0], sb[cj * 5 + 1], sb[cj * 5 + 2], sb[cj * 5 + 3]);
+      pa = sb[cj * 5 + 4];
+    }
+  };
+  if (w == 0 && cbs < cb1) fetch(cbs);
+  for (int cb = cbs; cb < cb1; ++cb) {
+    const int buf = (cb - cbs) & 1;
+    if (w == 0) {
+      cxy[buf][t] = pxy;
+      car[buf][t] = pa;
+      if (cb + 1 < cb1) fetch(cb + 1);
     }
     __syncthreads();
-    if (i < n) {
+    if (cb >= rb && row_ok) {
       unsigned long long bits = 0;
       const int lim = (int)min((long)64, n - (long)cb * 64);
       const int k0 = cb == rb ? t + 1 : 0;  // the diagonal block: only boxes after this one
       for (int k = k0; k < lim; ++k)
-        if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cxy[k], car[k], thr, thr_nonneg)) bits |= 1ull << k;
+        if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cxy[buf][k], car[buf][k], thr, thr_nonneg)) bits |= 1ull << k;
       mask[i * nw + cb] = bits;
     }
   }
 }
 
 // mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr.
-// grid (ceil(nw / NMS_CB), nw)
-__global__ __launch_bounds__(64) void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, double thr,
-                                                      unsigned long long* __restrict__ mask) {
-  const int cb0 = blockIdx.x * NMS_CB, rb = blockIdx.y;
-  if (cb0 + NMS_CB <= rb) return;
-  nms_mask_body(sb, n, nw, thr, mask, rb, cb0);
+// grid (ceil(nw / NMS_CB), ceil(nw / NMS_RW)), 256 threads
+__global__ __launch_bounds__(256) void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, double thr,
+                                                       unsigned long long* __restrict__ mask) {
+  const int cb0 = blockIdx.x * NMS_CB, rb0 = blockIdx.y * NMS_RW;
+  if (cb0 + NMS_CB <= rb0) return;
+  nms_mask_body(sb, n, nw, thr, mask, rb0, cb0);
 }
 
 constexpr int NMS_MAXW = 1024;  // n <= 65536
@@ -267,16 +280,16 @@ __global__ void nms_sorted_boxes_b_kernel(const float* __restrict__ b, const int
   d[4] = (x2 - x1) * (y2 - y1);
 }
 
-// grid (ceil(nwmax / NMS_CB), nwmax, samples)
-__global__ __launch_bounds__(64) void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
+// grid (ceil(nwmax / NMS_CB), ceil(nwmax / NMS_RW), samples), 256 threads
+__global__ __launch_bounds__(256) void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
                                                         const long* __restrict__ mask_off, double thr,
                                                         unsigned long long* __restrict__ mask_all) {
   const int sm = blockIdx.z;
   const long o = seg[sm], n = seg[sm + 1] - o;
   const int nw = (int)((n + 63) / 64);
-  const int cb0 = blockIdx.x * NMS_CB, rb = blockIdx.y;
-  if (cb0 >= nw || rb >= nw || cb0 + NMS_CB <= rb) return;
-  nms_mask_body(sb_all + o * 5, n, nw, thr, mask_all + mask_off[sm], rb, cb0);
+  const int cb0 = blockIdx.x * NMS_CB, rb0 = blockIdx.y * NMS_RW;
+  if (cb0 >= nw || rb0 >= nw || cb0 + NMS_CB <= rb0) return;
+  nms_mask_body(sb_all + o * 5, n, nw, thr, mask_all + mask_off[sm], rb0, cb0);
 }
 
 __global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long long* __restrict__ mask_all,
@@ -353,7 +366,8 @@ extern "C" int ivit_nms(const float* boxes_xywha, const float* scores, long n, d
   unsigned long long* mask = (unsigned long long*)w;
   hipLaunchKernelGGL(nms_rank_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, scores, n, order);
   hipLaunchKernelGGL(nms_sorted_boxes_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, boxes_xywha, order, n, sb);
-  hipLaunchKernelGGL(nms_mask_kernel, dim3(ivit_cdiv(nw, NMS_CB), nw), dim3(64), 0, st, sb, n, nw, iou_thr, mask);
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(ivit_cdiv(nw, NMS_CB), ivit_cdiv(nw, NMS_RW)), dim3(256), 0, st, sb, n, nw,
+                     iou_thr, mask);
   hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(256), 0, st, mask, n, nw, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;
@@ -424,8 +438,8 @@ extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, c
     return (int)e;
   }
   hipLaunchKernelGGL(nms_sorted_boxes_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, boxes_xywha, order, seg, sb);
-  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(ivit_cdiv(nwmax, NMS_CB), nwmax, n_samples), dim3(64), 0, st, sb, seg,
-                     mask_off, iou_thr, mask);
+  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(ivit_cdiv(nwmax, NMS_CB), ivit_cdiv(nwmax, NMS_RW), n_samples), dim3(256),
+                     0, st, sb, seg, mask_off, iou_thr, mask);
   hipLaunchKernelGGL(nms_scan_b_kernel, dim3(n_samples), dim3(256), 0, st, mask, seg, mask_off, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;
