@@ -22,6 +22,8 @@ for (k, g), cs in acc.items():
           f"lds-stall {a.get('SQ_WAIT_INST_LDS', 0) / w:5.1%})")
     if busy:
         print(f"   MFMA busy / (SQ busy cycles x 4 SIMD x ...): {a['SQ_VALU_MFMA_BUSY_CYCLES']:.3g} cyc; SQ_BUSY {busy:.3g}")
+    if a.get("SQ_INSTS_MFMA"):
+        print(f"   VALU instructions per MFMA {a.get('SQ_INSTS_VALU', 0) / a['SQ_INSTS_MFMA']:.2f}")
     for c in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"):
         if c in a:
             print(f"   {c:22s} {a[c]:.4g}")

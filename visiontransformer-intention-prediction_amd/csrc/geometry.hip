@@ -4,6 +4,9 @@
 
 #include <rocprim/device/device_segmented_radix_sort.hpp>
 
+#include <cmath>
+#include <cstring>
+
 #pragma clang fp contract(off)
 
 using namespace ivit;
@@ -85,76 +88,77 @@ __global__ void nms_sorted_boxes_kernel(const float* __restrict__ b, const int* 
   sb[p * 5 + 4] = (x2 - x1) * (y2 - y1);
 }
 
-// torchvision's test, bit for bit: (double)(inter / (area_i + area_j - inter)) > thr in f32. Disjoint
-// boxes (inter = 0, most pairs) give 0 / union = +-0 or NaN, never > a threshold >= 0: the f32
-// division (a ~10-instruction VALU sequence) runs only for overlapping pairs or a negative threshold.
-IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float ia, float4 c, float ca, double thr,
-                             bool thr_nonneg) {
+// torchvision's test, bit for bit: (double)RN32(inter / u) > thr with u = (area_i + area_j) - inter in
+// f32. For thr >= 0 and u > 0 it is decided without the division (a ~10-instruction VALU sequence,
+// and with divergent lanes the whole wave waits for it): with t the smallest float whose double
+// exceeds thr and mid the midpoint between t and its predecessor, RN32(x) >= t iff x > mid, or
+// x == mid and t is even (ties to even), and x > mid iff inter > mid * u — exact in double (mid has
+// 25 significant bits, u 24). Other cases (u <= 0, NaN, thr < 0) take the division.
+struct NmsThr {
+  double thr, mid;
+  int fast, t_even;
+};
+NmsThr nms_thr(double thr) {
+  NmsThr r{thr, 0.0, 0, 0};
+  if (!(thr >= 0.0) || !(thr < 1e30)) return r;
+  float t = (float)thr;
+  while ((double)t <= thr) t = nextafterf(t, INFINITY);
+  float tp;
+  while ((double)(tp = nextafterf(t, -INFINITY)) > thr) t = tp;  // smallest float above thr
+  tp = nextafterf(t, -INFINITY);
+  r.mid = 0.5 * ((double)tp + (double)t);
+  unsigned bits;
+  memcpy(&bits, &t, 4);
+  r.t_even = (bits & 1u) == 0;
+  r.fast = 1;
+  return r;
+}
+IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float ia, float4 c, float ca,
+                             const NmsThr& th) {
   const float xx1 = fmaxf(ix1, c.x), yy1 = fmaxf(iy1, c.y);
   const float xx2 = fminf(ix2, c.z), yy2 = fminf(iy2, c.w);
   const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
   const float inter = w * h;
-  if (thr_nonneg && !(inter > 0.f)) return false;
-  const float ovr = inter / ((ia + ca) - inter);
-  return (double)ovr > thr;
+  const float u = (ia + ca) - inter;
+  if (th.fast && u > 0.f) {
+    const double lhs = (double)inter, rhs = th.mid * (double)u;
+    return lhs > rhs || (lhs == rhs && th.t_even);
+  }
+  const float ovr = inter / u;
+  return (double)ovr > th.thr;
 }
 
-// One 256-thread workgroup per (NMS_RW = 4 row blocks, chunk of NMS_CB column blocks): wave w takes
-// rows (rb0 + w) * 64 + t against the column blocks cb >= rb of the chunk. Wave 0 stages each column
-// block in LDS (corners as one float4, the area) double-buffered, and loads the next block's boxes
-// while the current one is compared (one barrier per column block); the earlier one-wave-per-(rb, cb)
-// grid launched ~4 M mostly empty workgroups per eval batch.
-constexpr int NMS_CB = 8, NMS_RW = 4;
-IVIT_DEV void nms_mask_body(const float* __restrict__ sb, long n, int nw, double thr,
-                            unsigned long long* __restrict__ mask, int rb0, int cb0) {
-  __shared__ float4 cxy[2][64];
-  __shared__ float car[2][64];
-  const int t = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int rb = rb0 + w;
+// one 64-thread workgroup per (row block, column block >= it): the column block's boxes staged in LDS
+// as corners (one ds_read_b128) and area
+IVIT_DEV void nms_mask_body(const float* __restrict__ sb, long n, int nw, const NmsThr& th,
+                            unsigned long long* __restrict__ mask, int rb, int cb) {
+  __shared__ float4 cxy[64];
+  __shared__ float car[64];
+  const int t = threadIdx.x;
+  const long cj = (long)cb * 64 + t;
+  if (cj < n) {
+    cxy[t] = make_float4(sb[cj * 5 + 0], sb[cj * 5 + 1], sb[cj * 5 + 2], sb[cj * 5 + 3]);
+    car[t] = sb[cj * 5 + 4];
+  }
+  __syncthreads();
   const long i = (long)rb * 64 + t;
-  const bool row_ok = rb < nw && i < n;
-  float ix1 = 0.f, iy1 = 0.f, ix2 = 0.f, iy2 = 0.f, ia = 0.f;
-  if (row_ok) {
-    ix1 = sb[i * 5 + 0]; iy1 = sb[i * 5 + 1]; ix2 = sb[i * 5 + 2]; iy2 = sb[i * 5 + 3]; ia = sb[i * 5 + 4];
-  }
-  const bool thr_nonneg = thr >= 0.0;
-  const int cbs = max(cb0, rb0), cb1 = min(cb0 + NMS_CB, nw);
-  float4 pxy = make_float4(0.f, 0.f, 0.f, 0.f);
-  float pa = 0.f;
-  auto fetch = [&](int cb) {
-    const long cj = (long)cb * 64 + t;
-    if (cj < n) {
-      pxy = make_float4(sb[cj * 5 + 0], sb[cj * 5 + 1], sb[cj * 5 + 2], sb[cj * 5 + 3]);
-      pa = sb[cj * 5 + 4];
-    }
-  };
-  if (w == 0 && cbs < cb1) fetch(cbs);
-  for (int cb = cbs; cb < cb1; ++cb) {
-    const int buf = (cb - cbs) & 1;
-    if (w == 0) {
-      cxy[buf][t] = pxy;
-      car[buf][t] = pa;
-      if (cb + 1 < cb1) fetch(cb + 1);
-    }
-    __syncthreads();
-    if (cb >= rb && row_ok) {
-      unsigned long long bits = 0;
-      const int lim = (int)min((long)64, n - (long)cb * 64);
-      const int k0 = cb == rb ? t + 1 : 0;  // the diagonal block: only boxes after this one
-      for (int k = k0; k < lim; ++k)
-        if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cxy[buf][k], car[buf][k], thr, thr_nonneg)) bits |= 1ull << k;
-      mask[i * nw + cb] = bits;
-    }
-  }
+  if (i >= n) return;
+  const float ix1 = sb[i * 5 + 0], iy1 = sb[i * 5 + 1], ix2 = sb[i * 5 + 2], iy2 = sb[i * 5 + 3],
+              ia = sb[i * 5 + 4];
+  unsigned long long bits = 0;
+  const int lim = (int)min((long)64, n - (long)cb * 64);
+  const int k0 = cb == rb ? t + 1 : 0;  // the diagonal block: only boxes after this one
+  for (int k = k0; k < lim; ++k)
+    if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cxy[k], car[k], th)) bits |= 1ull << k;
+  mask[i * nw + cb] = bits;
 }
 
-// mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr.
-// grid (ceil(nw / NMS_CB), ceil(nw / NMS_RW)), 256 threads
-__global__ __launch_bounds__(256) void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, double thr,
-                                                       unsigned long long* __restrict__ mask) {
-  const int cb0 = blockIdx.x * NMS_CB, rb0 = blockIdx.y * NMS_RW;
-  if (cb0 + NMS_CB <= rb0) return;
-  nms_mask_body(sb, n, nw, thr, mask, rb0, cb0);
+// mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr. grid (nw, nw)
+__global__ __launch_bounds__(64) void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, NmsThr th,
+                                                      unsigned long long* __restrict__ mask) {
+  const int cb = blockIdx.x, rb = blockIdx.y;
+  if (cb < rb) return;
+  nms_mask_body(sb, n, nw, th, mask, rb, cb);
 }
 
 constexpr int NMS_MAXW = 1024;  // n <= 65536
@@ -280,16 +284,16 @@ __global__ void nms_sorted_boxes_b_kernel(const float* __restrict__ b, const int
   d[4] = (x2 - x1) * (y2 - y1);
 }
 
-// grid (ceil(nwmax / NMS_CB), ceil(nwmax / NMS_RW), samples), 256 threads
-__global__ __launch_bounds__(256) void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
-                                                        const long* __restrict__ mask_off, double thr,
+// grid (nwmax, nwmax, samples)
+__global__ __launch_bounds__(64) void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
+                                                        const long* __restrict__ mask_off, NmsThr th,
                                                         unsigned long long* __restrict__ mask_all) {
   const int sm = blockIdx.z;
   const long o = seg[sm], n = seg[sm + 1] - o;
   const int nw = (int)((n + 63) / 64);
-  const int cb0 = blockIdx.x * NMS_CB, rb0 = blockIdx.y * NMS_RW;
-  if (cb0 >= nw || rb0 >= nw || cb0 + NMS_CB <= rb0) return;
-  nms_mask_body(sb_all + o * 5, n, nw, thr, mask_all + mask_off[sm], rb0, cb0);
+  const int cb = blockIdx.x, rb = blockIdx.y;
+  if (cb >= nw || rb >= nw || cb < rb) return;
+  nms_mask_body(sb_all + o * 5, n, nw, th, mask_all + mask_off[sm], rb, cb);
 }
 
 __global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long long* __restrict__ mask_all,
@@ -366,8 +370,7 @@ extern "C" int ivit_nms(const float* boxes_xywha, const float* scores, long n, d
   unsigned long long* mask = (unsigned long long*)w;
   hipLaunchKernelGGL(nms_rank_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, scores, n, order);
   hipLaunchKernelGGL(nms_sorted_boxes_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, boxes_xywha, order, n, sb);
-  hipLaunchKernelGGL(nms_mask_kernel, dim3(ivit_cdiv(nw, NMS_CB), ivit_cdiv(nw, NMS_RW)), dim3(256), 0, st, sb, n, nw,
-                     iou_thr, mask);
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(nw, nw), dim3(64), 0, st, sb, n, nw, nms_thr(iou_thr), mask);
   hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(256), 0, st, mask, n, nw, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;
@@ -438,8 +441,8 @@ extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, c
     return (int)e;
   }
   hipLaunchKernelGGL(nms_sorted_boxes_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, boxes_xywha, order, seg, sb);
-  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(ivit_cdiv(nwmax, NMS_CB), ivit_cdiv(nwmax, NMS_RW), n_samples), dim3(256),
-                     0, st, sb, seg, mask_off, iou_thr, mask);
+  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(nwmax, nwmax, n_samples), dim3(64), 0, st, sb, seg, mask_off,
+                     nms_thr(iou_thr), mask);
   hipLaunchKernelGGL(nms_scan_b_kernel, dim3(n_samples), dim3(256), 0, st, mask, seg, mask_off, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;
