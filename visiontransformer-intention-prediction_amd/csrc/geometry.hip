@@ -89,27 +89,31 @@ __global__ void nms_sorted_boxes_kernel(const float* __restrict__ b, const int* 
 }
 
 // torchvision's test, bit for bit: (double)RN32(inter / u) > thr with u = (area_i + area_j) - inter in
-// f32. For thr >= 0 and u > 0 it is decided without the division (a ~10-instruction VALU sequence,
-// and with divergent lanes the whole wave waits for it): with t the smallest float whose double
-// exceeds thr and mid the midpoint between t and its predecessor, RN32(x) >= t iff x > mid, or
-// x == mid and t is even (ties to even), and x > mid iff inter > mid * u — exact in double (mid has
-// 25 significant bits, u 24). Other cases (u <= 0, NaN, thr < 0) take the division.
+// f32, i.e. RN32(inter / u) >= t, t the smallest float whose double exceeds thr. The IEEE division is
+// a ~10-instruction VALU sequence, and with divergent lanes the whole wave waits for it (anchors
+// overlap their neighbours, so most 64-lane iterations had some lane dividing). Instead
+// q = inter * rcp(u) (relative error < 2^-22) decides every pair whose q lies outside
+// [t - 8 ulp, t + 8 ulp] (a margin of ~2^-20); the rest, and u <= 0 / non-finite operands / a
+// threshold that is negative or below the normal floats, take the exact division.
 struct NmsThr {
-  double thr, mid;
-  int fast, t_even;
+  double thr;
+  float lo, hi;
+  int fast;
 };
 NmsThr nms_thr(double thr) {
-  NmsThr r{thr, 0.0, 0, 0};
-  if (!(thr >= 0.0) || !(thr < 1e30)) return r;
+  NmsThr r{thr, 0.f, 0.f, 0};
+  if (!(thr >= 1e-30) || !(thr < 1e30)) return r;
   float t = (float)thr;
   while ((double)t <= thr) t = nextafterf(t, INFINITY);
   float tp;
-  while ((double)(tp = nextafterf(t, -INFINITY)) > thr) t = tp;  // smallest float above thr
-  tp = nextafterf(t, -INFINITY);
-  r.mid = 0.5 * ((double)tp + (double)t);
-  unsigned bits;
-  memcpy(&bits, &t, 4);
-  r.t_even = (bits & 1u) == 0;
+  while ((double)(tp = nextafterf(t, -INFINITY)) > thr) t = tp;  // the smallest float above thr
+  float lo = t, hi = t;
+  for (int k = 0; k < 8; ++k) {
+    lo = nextafterf(lo, -INFINITY);
+    hi = nextafterf(hi, INFINITY);
+  }
+  r.lo = lo;
+  r.hi = hi;
   r.fast = 1;
   return r;
 }
@@ -120,9 +124,10 @@ IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float i
   const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
   const float inter = w * h;
   const float u = (ia + ca) - inter;
-  if (th.fast && u > 0.f) {
-    const double lhs = (double)inter, rhs = th.mid * (double)u;
-    return lhs > rhs || (lhs == rhs && th.t_even);
+  if (th.fast && u >= 1.17549435e-38f && u < INFINITY && inter < INFINITY) {  // u normal: rcp(u) finite
+    const float q = inter * __builtin_amdgcn_rcpf(u);
+    if (q >= th.hi) return true;
+    if (q <= th.lo) return false;
   }
   const float ovr = inter / u;
   return (double)ovr > th.thr;
