@@ -152,10 +152,13 @@ IVIT_DEV void nms_mask_body(const float* __restrict__ sb, long n, int nw, const 
               ia = sb[i * 5 + 4];
   unsigned long long bits = 0;
   const int lim = (int)min((long)64, n - (long)cb * 64);
-  const int k0 = cb == rb ? t + 1 : 0;  // the diagonal block: only boxes after this one
-  for (int k = k0; k < lim; ++k)
+  // a wave-uniform loop (a per-lane start made the counter and the LDS addresses per-lane, every
+  // iteration under exec-mask control: 4.5 -> 6.3 ms per eval batch); the diagonal block keeps
+  // only the bits of boxes after this one
+  const unsigned long long keep_mask = cb == rb ? (t == 63 ? 0ull : ~0ull << (t + 1)) : ~0ull;
+  for (int k = 0; k < lim; ++k)
     if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cxy[k], car[k], th)) bits |= 1ull << k;
-  mask[i * nw + cb] = bits;
+  mask[i * nw + cb] = bits & keep_mask;
 }
 
 // mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr. grid (nw, nw)
