@@ -119,9 +119,13 @@ NmsThr nms_thr(double thr) {
 }
 IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float ia, float4 c, float ca,
                              const NmsThr& th) {
-  const float xx1 = fmaxf(ix1, c.x), yy1 = fmaxf(iy1, c.y);
-  const float xx2 = fminf(ix2, c.z), yy2 = fminf(iy2, c.w);
-  const float w = fmaxf(0.f, xx2 - xx1), h = fmaxf(0.f, yy2 - yy1);
+  // raw v_max / v_min: fmaxf / fminf on LDS values made the compiler canonicalise each operand
+  // first (one more instruction per use); the corners are never NaN for finite decoded boxes
+  auto vmax = [](float a, float b) { float d; asm("v_max_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b)); return d; };
+  auto vmin = [](float a, float b) { float d; asm("v_min_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b)); return d; };
+  const float xx1 = vmax(ix1, c.x), yy1 = vmax(iy1, c.y);
+  const float xx2 = vmin(ix2, c.z), yy2 = vmin(iy2, c.w);
+  const float w = vmax(0.f, xx2 - xx1), h = vmax(0.f, yy2 - yy1);
   const float inter = w * h;
   const float u = (ia + ca) - inter;
   if (th.fast && u >= 1.17549435e-38f && u < INFINITY && inter < INFINITY) {  // u normal: rcp(u) finite
@@ -133,40 +137,56 @@ IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float i
   return (double)ovr > th.thr;
 }
 
-// one 64-thread workgroup per (row block, column block >= it): the column block's boxes staged in LDS
-// as corners (one ds_read_b128) and area
+// One 64-thread workgroup per (row block rb, chunk of NMS_CB column blocks >= rb): the rows' boxes
+// stay in registers while the chunk's column blocks pass through LDS (corners as one float4, the
+// area), each block's boxes loaded into registers one block ahead. A workgroup per (rb, cb) pair
+// meant ~4 M one-wave workgroups per eval batch (half of them empty, below the diagonal).
+constexpr int NMS_CB = 8;
 IVIT_DEV void nms_mask_body(const float* __restrict__ sb, long n, int nw, const NmsThr& th,
-                            unsigned long long* __restrict__ mask, int rb, int cb) {
-  __shared__ float4 cxy[64];
-  __shared__ float car[64];
+                            unsigned long long* __restrict__ mask, int rb, int cb0) {
+  __shared__ float4 cxy[2][64];
+  __shared__ float car[2][64];
   const int t = threadIdx.x;
-  const long cj = (long)cb * 64 + t;
-  if (cj < n) {
-    cxy[t] = make_float4(sb[cj * 5 + 0], sb[cj * 5 + 1], sb[cj * 5 + 2], sb[cj * 5 + 3]);
-    car[t] = sb[cj * 5 + 4];
-  }
-  __syncthreads();
   const long i = (long)rb * 64 + t;
-  if (i >= n) return;
-  const float ix1 = sb[i * 5 + 0], iy1 = sb[i * 5 + 1], ix2 = sb[i * 5 + 2], iy2 = sb[i * 5 + 3],
-              ia = sb[i * 5 + 4];
-  unsigned long long bits = 0;
-  const int lim = (int)min((long)64, n - (long)cb * 64);
-  // a wave-uniform loop (a per-lane start made the counter and the LDS addresses per-lane, every
-  // iteration under exec-mask control: 4.5 -> 6.3 ms per eval batch); the diagonal block keeps
-  // only the bits of boxes after this one
-  const unsigned long long keep_mask = cb == rb ? (t == 63 ? 0ull : ~0ull << (t + 1)) : ~0ull;
-  for (int k = 0; k < lim; ++k)
-    if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cxy[k], car[k], th)) bits |= 1ull << k;
-  mask[i * nw + cb] = bits & keep_mask;
+  const bool row_ok = i < n;
+  float ix1 = 0.f, iy1 = 0.f, ix2 = 0.f, iy2 = 0.f, ia = 0.f;
+  if (row_ok) {
+    ix1 = sb[i * 5 + 0]; iy1 = sb[i * 5 + 1]; ix2 = sb[i * 5 + 2]; iy2 = sb[i * 5 + 3]; ia = sb[i * 5 + 4];
+  }
+  const int cbs = max(cb0, rb), cb1 = min(cb0 + NMS_CB, nw);
+  float4 pxy = make_float4(0.f, 0.f, 0.f, 0.f);
+  float pa = 0.f;
+  auto fetch = [&](int cb) {
+    const long cj = (long)cb * 64 + t;
+    if (cj < n) {
+      pxy = make_float4(sb[cj * 5 + 0], sb[cj * 5 + 1], sb[cj * 5 + 2], sb[cj * 5 + 3]);
+      pa = sb[cj * 5 + 4];
+    }
+  };
+  if (cbs < cb1) fetch(cbs);
+  for (int cb = cbs; cb < cb1; ++cb) {
+    const int buf = (cb - cbs) & 1;
+    cxy[buf][t] = pxy;
+    car[buf][t] = pa;
+    if (cb + 1 < cb1) fetch(cb + 1);
+    __syncthreads();  // one wave: publishes this block's boxes (the other buffer is the next one's)
+    const int lim = (int)min((long)64, n - (long)cb * 64);
+    // a wave-uniform loop; the diagonal block keeps only the bits of boxes after this one
+    const unsigned long long keep_mask = cb == rb ? (t == 63 ? 0ull : ~0ull << (t + 1)) : ~0ull;
+    unsigned long long bits = 0;
+    for (int k = 0; k < lim; ++k)
+      if (nms_suppresses(ix1, iy1, ix2, iy2, ia, cxy[buf][k], car[buf][k], th)) bits |= 1ull << k;
+    if (row_ok) mask[i * nw + cb] = bits & keep_mask;
+  }
 }
 
-// mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr. grid (nw, nw)
+// mask[p][w] bit k: sorted box 64w+k (> p) overlaps sorted box p with IoU > thr.
+// grid (ceil(nw / NMS_CB), nw)
 __global__ __launch_bounds__(64) void nms_mask_kernel(const float* __restrict__ sb, long n, int nw, NmsThr th,
                                                       unsigned long long* __restrict__ mask) {
-  const int cb = blockIdx.x, rb = blockIdx.y;
-  if (cb < rb) return;
-  nms_mask_body(sb, n, nw, th, mask, rb, cb);
+  const int cb0 = blockIdx.x * NMS_CB, rb = blockIdx.y;
+  if (cb0 + NMS_CB <= rb) return;
+  nms_mask_body(sb, n, nw, th, mask, rb, cb0);
 }
 
 constexpr int NMS_MAXW = 1024;  // n <= 65536
@@ -292,16 +312,16 @@ __global__ void nms_sorted_boxes_b_kernel(const float* __restrict__ b, const int
   d[4] = (x2 - x1) * (y2 - y1);
 }
 
-// grid (nwmax, nwmax, samples)
+// grid (ceil(nwmax / NMS_CB), nwmax, samples)
 __global__ __launch_bounds__(64) void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
                                                         const long* __restrict__ mask_off, NmsThr th,
                                                         unsigned long long* __restrict__ mask_all) {
   const int sm = blockIdx.z;
   const long o = seg[sm], n = seg[sm + 1] - o;
   const int nw = (int)((n + 63) / 64);
-  const int cb = blockIdx.x, rb = blockIdx.y;
-  if (cb >= nw || rb >= nw || cb < rb) return;
-  nms_mask_body(sb_all + o * 5, n, nw, th, mask_all + mask_off[sm], rb, cb);
+  const int cb0 = blockIdx.x * NMS_CB, rb = blockIdx.y;
+  if (cb0 >= nw || rb >= nw || cb0 + NMS_CB <= rb) return;
+  nms_mask_body(sb_all + o * 5, n, nw, th, mask_all + mask_off[sm], rb, cb0);
 }
 
 __global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long long* __restrict__ mask_all,
@@ -378,7 +398,8 @@ extern "C" int ivit_nms(const float* boxes_xywha, const float* scores, long n, d
   unsigned long long* mask = (unsigned long long*)w;
   hipLaunchKernelGGL(nms_rank_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, scores, n, order);
   hipLaunchKernelGGL(nms_sorted_boxes_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, boxes_xywha, order, n, sb);
-  hipLaunchKernelGGL(nms_mask_kernel, dim3(nw, nw), dim3(64), 0, st, sb, n, nw, nms_thr(iou_thr), mask);
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(ivit_cdiv(nw, NMS_CB), nw), dim3(64), 0, st, sb, n, nw, nms_thr(iou_thr),
+                     mask);
   hipLaunchKernelGGL(nms_scan_kernel, dim3(1), dim3(256), 0, st, mask, n, nw, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;
@@ -449,8 +470,8 @@ extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, c
     return (int)e;
   }
   hipLaunchKernelGGL(nms_sorted_boxes_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, boxes_xywha, order, seg, sb);
-  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(nwmax, nwmax, n_samples), dim3(64), 0, st, sb, seg, mask_off,
-                     nms_thr(iou_thr), mask);
+  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(ivit_cdiv(nwmax, NMS_CB), nwmax, n_samples), dim3(64), 0, st, sb, seg,
+                     mask_off, nms_thr(iou_thr), mask);
   hipLaunchKernelGGL(nms_scan_b_kernel, dim3(n_samples), dim3(256), 0, st, mask, seg, mask_off, order, keep, count);
   IVIT_LAUNCH_CHECK();
   return 0;
