@@ -94,7 +94,8 @@ __global__ void nms_sorted_boxes_kernel(const float* __restrict__ b, const int* 
 // overlap their neighbours, so most 64-lane iterations had some lane dividing). Instead
 // q = inter * rcp(u) (relative error < 2^-22) decides every pair whose q lies outside
 // [t - 8 ulp, t + 8 ulp] (a margin of ~2^-20); the rest, and u <= 0 / non-finite operands / a
-// threshold that is negative or below the normal floats, take the exact division.
+// threshold that is negative or below the normal floats, take the exact division. Disjoint pairs
+// (inter = 0) are decided before any of it.
 struct NmsThr {
   double thr;
   float lo, hi;
@@ -127,6 +128,8 @@ IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float i
   const float xx2 = vmin(ix2, c.z), yy2 = vmin(iy2, c.w);
   const float w = vmax(0.f, xx2 - xx1), h = vmax(0.f, yy2 - yy1);
   const float inter = w * h;
+  // disjoint boxes (most pairs): inter = 0 gives 0 / u = +-0 or NaN, never above a threshold >= 0
+  if (th.fast && !(inter > 0.f)) return false;
   const float u = (ia + ca) - inter;
   if (th.fast && u >= 1.17549435e-38f && u < INFINITY && inter < INFINITY) {  // u normal: rcp(u) finite
     const float q = inter * __builtin_amdgcn_rcpf(u);
