@@ -197,9 +197,9 @@ constexpr int NMS_MAXW = 1024;  // n <= 65536
 // The greedy walk of torchvision's nms over the suppression mask (one workgroup per sample):
 // column block c (64 sorted boxes) is settled by wave 0 on SCALAR registers (each diagonal word
 // read by v_readlane; the serial 64-step chain runs on the scalar unit), then the kept boxes'
-// mask rows are OR-ed into the removed words of the later columns by all 256 threads, 32 word
-// lanes x 8 kept-box groups, with 64-bit LDS atomic ORs: a column's loads are independent
-// (the earlier per-word loop over the kept bits waited for each load in turn).
+// mask rows are OR-ed into the removed words of the later columns, one owner thread per word with
+// the kept rows' words loaded eight at a time (the earlier per-word loop over the kept bits waited
+// for each load in turn).
 IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n, int nw, const int* __restrict__ order,
                             long* __restrict__ keep, long* __restrict__ count_out) {
   __shared__ unsigned long long removed[NMS_MAXW];
@@ -257,19 +257,18 @@ IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n,
     }
     const int K = __popcll(kept_s);
     if (K) {
-      const int wl = threadIdx.x & 31, bg = threadIdx.x >> 5;
+      // each later word has one owner thread (no atomics); its kept rows' words are loaded 8 at a time
       const unsigned long long* blk = mask + (long)c * 64 * nw;
-      for (int wc = c + 1 + wl; wc < nw; wc += 32) {
-        unsigned long long v[8];
+      for (int wc = c + 1 + threadIdx.x; wc < nw; wc += 256) {
+        unsigned long long acc = removed[wc];
+        for (int b0 = 0; b0 < K; b0 += 8) {
+          unsigned long long v[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {  // up to 8 independent loads in flight per thread
-          const int b = bg + 8 * q;
-          v[q] = b < K ? blk[(long)kbit[b] * nw + wc] : 0ull;
+          for (int q = 0; q < 8; ++q) v[q] = b0 + q < K ? blk[(long)kbit[b0 + q] * nw + wc] : 0ull;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc |= v[q];
         }
-        unsigned long long acc = 0ull;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc |= v[q];
-        if (acc) atomicOr(&removed[wc], acc);
+        removed[wc] = acc;
       }
     }
     __syncthreads();
