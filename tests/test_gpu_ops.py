@@ -153,20 +153,15 @@ def test_attention(B, N, H, cd):
         assert _rel(d[:, i], g[:, i]) < (1e-4 if cdt == F32 else 3e-2), ("qkv"[i], _rel(d[:, i], g[:, i]))
 
 
-@pytest.mark.parametrize("form", ["000", "110", "111"])
 @pytest.mark.parametrize("B,N,H", [(1, 64, 1), (2, 257, 3), (1, 4501, 2), (1, 1, 1), (1, 33, 1), (1, 128, 2),
                                    (1, 130, 1), (1, 200, 1), (1, 320, 2), (3, 449, 1)])
-def test_attention_q2_prescaled_path(B, N, H, form, monkeypatch):
+def test_attention_q2_prescaled_path(B, N, H):
     """bf16 ViT-block path: the qkv projection stores q * log2(e)/8 (ivit_linear_fwd_qs) and the
     attention kernels run on it (ivit_attn_fwd_q2 / _bwd_q2). Outputs, lse and the gradient w.r.t.
-    the UNSCALED q, k, v against the f64 reference on the unscaled q (bf16 tolerances). form: the
-    dK/dV, dQ and forward kernels in their 32x32x16 (0) or v_mfma_f32_16x16x32_bf16 (1) forms
-    (IVIT_ATTN_DKV16, IVIT_ATTN_DQ16, IVIT_ATTN_FWD16)."""
+    the UNSCALED q, k, v against the f64 reference on the unscaled q (bf16 tolerances). The backward
+    runs the v_mfma_f32_16x16x32_bf16 dQ and dK/dV kernels (incl. the masked ragged key tile)."""
     import ops
     from _lib import BF16
-    monkeypatch.setenv("IVIT_ATTN_DKV16", form[0])
-    monkeypatch.setenv("IVIT_ATTN_DQ16", form[1])
-    monkeypatch.setenv("IVIT_ATTN_FWD16", form[2])
     D = H * 64
     M, K = B * N, 96
     x = torch.randn(M, K)

@@ -9,7 +9,7 @@
 //             CDNA4 transposing LDS read.
 //   backward: dQ kernel (query block, sweep keys) and dK/dV kernel (key block, sweep
 //             queries); both recompute P from the saved LSE. No atomics. The prescaled-Q
-//             (bf16 ViT block) path runs the software-pipelined v3 kernels; the plain bf16
+//             (bf16 ViT block) path runs the software-pipelined 16x16x32 v4 kernels; the plain bf16
 //             entry point keeps the v2 tile loops.
 // f32 path (parity): exact-f32 MFMA GEMMs through the generic engine with the score
 //             matrix materialised in the workspace, plus row-softmax kernels.
@@ -319,255 +319,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
   if (q < N && hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
 }
 
-// ------------------------------------------------------------------------- forward v7 (16x16x32)
-// v6's algorithm (prescaled Q, -m as the S chains' initial accumulator, lazy rescale, one barrier
-// per key tile, K two tiles ahead and V one by LDS-DMA) with every product as
-// v_mfma_f32_16x16x32_bf16. Per wave 32 queries = 2 query blocks i; per 64-key tile 4 key blocks kb:
-//   S'^T_{kb,i} = K_kb Q_i^T - m_i        (C layout: lane (g, c) holds keys 16kb + 4g + r of query
-//                                          16i + c)                                  16 MFMA
-//   O^T_{e,i} += V^T_{e,.} P^T_{.,i}     (B operand of k step s = (P_{2s,i}, P_{2s+1,i}) packed as
-//                                          they stand; A operand two transposing reads of V)   16 MFMA
-//   l_i += 1^T P^T_{.,i}                                                                          4 MFMA
-// A query's row max spans the four lanes c, c + 16, c + 32, c + 48 (quad_max: two permlane swaps).
-template <int W, bool PRE>
-__global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v7_kernel(const bf16* __restrict__ qkv, int N, int H,
-                                                                        bf16* __restrict__ out,
-                                                                        float* __restrict__ lse, float c2) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int g = lane >> 4, c16 = lane & 15;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int2 bid = attn_block_id();
-  const int z = bid.y, b = z / H, h = z - b * H;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
-  const int qw = bid.x * (32 * W) + wv * 32;
-  bf16x8 qf[2][2];  // B operand: Q[qw + 16i + c][dims 32s + 8g .. +7]
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = qw + 16 * i + c16;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      Pack8 pq;
-      pq.u = q < N ? *(const uint4*)(Qb + (long)q * ld + 32 * s + 8 * g) : make_uint4(0, 0, 0, 0);
-      qf[i][s] = pq.v;
-      if constexpr (PRE) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) qf[i][s][e] = (bf16)((float)qf[i][s][e] * c2);
-      }
-    }
-  }
-  const int nt = (N + AK - 1) / AK, nfull = N / AK;
-  unsigned off[8 / W];
-#pragma unroll
-  for (int i = 0; i < 8 / W; ++i) off[i] = 2u * dma_off16<W>(i, wv, lane, ld);
-  auto issue1 = [&](const bf16* base, int kt, char* img) {
-    const char* sb = uniform_ptr(base + (long)kt * AK * ld);
-#pragma unroll
-    for (int i = 0; i < 8 / W; ++i) {
-      const int piece = wv * (8 / W) + i;
-      unsigned o = off[i];
-      if (kt >= nfull) {  // keys past N: row N-1 (finite V; their scores are masked)
-        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ (row & 6);
-        o = 2u * (unsigned)((min(kt * AK + row, N - 1) - kt * AK) * ld + c * 8);
-      }
-      glds_s<false>(o, sb, img + piece * 1024);
-    }
-  };
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-  // per-lane LDS offsets: K row reads (+ 2048 kb), V transposed reads (+ 4096 s, + 2048 second half)
-  unsigned kro[2], vtr[4];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) kro[s] = (unsigned)t16_off(c16, 4 * s + g);
-  {
-    const int q = (lane >> 2) & 3, p = lane & 3;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) vtr[e] = (unsigned)(t16_off(4 * g + q, 2 * e + (p >> 1)) + 8 * (p & 1));
-  }
-#pragma unroll
-  for (int s = 0; s < 2; ++s) asm volatile("" : "+v"(kro[s]));
-#pragma unroll
-  for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(vtr[e]));
-  auto kfrag = [&](const char* kimg, int kb, int s) { return *(const bf16x8*)(kimg + kro[s] + 2048 * kb); };
-  auto vfrag = [&](const char* vimg, int e, int s) {
-    union { s16x4 s[2]; bf16x8 v; } u;
-    u.s[0] = ds_tr(vimg + vtr[e] + 4096 * s);
-    u.s[1] = ds_tr(vimg + vtr[e] + 4096 * s + 2048);
-    return u.v;
-  };
-  auto mask_tile = [&](f32x4 (&t)[4][2], int kbase) {  // keys >= N -> NEG_BIG (ragged tile only)
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool dead = kbase + 16 * kb + 4 * g + r >= N;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) t[kb][i][r] = dead ? NEG_BIG : t[kb][i][r];
-      }
-  };
-  auto tile_max = [&](const f32x4 (&t)[4][2], int i) {
-    float a = NEG_BIG, bm = NEG_BIG;
-#pragma unroll
-    for (int kb = 0; kb < 4; kb += 2) {
-      a = vmax3(a, t[kb][i][0], t[kb][i][1]);
-      a = vmax3(a, t[kb][i][2], t[kb][i][3]);
-      bm = vmax3(bm, t[kb + 1][i][0], t[kb + 1][i][1]);
-      bm = vmax3(bm, t[kb + 1][i][2], t[kb + 1][i][3]);
-    }
-    return quad_max(fmaxf(a, bm));
-  };
-
-  // prologue: S'_0 (from a zero accumulator), m = its row max, then S'_0 - m; K_1 in flight
-  issue1(Kb, 0, smem[0][0]);
-  issue1(Vb, 0, smem[0][1]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (nt > 1) issue1(Kb, 1, smem[1][0]);
-  f32x4 sc[4][2], sn[4][2];
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      sc[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < 2; ++s) sc[kb][i] = mfma16(kfrag(smem[0][0], kb, s), qf[i][s], sc[kb][i]);
-    }
-  if (nfull == 0) mask_tile(sc, 0);
-  float m[2];
-  f32x4 negm[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    m[i] = tile_max(sc, i);
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sc[kb][i][r] -= m[i];
-    negm[i] = f32x4{-m[i], -m[i], -m[i], -m[i]};
-  }
-  f32x4 o[4][2], lacc[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    lacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-
-  // one tile step: S'_{j+1} = K_{j+1} Q^T - m (16 MFMA) beside P_j = exp2(S'_j) (VALU), then
-  // O^T += V_j^T P_j^T, l += 1^T P_j^T (20 MFMA) beside the row max of S'_{j+1}
-  auto step = [&](const char* kimg, const char* vimg, f32x4 (&cur)[4][2], f32x4 (&nxt)[4][2], int kbase,
-                  float (&mt)[2]) {
-    unsigned pw[2][2][4];  // [i][s][word]: B operand of PV k step s for query block i
-    auto ex = [&](int k) {  // k = 0..15: (i, s, word): two exps, one packed word
-      const int i = k >> 3, s = (k >> 2) & 1, w = k & 3;
-      const int kb = 2 * s + (w >> 1), r = 2 * (w & 1);
-      pw[i][s][w] = pk_bf16(fast_exp2(cur[kb][i][r]), fast_exp2(cur[kb][i][r + 1]));
-    };
-    bf16x8 kf[3];
-    kf[0] = kfrag(kimg, 0, 0);
-    kf[1] = kfrag(kimg, 1, 0);
-#pragma unroll
-    for (int mi = 0; mi < 16; ++mi) {
-      const int s = mi >> 3, kb = (mi >> 1) & 3, i = mi & 1;
-      const int f = mi >> 1;  // fragment (s, kb) index, used by i = 0 and 1
-      if (i == 0 && f + 2 < 8) kf[(f + 2) % 3] = kfrag(kimg, ((f + 2) & 3), (f + 2) >> 2);
-      nxt[kb][i] = mfma16(kf[f % 3], qf[i][s], s == 0 ? negm[i] : nxt[kb][i]);
-      ex(mi);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    bf16x8 vf[3];
-    vf[0] = vfrag(vimg, 0, 0);
-    vf[1] = vfrag(vimg, 1, 0);
-    if (kbase + AK > N) mask_tile(nxt, kbase);
-    float a[2] = {NEG_BIG, NEG_BIG};
-#pragma unroll
-    for (int mi = 0; mi < 20; ++mi) {
-      // 8 V fragments (s, e), each feeding two MFMAs (i = 0, 1); the l MFMAs after each k step
-      if (mi < 16) {
-        const int s = mi >> 3, e = (mi >> 1) & 3, i = mi & 1, f = mi >> 1;
-        if (i == 0 && f + 2 < 8) vf[(f + 2) % 3] = vfrag(vimg, (f + 2) & 3, (f + 2) >> 2);
-        o[e][i] = mfma16(vf[f % 3], __builtin_bit_cast(bf16x8, make_uint4(pw[i][s][0], pw[i][s][1], pw[i][s][2],
-                                                                            pw[i][s][3])),
-                         o[e][i]);
-      } else {
-        const int s = (mi - 16) >> 1, i = (mi - 16) & 1;
-        lacc[i] = mfma16(ones, __builtin_bit_cast(bf16x8, make_uint4(pw[i][s][0], pw[i][s][1], pw[i][s][2],
-                                                                       pw[i][s][3])),
-                         lacc[i]);
-      }
-      if (mi >= 4 && mi < 12) {  // row max of S'_{j+1}: block kb = mi - 4 (two per i)
-        const int kb = (mi - 4) >> 1, i = (mi - 4) & 1;
-        a[i] = vmax3(a[i], nxt[kb][i][0], nxt[kb][i][1]);
-        a[i] = vmax3(a[i], nxt[kb][i][2], nxt[kb][i][3]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    mt[0] = quad_max(a[0]);
-    mt[1] = quad_max(a[1]);
-  };
-  // after S'_{j+1} - m and its row max mt: move m lazily; the next tile is shifted with it
-  auto rescale = [&](const float (&mt)[2], f32x4(&nxt)[4][2]) {
-    const bool moved0 = mt[0] > TAU, moved1 = mt[1] > TAU;
-    if (__any(moved0 || moved1)) {
-      const float d[2] = {moved0 ? mt[0] : 0.f, moved1 ? mt[1] : 0.f};
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const float alpha = fast_exp2(-d[i]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[e][i][r] *= alpha;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) lacc[i][r] *= alpha;
-#pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) nxt[kb][i][r] -= d[i];
-        m[i] += d[i];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) asm volatile("v_sub_f32 %0, %0, %1" : "+v"(negm[i][r]) : "v"(d[i]));
-      }
-    }
-  };
-  auto body = [&](auto stage, int j, f32x4(&cur)[4][2], f32x4(&nxt)[4][2]) {
-    constexpr int S = decltype(stage)::value;  // V_j in smem[S][1], K_{j+1} in smem[S^1][0]
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (j + 2 < nt) issue1(Kb, j + 2, smem[S][0]);
-    if (j + 1 < nt) issue1(Vb, j + 1, smem[S ^ 1][1]);
-    float mt[2];
-    step(smem[S ^ 1][0], smem[S][1], cur, nxt, (j + 1) * AK, mt);
-    rescale(mt, nxt);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  int j = 0;
-  for (; j + 1 < nt; j += 2) {
-    body(I0{}, j, sc, sn);
-    body(I1{}, j + 1, sn, sc);
-  }
-  if (j < nt) body(I0{}, j, sc, sn);
-  // epilogue: lane (g, c) holds O[q = qw + 16i + c][d = 16e + 4g + r]: 8-B stores
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = qw + 16 * i + c16;
-    const float l = lacc[i][0];
-    const float inv = 1.f / l;
-    if (q < N) {
-      bf16* orow = out + ((long)b * N + q) * D + h * 64 + 4 * g;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        *(uint2*)(orow + 16 * e) = make_uint2(pk_bf16(o[e][i][0] * inv, o[e][i][1] * inv),
-                                              pk_bf16(o[e][i][2] * inv, o[e][i][3] * inv));
-      if (g == 0) lse[(long)z * N + q] = (m[i] + log2f(l)) * 0.69314718055994531f;
-    }
-  }
-}
-
 // ------------------------------------------------------------------------- backward v2 (bf16)
 // Row constants for the backward in a padded layout [z][Npad] (Npad = N rounded up to 64):
 // lse2 = lse * log2(e) (+1e30 on padding rows, so their probabilities are exactly 0) and
@@ -849,8 +600,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
   }
 }
 
-// ------------------------------------------------------------------------- backward v3 (bf16, prescaled Q)
-// The v2 loops were issue-bound: per 64x32 wave-tile of the dK/dV kernel ~140 VALU beside 32
+// ------------------------------------------------------------------------- backward pipeline (prescaled Q)
+// (The round-2 "v3" structure, kept by the 16x16x32 v4 kernels below.) The v2 loops were issue-bound: per 64x32 wave-tile of the dK/dV kernel ~140 VALU beside 32
 // MFMAs (the element-wise bf16 packing re-shuffled by v_alignbit / v_perm, accumulator copies),
 // and every S / dP chain MFMA waited (lgkmcnt) on the LDS read issued just before it. v3 keeps
 // the same algorithm and data flow, software-pipelined over 32-row units u (half a 64-row tile):
@@ -863,223 +614,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __r
 // the first body of the following tile. One barrier per tile, in the middle of its second body:
 // it publishes the next tile (DMA issued one tile ahead) and frees the stage of the tile before.
 
-// accumulator registers 8s..8s+7 -> bf16x8 operand, 4 v_cvt_pk_bf16_f32 (no re-packing)
-IVIT_DEV bf16x8 pack8(const f32x16& a, int s) {
-  const uint4 u = make_uint4(pk_bf16(a[8 * s], a[8 * s + 1]), pk_bf16(a[8 * s + 2], a[8 * s + 3]),
-                             pk_bf16(a[8 * s + 4], a[8 * s + 5]), pk_bf16(a[8 * s + 6], a[8 * s + 7]));
-  return __builtin_bit_cast(bf16x8, u);
-}
-
-constexpr int BNS = 3;  // LDS stages of the v3 backward kernels
-
-// dK/dV: W waves x 32 keys (K, V fragments in registers), query tiles of 64 rows with their
-// negated row constants (-lse2, -delta; padded rows -1e30 / 0, so P = 0 there, no mask).
-// (W = 8, one 512-thread workgroup per CU sharing each Q / dO tile, halves the L2 -> LDS bytes
-// but measured slower; the product uses W = 4.)
-template <int W>
-__global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v3_kernel(const bf16* __restrict__ qkv,
-                                                                 const bf16* __restrict__ dout,
-                                                                 const float* __restrict__ nlse2p,
-                                                                 const float* __restrict__ ndeltap, int N, int Npad,
-                                                                 int H, bf16* __restrict__ dqkv, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][Q|dO]
-  __shared__ __attribute__((aligned(16))) float srow[BNS][2][AK];  // [stage][-lse2|-delta]
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int2 bid = attn_block_id();
-  const int z = bid.y, b = z / H, h = z - b * H;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
-  const bf16* Gb = dout + (long)b * N * D + h * 64;
-  const char* Ls = uniform_ptr(nlse2p + (long)z * Npad);
-  const char* Ds = uniform_ptr(ndeltap + (long)z * Npad);
-  constexpr int PW = 8 / W;  // DMA pieces per wave per 8-KiB tile image
-  const int key = bid.x * (32 * W) + wv * 32 + (lane & 31);
-  bf16x8 kf[4], vf[4];
-  load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
-  load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
-  retire_loads(kf, vf);
-  f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
-  const int nt = (N + AK - 1) / AK, nfull = N / AK;
-  // DMA: saddr form (tile base in SGPRs, 32-bit per-lane byte offsets, k-invariant on full
-  // tiles); rows past N are clamped to row N-1: their lse2 padding makes P = 0 there
-  unsigned offq[PW], offg[PW];
-#pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    offq[i] = 2u * dma_off<W>(i, wv, lane, ld);
-    offg[i] = 2u * dma_off<W>(i, wv, lane, D);
-  }
-  auto issue = [&](int qt, int S) {
-    char* qimg = smem[S][0];
-    char* gimg = smem[S][1];
-    const char* qb = uniform_ptr(Qb + (long)qt * AK * ld);
-    const char* gb = uniform_ptr(Gb + (long)qt * AK * D);
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int piece = wv * PW + i;
-      unsigned oq = offq[i], og = offg[i];
-      if (qt >= nfull) {
-        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128(row);
-        const int r = min(qt * AK + row, N - 1) - qt * AK;
-        oq = 2u * (unsigned)(r * ld + c * 8);
-        og = 2u * (unsigned)(r * D + c * 8);
-      }
-      glds_s<false>(oq, qb, qimg + piece * 1024);
-      glds_s<false>(og, gb, gimg + piece * 1024);
-    }
-    if (wv == 0) {  // bases in SGPRs, the tile offset in the per-lane offset
-      glds4_s(4u * (lane + qt * AK), Ls, &srow[S][0][0]);
-      glds4_s(4u * (lane + qt * AK), Ds, &srow[S][1][0]);
-    }
-  };
-
-  // pipeline registers: fragments + initial accumulators of the next A, scores of the last A,
-  // packed P / dS and transposed fragments of the pending B
-  bf16x8 qa[4], ga[4];
-  f32x16 sn, dn;   // A(u+1) chains' initial accumulators (-lse2 / -delta rows of its 32 queries)
-  f32x16 sc, dc;   // A(u) results: S' - lse2, dP - delta
-  auto read_frag = [&](const char* qimg, const char* gimg, int t, int ks) {
-    qa[ks] = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-    ga[ks] = *(const bf16x8*)(gimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-  };
-  auto read_rows = [&](const float* lr, const float* dr, int t, int part) {  // 4 of the 16 row constants
-    const float4 l4 = *(const float4*)(lr + 32 * t + 8 * part + 4 * hl);
-    const float4 d4 = *(const float4*)(dr + 32 * t + 8 * part + 4 * hl);
-    sn[4 * part] = l4.x; sn[4 * part + 1] = l4.y; sn[4 * part + 2] = l4.z; sn[4 * part + 3] = l4.w;
-    dn[4 * part] = d4.x; dn[4 * part + 1] = d4.y; dn[4 * part + 2] = d4.z; dn[4 * part + 3] = d4.w;
-  };
-  unsigned up[8], ud[8];  // packed P / dS of the pending B (words 4ss..4ss+3: 16-row half ss)
-  bf16x8 tg0[2], tg1[2], tq0[2], tq1[2];
-  // E: scores 2i, 2i+1 -> one packed word of P and of dS
-  auto e_step = [&](int i) {
-    const float p0 = fast_exp2(sc[2 * i]), p1 = fast_exp2(sc[2 * i + 1]);
-    up[i] = pk_bf16(p0, p1);
-    ud[i] = pk_bf16(p0 * dc[2 * i], p1 * dc[2 * i + 1]);
-  };
-  auto word8 = [&](const unsigned (&w)[8], int ss) {
-    return __builtin_bit_cast(bf16x8, make_uint4(w[4 * ss], w[4 * ss + 1], w[4 * ss + 2], w[4 * ss + 3]));
-  };
-  auto read_b = [&](const char* qimg, const char* gimg, int t, int ss) {
-    const int rb = 32 * t + 16 * ss;
-    tg0[ss] = tr_acc_order(gimg, rb, 0, lane);
-    tg1[ss] = tr_acc_order(gimg, rb, 32, lane);
-    tq0[ss] = tr_acc_order(qimg, rb, 0, lane);
-    tq1[ss] = tr_acc_order(qimg, rb, 32, lane);
-  };
-  // body: A(u) on (SA, tA) || E(u-1); B(u-1) on (SB, tB) || reads of A(u+1) on (SN, tN).
-  // BAR: barrier in the middle (tA == 1): tile of A(u+1) published, DMA of tile jn issued.
-  auto body = [&](auto sa, auto ta, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
-    constexpr int SA = decltype(sa)::value, TA = decltype(ta)::value, SB = decltype(sb)::value;
-    constexpr int TB = decltype(tb)::value, SN = decltype(sn_)::value, TN = decltype(tn)::value;
-    constexpr bool BAR = decltype(bar)::value;
-    f32x16 s = sn, dp = dn;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      const int ks = g >> 1;
-      if ((g & 1) == 0) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[ks], kf[ks], s, 0, 0, 0);
-      else dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[ks], vf[ks], dp, 0, 0, 0);
-      if ((g & 1) == 0 && ks < 3) read_frag(smem[SA][0], smem[SA][1], TA, ks + 1);  // 2-3 gaps ahead
-      e_step(g);
-      if (g == 4) read_b(smem[SB][0], smem[SB][1], TB, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (BAR) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (jn < nt) issue(jn, jn % BNS);
-    }
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      const int ss = g >> 2;
-      if (g == 1) read_b(smem[SB][0], smem[SB][1], TB, 1);
-      switch (g & 3) {
-        case 0: dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(up, ss), tg0[ss], dv0, 0, 0, 0); break;
-        case 1: dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq0[ss], dk0, 0, 0, 0); break;
-        case 2: dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(up, ss), tg1[ss], dv1, 0, 0, 0); break;
-        default: dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq1[ss], dk1, 0, 0, 0); break;
-      }
-      if (more) {
-        if (g & 1) read_rows(srow[SN][0], srow[SN][1], TN, g >> 1);
-        if (g == 6) read_frag(smem[SN][0], smem[SN][1], TN, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    sc = s;
-    dc = dp;
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using F = std::false_type;
-  using T = std::true_type;
-
-  // prologue: tiles 0 (and 1) in flight, A(0)'s operands; B(-1) runs on P = dS = 0 against a
-  // zeroed stage 2 so that every body has the same shape
-  issue(0, 0);
-  if (nt > 1) issue(1, 1);
-  {
-    uint4* z2 = (uint4*)&smem[2][0][0];  // B(-1)'s stage: finite zeros
-    for (int i = tid; i < 2 * 8192 / 16; i += 64 * W) z2[i] = make_uint4(0, 0, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int part = 0; part < 4; ++part) read_rows(srow[0][0], srow[0][1], 0, part);
-  read_frag(smem[0][0], smem[0][1], 0, 0);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    sc[r] = NEG_BIG;  // exp2 -> 0
-    dc[r] = 0.f;
-  }
-  // tile j in stage j % 3: body(2j) = A(j,0) | B(j-1,1) | next A(j,1); body(2j+1) = A(j,1) |
-  // barrier (tile j+1 landed; issue tile j+2) | B(j,0) | next A(j+1,0)
-  auto tile = [&](auto s, int j) {
-    constexpr int S = decltype(s)::value;
-    using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
-    using SNX = std::integral_constant<int, (S + 1) % BNS>;
-    using SC = std::integral_constant<int, S>;
-    body(SC{}, I0{}, SP{}, I1{}, SC{}, I1{}, F{}, 0, true);
-    body(SC{}, I1{}, SC{}, I0{}, SNX{}, I0{}, T{}, j + 2, j + 1 < nt);
-  };
-  int j = 0;
-  for (; j + 3 <= nt; j += 3) {
-    tile(I0{}, j);
-    tile(I1{}, j + 1);
-    tile(I2{}, j + 2);
-  }
-  if (j < nt) tile(I0{}, j);
-  if (j + 1 < nt) tile(I1{}, j + 1);
-  // drain: E and B of the last unit (tile nt-1, rows 32..63)
-  {
-    const int S = (nt - 1) % BNS;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) e_step(i);
-    read_b(smem[S][0], smem[S][1], 1, 0);
-    read_b(smem[S][0], smem[S][1], 1, 1);
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(up, ss), tg0[ss], dv0, 0, 0, 0);
-      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq0[ss], dk0, 0, 0, 0);
-      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(up, ss), tg1[ss], dv1, 0, 0, 0);
-      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(word8(ud, ss), tq1[ss], dk1, 0, 0, 0);
-    }
-  }
-  const int kw = bid.x * (32 * W) + wv * 32;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;
-    if (kk < N) {
-      bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
-      row[D + (lane & 31)] = (bf16)(dk0[r] * scale);
-      row[D + 32 + (lane & 31)] = (bf16)(dk1[r] * scale);
-      row[2 * D + (lane & 31)] = (bf16)dv0[r];
-      row[2 * D + 32 + (lane & 31)] = (bf16)dv1[r];
-    }
-  }
-}
+constexpr int BNS = 3;  // LDS stages of the pipelined backward kernels
 
 // ------------------------------------------------------------------------- backward v4 (16x16x32)
 // The dK/dV kernel with every product as v_mfma_f32_16x16x32_bf16 (MI355X_MICROARCH.md DVFS item 7:
@@ -1330,203 +865,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
         }
       }
     }
-}
-
-// dQ: 4 waves x 32 queries (prescaled Q and dO fragments in registers), key tiles of 64 rows;
-// also forms the queries' row constants (as attn_bwd_dq_v2_kernel<true, true>) and writes them
-// negated for the dK/dV kernel. The pipeline runs over the full key tiles; a ragged last tile
-// (keys past N masked) goes through dq_tile afterwards.
-template <int W>
-__global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v3_kernel(const bf16* __restrict__ qkv,
-                                                                const bf16* __restrict__ dout,
-                                                                float* __restrict__ nlse2p,
-                                                                float* __restrict__ ndeltap, int N, int Npad, int H,
-                                                                bf16* __restrict__ dqkv, float scale,
-                                                                const bf16* __restrict__ out,
-                                                                const float* __restrict__ lse) {
-  __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][K|V]
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int2 bid = attn_block_id();
-  const int z = bid.y, b = z / H, h = z - b * H;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
-  constexpr int PW = 8 / W;
-  const int q = bid.x * (32 * W) + wv * 32 + (lane & 31);
-  const bool qv = q < N;
-  bf16x8 qf[4], gf[4];
-  load_row_frags(Qb + (long)q * ld, qv, lane, qf);
-  load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
-  float lse2, dlt;
-  {
-    bf16x8 of[4];
-    load_row_frags(out + ((long)b * N + q) * D + h * 64, qv, lane, of);
-    float d = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d = fmaf((float)of[i][e], (float)gf[i][e], d);
-    d = half_swap_sum(d);  // the other 32 of the 64 dims sit in lane ^ 32
-    lse2 = qv ? lse[(long)z * N + q] * LOG2E : 1e30f;
-    dlt = qv ? d : 0.f;
-    if (hl == 0 && q < Npad) {
-      nlse2p[(long)z * Npad + q] = -lse2;
-      ndeltap[(long)z * Npad + q] = -dlt;
-    }
-  }
-  f32x16 a0 = zero16(), a1 = zero16();
-  f32x16 nl, nd;  // S' and dP chains start from -lse2 / -delta (the query is the lane)
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    nl[r] = -lse2;
-    nd[r] = -dlt;
-  }
-  const int nt = (N + AK - 1) / AK, nfull = N / AK;
-  unsigned off[PW];
-#pragma unroll
-  for (int i = 0; i < PW; ++i) off[i] = 2u * dma_off<W>(i, wv, lane, ld);
-  auto issue = [&](int kt, int S) {  // as the dK/dV kernel; keys past N are masked in dq_tile
-    char* kimg = smem[S][0];
-    char* vimg = smem[S][1];
-    const char* kb = uniform_ptr(Kb + (long)kt * AK * ld);
-    const char* vb = uniform_ptr(Vb + (long)kt * AK * ld);
-#pragma unroll
-    for (int i = 0; i < PW; ++i) {
-      const int piece = wv * PW + i;
-      unsigned o = off[i];
-      if (kt >= nfull) {
-        const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ swz128(row);
-        o = 2u * (unsigned)((min(kt * AK + row, N - 1) - kt * AK) * ld + c * 8);
-      }
-      glds_s<false>(o, kb, kimg + piece * 1024);
-      glds_s<false>(o, vb, vimg + piece * 1024);
-    }
-  };
-  issue(0, 0);
-  if (nt > 1) issue(1, 1);
-  {
-    uint4* z2 = (uint4*)&smem[2][0][0];
-    for (int i = tid; i < 2 * 8192 / 16; i += 64 * W) z2[i] = make_uint4(0, 0, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  if (nfull > 0) {
-    bf16x8 ka[4], va[4];
-    f32x16 sc, dc;
-    bf16x8 pdq[2];
-    bf16x8 tk0[2], tk1[2];
-    auto read_a = [&](const char* kimg, const char* vimg, int t, int ks) {
-      ka[ks] = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-      va[ks] = *(const bf16x8*)(vimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-    };
-    auto e_step = [&](int i) {
-      const float p0 = fast_exp2(sc[2 * i]), p1 = fast_exp2(sc[2 * i + 1]);
-      uint4 u = __builtin_bit_cast(uint4, pdq[i >> 2]);
-      const unsigned w = pk_bf16(p0 * dc[2 * i], p1 * dc[2 * i + 1]);
-      switch (i & 3) {
-        case 0: u.x = w; break;
-        case 1: u.y = w; break;
-        case 2: u.z = w; break;
-        default: u.w = w; break;
-      }
-      pdq[i >> 2] = __builtin_bit_cast(bf16x8, u);
-    };
-    auto read_b = [&](const char* kimg, int t, int ss) {
-      const int rb = 32 * t + 16 * ss;
-      tk0[ss] = tr_acc_order(kimg, rb, 0, lane);
-      tk1[ss] = tr_acc_order(kimg, rb, 32, lane);
-    };
-    auto body = [&](auto sa, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
-      constexpr int SB = decltype(sb)::value, TB = decltype(tb)::value;
-      constexpr int SN = decltype(sn_)::value, TN = decltype(tn)::value;
-      constexpr bool BAR = decltype(bar)::value;
-      (void)sa;
-      f32x16 s = nl, dp = nd;
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        const int ks = g >> 1;
-        if ((g & 1) == 0) s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[ks], qf[ks], s, 0, 0, 0);
-        else dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[ks], gf[ks], dp, 0, 0, 0);
-        e_step(g);
-        if (g == 2) read_b(smem[SB][0], TB, 0);
-        if (g == 5) read_b(smem[SB][0], TB, 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (BAR) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (jn < nt) issue(jn, jn % BNS);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int ss = g >> 1;
-        if ((g & 1) == 0) a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pdq[ss], tk0[ss], a0, 0, 0, 0);
-        else a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pdq[ss], tk1[ss], a1, 0, 0, 0);
-        if (more) read_a(smem[SN][0], smem[SN][1], TN, g);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      sc = s;
-      dc = dp;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using F = std::false_type;
-    using T = std::true_type;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) read_a(smem[0][0], smem[0][1], 0, ks);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sc[r] = NEG_BIG;
-      dc[r] = 0.f;
-    }
-    auto tile = [&](auto s, int j) {
-      constexpr int S = decltype(s)::value;
-      using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
-      using SNX = std::integral_constant<int, (S + 1) % BNS>;
-      using SC = std::integral_constant<int, S>;
-      body(SC{}, SP{}, I1{}, SC{}, I1{}, F{}, 0, true);
-      body(SC{}, SC{}, I0{}, SNX{}, I0{}, T{}, j + 2, j + 1 < nfull);
-    };
-    int j = 0;
-    for (; j + 3 <= nfull; j += 3) {
-      tile(I0{}, j);
-      tile(I1{}, j + 1);
-      tile(I2{}, j + 2);
-    }
-    if (j < nfull) tile(I0{}, j);
-    if (j + 1 < nfull) tile(I1{}, j + 1);
-    const int S = (nfull - 1) % BNS;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) e_step(i);
-    read_b(smem[S][0], 1, 0);
-    read_b(smem[S][0], 1, 1);
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pdq[ss], tk0[ss], a0, 0, 0, 0);
-      a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pdq[ss], tk1[ss], a1, 0, 0, 0);
-    }
-  }
-  if (nt > nfull) {  // ragged last key tile (DMA issued one tile ahead, or in the prologue)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const int S = nfull % BNS;
-    dq_tile<true, true>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, nfull * AK, N, 1.0f, lane, nl);
-  }
-  const int qw = bid.x * (32 * W) + wv * 32;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int qq = qw + (r & 3) + 8 * (r >> 2) + 4 * hl;
-    if (qq < N) {
-      bf16* row = dqkv + ((long)b * N + qq) * ld + h * 64;
-      row[lane & 31] = (bf16)(a0[r] * scale);
-      row[32 + (lane & 31)] = (bf16)(a1[r] * scale);
-    }
-  }
 }
 
 // ------------------------------------------------------------------------- dQ v4 (16x16x32)
@@ -2066,13 +1404,10 @@ extern "C" int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh
   (void)work_bytes;
   if (B * N * H == 0) return 0;
   dim3 g(ivit_cdiv(N, 128), B * H);
-  const char* f16 = getenv("IVIT_ATTN_FWD16");  // A/B switch: the 16x16x32 forward (read per launch)
-  if (f16 && atoi(f16) == 1)
-    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v7_kernel<4, false>, g, dim3(256), ivit_stream(stream),
-              (const bf16*)qkv, (int)N, (int)H, (bf16*)out, lse, 1.0f);
-  else
-    kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream),
-              (const bf16*)qkv, (int)N, (int)H, (bf16*)out, lse, 1.0f);
+  // (a 16x16x32 form of this kernel measured slower: 0.295-0.302 vs 0.281-0.283 ms isolated, 43.65-43.88
+  // vs 42.77-42.83 ms per step, profiles/r05_d_attn_fwd16_ab.txt; removed)
+  kt_launch(IVIT_KT_ATTN_FWD, attn_fwd_bf16_v6_kernel<4, false>, g, dim3(256), ivit_stream(stream), (const bf16*)qkv,
+            (int)N, (int)H, (bf16*)out, lse, 1.0f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
@@ -2095,25 +1430,13 @@ extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* do
   // independent workgroup to fill its gaps)
   constexpr int BW = 4;
   const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
-  // dQ: the 16x16x32 form (v4) by default — isolated 0.332-0.334 -> 0.316 ms, same call
-  // (profiles/r05_c_attn_dq16_ab.txt); IVIT_ATTN_DQ16=0 restores v3 (A/B, read per launch)
-  const char* dq16e = getenv("IVIT_ATTN_DQ16");
-  if (!(dq16e && atoi(dq16e) == 0))
-    kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
-  else
-    kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
-  // dK/dV: the 16x16x32 form (v4) by default — isolated 0.441-0.445 -> 0.406 ms, same call
-  // (profiles/r05_b_attn_dkv16_ab.txt); IVIT_ATTN_DKV16=0 restores v3 (A/B, read per launch)
-  const char* dv16 = getenv("IVIT_ATTN_DKV16");
-  const bool dkv16 = !(dv16 && atoi(dv16) == 0);
-  if (dkv16)
-    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
-  else
-    kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v3_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-              (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
+  // the 16x16x32 forms (v4). Same-call A/B against the 32x32x16 v3 kernels they replaced (removed):
+  // dK/dV 0.441-0.445 -> 0.406 ms, dQ 0.332-0.334 -> 0.316 ms isolated, step 44.07-44.14 -> 43.29 ms
+  // with dK/dV alone (profiles/r05_b_attn_dkv16_ab.txt, r05_c_attn_dq16_ab.txt, r05_c_ab_dkv16_*.json)
+  kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
+  kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
