@@ -499,12 +499,16 @@ def test_patch_embed_fused_exact(B, C, H, W, D):
 
 
 @pytest.mark.parametrize("B,C,H,W", [(2, 9, 32, 48), (3, 290, 24, 40), (2, 4, 400, 720), (1, 3, 16, 16),
-                                     (2, 290, 64, 128), (1, 290, 160, 200)])
+                                     (2, 290, 64, 128), (1, 290, 160, 200), (2, 7, 264, 264), (1, 64, 256, 256),
+                                     (3, 33, 200, 360), (2, 65, 256, 264), (1, 290, 400, 720)])
 def test_patch_wgrad_raster_exact(B, C, H, W):
     """bf16 weight gradient straight from the raster (ivit_patch_embed_wgrad, D = 384: the
-    persistent channel-pair kernel + slab reduction) vs the same products in f64: odd channel
-    counts, 32-patch chunks crossing images, workgroups spanning two / several channel pairs, tiny
-    grids with idle workgroups; dbias / dpos / dcls as before."""
+    persistent channel-pair kernels + slab reduction) vs the same products in f64: odd channel
+    counts, 32-patch chunks crossing images and patch rows, workgroups spanning two / several
+    channel pairs, tiny grids with idle workgroups; dbias / dpos / dcls as before. Patch grids at
+    least 32 wide run the wave-specialised kernel — with >= 32 channel pairs and >= 64 chunks
+    (the last two shapes: 33 pairs with an odd last channel, and one LiDAR frame) on the
+    XCD-sharded schedule — narrower ones the all-waves form."""
     from _lib import BF16, lib, ptr, stream
     D = 384
     g = torch.Generator().manual_seed(7 * C + B)

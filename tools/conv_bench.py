@@ -2,7 +2,7 @@
 288 x 256 panel kernel (conv_panel.hip) and the 128 x 128 engine (IVIT_CONV_PANEL=0), alternating
 in one process; HIP events around 20 back-to-back launches.
 
-    python tools/conv_bench.py
+    python tools/conv_bench.py [--panel-only]   (--panel-only: the fusion shapes on the panel kernels)
 """
 import os
 import sys
@@ -26,6 +26,7 @@ def timed(fn, reps=20):
 
 
 def main():
+    panel_only = "--panel-only" in sys.argv
     import ops
     from _lib import BF16
     dev = torch.device("cuda", 0)
@@ -38,7 +39,7 @@ def main():
         wp = ops.pack_conv(w, BF16)
         fl = 2.0 * M * cout * cin * k * k
         for rep in range(2):
-            for mode in ("1", "0"):
+            for mode in (("1",) if panel_only else ("1", "0")):
                 os.environ["IVIT_CONV_PANEL"] = mode
                 tf = timed(lambda: ops.conv_fwd(x, B, H, W, wp, None, BF16, torch.float32))
                 td = timed(lambda: ops.conv_dgrad(dy, B, H, W, wp, BF16, torch.float32, w=w))
@@ -48,6 +49,8 @@ def main():
                       f"dgrad(+pack) {td:7.1f} us ({fl / td / 1e6:6.1f} TF/s)  "
                       f"wgrad(+reduce) {tw:7.1f} us ({fl / tw / 1e6:6.1f} TF/s)", flush=True)
     os.environ["IVIT_CONV_PANEL"] = "1"
+    if panel_only:
+        return
     # head conv data gradient (75 channels packed to 80): engine vs the panel kernel on rows zero-padded to 128
     cin, cw, cp, cq = 512, 75, 80, 128
     w = torch.randn(cw, cin, 3, 3, device=dev) / (cin * 9) ** 0.5

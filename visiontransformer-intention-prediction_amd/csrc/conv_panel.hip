@@ -36,6 +36,14 @@ constexpr int CP_PBW = CP_PB / CP_W;                        // 4 B pieces per wa
 static_assert(CP_PB % CP_W == 0 && CP_PAX > 0, "piece split");
 
 __device__ __attribute__((aligned(16))) uint4 cp_zero16[4];
+#ifndef CP_ILV
+#define CP_ILV 0
+#endif
+// anatomy builds (tools/ab_build.sh -DCP_ANAT=1 / 2; timing only, wrong results): 1 no fragment reads
+// or MFMAs (the DMA / barrier skeleton), 2 no DMA after the first K tile (MFMAs on stale stages)
+#ifndef CP_ANAT
+#define CP_ANAT 0
+#endif
 
 // 128-B image rows (64 k), 16-B chunk c of row r at chunk c ^ ((r >> 1) & 7): the 16x16x32 operand
 // reads (rows r0 .. r0+15, chunks 4t .. 4t+3) hit 16 distinct bank quads per ds_read_b128 lane group.
@@ -84,30 +92,44 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
     const int n = min(n0 + row, p.N - 1);
     boff[i] = 2u * (unsigned)(n * p.K + c * 8);
   }
-  auto issue = [&](int kt, int s) {
-    char* sa = smem + s * CP_STAGE;
-    char* sb = sa + CP_SA;
-    // K order: channel tile major, the k*k taps inside it (Cin % 64 == 0: a K tile is one tap), so
-    // the k*k shifted reads of a 64-channel slab of the pixel panel follow each other and all but
-    // the first hit the XCD's L2 (tap-major order streamed the whole panel once per tap: 9x the
-    // Infinity-Cache traffic for a 3x3 conv)
+  // K order: channel tile major, the k*k taps inside it (Cin % 64 == 0: a K tile is one tap), so
+  // the k*k shifted reads of a 64-channel slab of the pixel panel follow each other and all but
+  // the first hit the XCD's L2 (tap-major order streamed the whole panel once per tap: 9x the
+  // Infinity-Cache traffic for a 3x3 conv)
+  struct Tile { long shift; const char* bsb; int dy, dx; };
+  auto tile_of = [&](int kt) {
     const int nt = p.ks * p.ks, ct = kt / nt, tap = kt - ct * nt, ci0 = ct * 64;
     const int k0 = tap * p.Cin + ci0;  // the weight's K offset ([N][k][k][Cin] packing)
     const int ky = tap / p.ks, kx = tap - ky * p.ks;
-    const int dy = ky - pad, dx = kx - pad;
-    const long shift = (long)(dy * p.W + dx) * p.lda + ci0;
-#pragma unroll
-    for (int i = 0; i < CP_PAW; ++i) {
-      if (i < npa) {
-        const int yy = (ayx[i] >> 16) + dy, xx = (ayx[i] & 0xffff) + dx;
+    Tile t;
+    t.dy = ky - pad;
+    t.dx = kx - pad;
+    t.shift = (long)(t.dy * p.W + t.dx) * p.lda + ci0;
+    t.bsb = uniform_ptr(p.Bk + k0);
+    return t;
+  };
+  // the zero page's address once, in SGPRs (re-deriving it per piece is a GOT scalar load whose
+  // lgkmcnt(0) wait would also drain the fragment reads in flight)
+  const char* zpage = (const char*)cp_zero16;
+  asm volatile("" : "+s"(zpage));
+  // piece q of a K tile: q < CP_PAW the wave's A (map) piece q, else its B (weight) piece q - CP_PAW
+  auto issue_piece = [&](const Tile& t, int s, int q) {
+    char* sa = smem + s * CP_STAGE;
+    if (q < CP_PAW) {
+      if (q < npa) {
+        const int yy = (ayx[q] >> 16) + t.dy, xx = (ayx[q] & 0xffff) + t.dx;
         const bool ok = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-        const void* src = ok ? (const void*)(p.A + (shift + abase[i])) : (const void*)cp_zero16;
-        glds_v<false>(src, sa + (wv + CP_W * i) * 1024);
+        const void* src = ok ? (const void*)(p.A + (t.shift + abase[q])) : (const void*)zpage;
+        glds_v<false>(src, sa + (wv + CP_W * q) * 1024);
       }
+    } else {
+      glds_s<false>(boff[q - CP_PAW], t.bsb, sa + CP_SA + (wv + CP_W * (q - CP_PAW)) * 1024);
     }
-    const char* bsb = uniform_ptr(p.Bk + k0);
+  };
+  auto issue = [&](int kt, int s) {
+    const Tile t = tile_of(kt);
 #pragma unroll
-    for (int i = 0; i < CP_PBW; ++i) glds_s<false>(boff[i], bsb, sb + (wv + CP_W * i) * 1024);
+    for (int q = 0; q < CP_PAW + CP_PBW; ++q) issue_piece(t, s, q);
   };
 
   f32x4 acc[CP_MB][CP_NB];
@@ -124,7 +146,14 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
     // wave is done reading stage cur ^ 1 (tile kt-1), which tile kt+1 then refills
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const bool more = kt + 1 < nk;
+    Tile tn1;
+    if (CP_ILV) {
+      if (more) tn1 = tile_of(kt + 1);
+    } else if (more && CP_ANAT != 2) {
+      issue(kt + 1, cur ^ 1);
+    }
+    if (CP_ANAT == 1) continue;
     const char* ia = smem + cur * CP_STAGE;
     const char* ib = ia + CP_SA;
     bf16x8 bfr[2][CP_NB];
@@ -149,6 +178,9 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
 #pragma unroll
       for (int j = 0; j < CP_NB; ++j)
         acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[t][j], fr[f % 4], acc[mb][j], 0, 0, 0);
+      // CP_ILV: the next tile's pieces one per MFMA group (from the second on) instead of a burst
+      // before the first
+      if (CP_ILV && more && f >= 1 && f - 1 < CP_PAW + CP_PBW) issue_piece(tn1, cur ^ 1, f - 1);
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of this stage are done

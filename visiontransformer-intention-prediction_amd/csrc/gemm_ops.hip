@@ -470,8 +470,8 @@ extern "C" long ivit_patch_embed_wgrad_workspace(long B, long C, long H, long W,
   const long s2 = wgrad_splits(D, C * 64, B * Np, true);
   if (s2 > s) s = s2;
   long main = s * D * C * 64 * 4;
-  if (patch_wgrad_raster_ok(B, C, H, W, D) && patch_wgrad_raster_workspace2(C, D) > main)
-    main = patch_wgrad_raster_workspace2(C, D);
+  if (patch_wgrad_raster_ok(B, C, H, W, D) && patch_wgrad_raster_workspace2(B, C, H, W, D) > main)
+    main = patch_wgrad_raster_workspace2(B, C, H, W, D);
   return main + ivit_colsum_workspace(B * Np, D);
 }
 
@@ -500,7 +500,7 @@ extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* 
   const int splits = (int)wgrad_splits(D, C * 64, B * Np, bf);
   long cw_off = (long)splits * n * 4;  // colsum workspace after the slab
   if (bf && patch_wgrad_raster_ok(B, C, H, W, D)) {  // raster read once (patch_embed.hip)
-    cw_off = patch_wgrad_raster_workspace2(C, D);
+    cw_off = patch_wgrad_raster_workspace2(B, C, H, W, D);
     int rc = patch_wgrad_raster((const bf16*)dtok, img, B, C, H, W, D, dW, accumulate, work, st);
     if (rc) return rc;
     IVIT_LAUNCH_CHECK();

@@ -237,18 +237,20 @@ __global__ __launch_bounds__(256) void colreduce_kernel(const float* __restrict_
   const int c = blockIdx.x * CR_COLS + cl;
   float s = 0.f;
   if (c < C) {
-    // the first 16 rows of this phase loaded at once (16 loads in flight per lane: the reduce is
-    // latency-bound), summed in the same order as the sequential loop
-    float v[16];
+    // this phase's rows in batches of 16 loads in flight per lane (the reduce is latency-bound: a
+    // serial tail of one load per add took ~19 L2 round trips at nb = 563), each batch summed in
+    // row order, so the result is the plain sequential sum over the phase's rows
+    for (int b0 = ph; b0 < nb; b0 += 256) {
+      float v[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int b = ph + 16 * i;
-      v[i] = b < nb ? part[(long)b * pstride + c] : 0.f;
+      for (int i = 0; i < 16; ++i) {
+        const int b = b0 + 16 * i;
+        v[i] = b < nb ? part[(long)b * pstride + c] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (b0 + 16 * i < nb) s += v[i];
     }
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (ph + 16 * i < nb) s += v[i];
-    for (int b = ph + 256; b < nb; b += 16) s += part[(long)b * pstride + c];
   }
   __shared__ float red[16][CR_COLS];
   red[ph][cl] = s;

@@ -7,7 +7,7 @@ namespace ivit {
 // dW [D][C*64] (+)= sum over patches of dtok (token rows, CLS skipped) x patch(raster).
 bool patch_wgrad_raster_ok(long B, long C, long H, long W, long D);
 long patch_wgrad_raster_workspace(long D);
-long patch_wgrad_raster_workspace2(long C, long D);  // covers both forms (split and persistent)
+long patch_wgrad_raster_workspace2(long B, long C, long H, long W, long D);  // every schedule of the shape
 int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long H, long W, long D, float* dW,
                        int accumulate, void* work, hipStream_t st);
 }  // namespace ivit

@@ -578,6 +578,275 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
   }
 }
 
+// The wave-specialised form of patch_wgrad_kernel (same units, slab layout and sums): waves 0-3
+// only compute, waves 4-7 only load. patch_wgrad_kernel's eight waves each issue their unit's
+// LDS-DMA pieces, convert their raster pieces and compute, behind one barrier per unit, and the
+// unit cadence (~1.6 us per 40 KiB unit per CU, 25 GB/s of intake) was its bound, not either
+// operand's source. Here:
+//   * a compute wave owns 96 output rows (n) x the pair's 128 columns (k): 3 x 4 blocks of
+//     v_mfma_f32_32x32x16_bf16 (192 accumulator VGPRs), one wave per SIMD, 7 fragment reads
+//     (14 transposing LDS reads) per 12 MFMAs;
+//   * a loader wave fetches its share of a unit's token-gradient rows by LDS-DMA (6 of the 24
+//     1-KiB pieces) three units ahead, and its raster pieces (one channel of the pair, 4 of the 8
+//     ky rows: 4 x 16 B per lane) into VGPRs four units ahead, converts them to bf16 and writes
+//     the unit's X image itself just before the barrier that publishes the unit — the f32 raster
+//     never passes through LDS;
+//   * LDS: 4 token-gradient stages (24 KiB) + 2 X images (8 KiB) = 112 KiB.
+// Issue order per loader wave (vmcnt retires in issue order): R(0) T(0) R(1) T(1) R(2) T(2) R(3),
+// then iteration k issues T(k+3) R(k+4); before the barrier of unit i, R(i) and T(i) must have
+// landed: vmcnt = the ops issued after T(i) (R(i+1) and iterations i-2, i-1).
+#ifndef IVIT_PW_WS
+#define IVIT_PW_WS 1
+#endif
+// anatomy builds (tools/ab_build.sh -DPW_ANAT=n; timing only, wrong results): 1 no MFMAs, 2 no raster
+// loads, 3 no token-gradient DMA, 4 neither load, 5 every unit's token-gradient rows from chunk 0
+#ifndef PW_ANAT
+#define PW_ANAT 0
+#endif
+constexpr int PW_NT = 4;  // token-gradient LDS stages
+constexpr int PW_RR = 4;  // raster register sets (units in flight)
+template <int SLOT>
+using pw_slot = std::integral_constant<int, SLOT>;
+
+// Schedules. P == 0, linear: as patch_wgrad_kernel (workgroup w takes the g-major unit range
+// [u0, u1), at most two pairs; slab [w][2][D][128]). P > 0, XCD-sharded: workgroup b runs on XCD
+// x = b % 8 (round-robin dispatch) as its s = b / 8-th workgroup, and takes pairs s, s + P, ... over
+// the XCD's chunk range [x J / 8, (x+1) J / 8); the P workgroups of an XCD move through the same
+// chunks together, so each token-gradient chunk comes from HBM / Infinity Cache once per XCD and
+// from its L2 for the other pairs (the full-grid token gradient re-read per pair was 4 GB of the
+// 6.9 GB a LiDAR launch fetched; with every unit reading one L2-resident chunk the kernel took
+// 0.66 vs 0.95 ms). Slab [x][G][D][128], reduced over x by patch_wgrad_xreduce_kernel.
+__global__ __launch_bounds__(512, 1) void patch_wgrad_ws_kernel(const bf16* __restrict__ dtok,
+                                                              const float* __restrict__ img, int C, int H, int W,
+                                                              int Wp, int Np, int M, int J, int P,
+                                                              float* __restrict__ slab) {
+  constexpr int D = 384, NT = 3;
+  constexpr int TST = NT * WG_TIMG;  // 24 KiB
+  __shared__ __attribute__((aligned(16))) char smem[PW_NT * TST + 2 * WG_XST];
+  char* const treg = smem;
+  char* const ximg = smem + PW_NT * TST;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = (C + 1) / 2;
+  const int w = blockIdx.x;
+  int g0, j0, nu, jb, je, gstep;
+  long slot0;  // slab slot (of D x 128 floats) of pair g0; pair g's is slot0 + (g - g0) / gstep
+  if (P == 0) {
+    const long U = (long)G * J;
+    const long u0 = wg_unit_start(w, U), u1 = wg_unit_start(w + 1, U);
+    nu = (int)(u1 - u0);
+    g0 = (int)(u0 / J);
+    j0 = (int)(u0 - (long)g0 * J);
+    jb = 0;
+    je = J;
+    gstep = 1;
+    slot0 = (long)w * 2;
+  } else {
+    const int x = w & 7, sx = w >> 3;
+    jb = x * J / 8;
+    je = (x + 1) * J / 8;
+    g0 = sx;
+    j0 = jb;
+    gstep = P;
+    nu = (g0 < G ? (G - 1 - g0) / P + 1 : 0) * (je - jb);
+    slot0 = (long)x * G + g0;
+  }
+  if (nu <= 0) return;
+  const int Hp = H / 8;
+  struct Cur { int g, j; };
+  auto cnext = [&](Cur& c) { if (++c.j == je) { c.j = jb; c.g += gstep; } };
+  // slab slot of pair g: w * 2 + (g - g0) (linear), x * G + g (sharded)
+  auto slot_of = [&](int g) { return slot0 + (g - g0); };
+
+  if (wv >= 4) {  // ------------------------------------------------------------------- loader
+    // Addressing is wave-uniform chunk cursors (scalar) + per-lane constants: a 32-patch chunk
+    // meets at most two images and two patch rows (the host launches this form for Wp >= 32 only),
+    // so a lane's position is the chunk's plus one conditional wrap.
+    const int lw = wv - 4;
+    const int cl = lw >> 1, ky0 = (lw & 1) * 4;  // raster: channel cl of the pair, ky rows ky0 .. +3
+    const int pl = lane >> 1, half = lane & 1;   // raster lane: patch pl of the chunk, 16-B half
+    const long HWl = (long)H * W;
+    const unsigned chw4 = (unsigned)(C * HWl * 4);  // one image of the raster, bytes (host: < 2^32)
+    const unsigned row4 = (unsigned)W * 4;
+    // token-gradient pieces 6 lw .. 6 lw + 5 (image ti = piece >> 3, rows 4 (piece & 7) + lane >> 4);
+    // a lane's 16-B chunk of its 256-B row segment is the same in every piece
+    constexpr int TPL = 6;
+    const unsigned tcol = (unsigned)(((lane & 15) ^ ((lane >> 4) << 2)) * 16);
+    const int tok_last = (M - 1) + (M - 1) / Np + 1;  // token row of patch M - 1 (rows past M clamp)
+    const char* dsb = uniform_ptr(dtok);
+    // X image byte offsets of the lane's four (cl, ky0 + i) chunks in row pl
+    int xoff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xoff[i] = wg_mn_off(pl, cl * 8 + ky0 + i) + half * 8;
+    u32x4 rr[PW_RR][4];
+
+    // chunk cursors (all wave-uniform): unit (g, j); its first patch at image b, in-image patch p,
+    // patch row gy, column gx
+    struct Ch { int g, j, b, p, gy, gx; };
+    auto ch_at = [&](int g, int j) {
+      Ch c;
+      c.g = g;
+      c.j = j;
+      const int m = j * WG_MU;
+      c.b = m / Np;
+      c.p = m - c.b * Np;
+      c.gy = c.p / Wp;
+      c.gx = c.p - c.gy * Wp;
+      return c;
+    };
+    auto ch_next = [&](Ch& c) {
+      if (++c.j == je) {
+        c = ch_at(c.g + gstep, jb);
+        return;
+      }
+      c.p += WG_MU;
+      if (c.p >= Np) { c.p -= Np; ++c.b; }
+      c.gx += WG_MU;
+      if (c.gx >= Wp) { c.gx -= Wp; if (++c.gy == Hp) { c.gy = 0; } }
+    };
+    Ch cr = ch_at(g0, j0), ct = cr;
+    Cur cc{g0, j0};
+
+    auto issue_t = [&](int k) {
+      char* st = treg + (k % PW_NT) * TST;
+      const int tbase = ct.b * (Np + 1) + 1;
+#pragma unroll
+      for (int i = 0; i < TPL; ++i) {
+        const int piece = lw * TPL + i, ti = piece >> 3, row = (piece & 7) * 4 + (lane >> 4);
+        const int p = ct.p + row;
+        int tok = tbase + p + (p >= Np ? 1 : 0);
+        tok = ct.j * WG_MU + row < M ? tok : tok_last;
+        if (PW_ANAT == 5) tok = 1 + row;  // diagnostic: every unit reads chunk 0 (L2-resident)
+        if (PW_ANAT != 3 && PW_ANAT != 4)
+          glds_s<false>((unsigned)tok * (unsigned)(D * 2) + (unsigned)(ti * 256) + tcol, dsb,
+                        st + ti * WG_TIMG + (piece & 7) * 1024);
+      }
+      ch_next(ct);
+    };
+    // the raster cursor's unit into register set SLOT (4 x 16 B per lane, streamed: nt)
+    auto issue_r = [&](auto slot) {
+      constexpr int S = decltype(slot)::value;
+      const int c = min(2 * cr.g + cl, C - 1);  // a missing odd channel is zeroed in convert
+      const char* sb = uniform_ptr(img + ((long)cr.b * C + c) * HWl + (long)ky0 * W);
+      int gx = cr.gx + pl, gy = cr.gy;
+      unsigned ib = 0;
+      if (gx >= Wp) {
+        gx -= Wp;
+        if (++gy == Hp) { gy = 0; ib = chw4; }
+      }
+      unsigned vo = ib + (unsigned)(gy * 8) * row4 + (unsigned)(gx * 32 + half * 16);
+      vo = cr.j * WG_MU + pl < M ? vo : 0u;  // past M: any valid address (zeroed in convert)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (PW_ANAT != 2 && PW_ANAT != 4)
+          asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=v"(rr[S][i]) : "v"(vo), "s"(sb) : "memory");
+        vo += row4;
+      }
+      ch_next(cr);
+    };
+    // register set SLOT (landed) -> X image k & 1: lane's 4 kx of (cl, ky, patch) -> 8 bytes of
+    // chunk cl * 8 + ky of row = patch; zero past M / C
+    auto convert = [&](auto slot, int k) {
+      constexpr int S = decltype(slot)::value;
+      char* xi = ximg + (k & 1) * WG_XST;
+      const bool ok = cc.j * WG_MU + pl < M && 2 * cc.g + cl < C;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        asm volatile("" : "+v"(rr[S][i]));  // after the counted wait
+        const float4 v = __builtin_bit_cast(float4, rr[S][i]);
+        const uint2 val = ok ? make_uint2(pk_bf16(v.x, v.y), pk_bf16(v.z, v.w)) : make_uint2(0u, 0u);
+        *(uint2*)(xi + xoff[i]) = val;
+      }
+      cnext(cc);
+    };
+    // prologue: R(0) T(0) R(1) T(1) R(2) T(2) R(3)
+    issue_r(pw_slot<0>{});
+    issue_t(0);
+    if (nu > 1) issue_r(pw_slot<1>{});
+    if (nu > 1) issue_t(1);
+    if (nu > 2) issue_r(pw_slot<2>{});
+    if (nu > 2) issue_t(2);
+    if (nu > 3) issue_r(pw_slot<3>{});
+    // one unit of the loader's loop with register set SLOT = i % 4
+    auto step = [&](auto slot, int i) {
+      if (i >= 2 && i + 4 < nu) {  // steady state: R(i+1) and iterations i-2, i-1 issued after T(i)
+        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      } else {
+        int after = i + 1 < nu ? 4 : 0;
+#pragma unroll
+        for (int k = i - 2; k < i; ++k) after += (k + 3 < nu ? 6 : 0) + (k + 4 < nu ? 4 : 0);
+        wait_vm(after);
+      }
+      convert(slot, i);
+      lds_barrier();  // publishes X(i) (own ds_writes) and, with every loader's wait, T(i)
+      if (i + 3 < nu) issue_t(i + 3);
+      if (i + 4 < nu) issue_r(slot);  // (i + 4) % 4 == i % 4: the set converted just now
+    };
+    for (int i = 0; i < nu; i += 4) {
+      step(pw_slot<0>{}, i);
+      if (i + 1 < nu) step(pw_slot<1>{}, i + 1);
+      if (i + 2 < nu) step(pw_slot<2>{}, i + 2);
+      if (i + 3 < nu) step(pw_slot<3>{}, i + 3);
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------------------------ compute
+  const int nb0 = wv * 3;  // 32-row n blocks nb0 .. nb0 + 2
+  f32x16 acc[3][4];
+  auto zero = [&]() {
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[a][j][r] = 0.f;
+  };
+  auto flush = [&](int g) {
+    // the lane's offset laundered here, so that the 192 store addresses are formed at the flush
+    // and not hoisted out of the unit loop (they spilled: 272 B of scratch)
+    int lo = 4 * (lane >> 5) * 128 + (lane & 31);
+    asm volatile("" : "+v"(lo));
+    float* o = slab + slot_of(g) * D * 128 + nb0 * 32 * 128 + lo;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[(a * 32 + (r & 3) + 8 * (r >> 2)) * 128 + j * 32] = acc[a][j][r];
+  };
+  zero();
+  Cur cm{g0, j0};
+  for (int i = 0; i < nu; ++i) {
+    __builtin_amdgcn_s_barrier();
+    const char* ti = treg + (i % PW_NT) * TST;
+    const char* xi = ximg + (i & 1) * WG_XST;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x8 fa[3], fb[4];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int nb = nb0 + a;
+        fa[a] = wg_frag(ti + (nb >> 2) * WG_TIMG, 16 * t, (nb & 3) * 32, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = wg_frag(xi, 16 * t, j * 32, lane);
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (PW_ANAT != 1) acc[a][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[j], acc[a][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of this unit are done
+    const int g = cm.g;
+    cnext(cm);
+    if (i + 1 == nu || cm.g != g) {
+      flush(g);
+      zero();
+    }
+  }
+}
+
 // dW[n][g*128 + k] (+)= sum of the partial tiles of pair g (workgroups whose unit range meets it).
 // D * 128 is a multiple of the block's 256 V elements, so a block's pair g, and the range of
 // workgroups whose unit range meets it, are block-uniform (scalar; one 64-bit division per block,
@@ -640,12 +909,45 @@ __global__ __launch_bounds__(256) void patch_wgrad_reduce_kernel(const float* __
   }
 }
 
+// dW[n][g*128 + k] (+)= sum over the XCDs x (in order; those with a non-empty chunk range) of
+// slab[x][g][n][k] (the sharded schedule's partials), four consecutive k per thread.
+__global__ __launch_bounds__(256) void patch_wgrad_xreduce_kernel(const float* __restrict__ slab, int C, int J, int D,
+                                                                  float* __restrict__ dW, int accumulate) {
+  const int G = (C + 1) / 2;
+  const long per = (long)D * 128, e = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (e >= (long)G * per) return;
+  const int g = (int)(e / per), r = (int)(e - (long)g * per), n = r >> 7, k = r & 127;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    if ((x + 1) * J / 8 == x * J / 8) continue;
+    const float4 v = *(const float4*)(slab + ((long)x * G + g) * per + r);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  if (2 * g + (k >> 6) >= C) return;
+  float4* o = (float4*)(dW + (long)n * C * 64 + (long)g * 128 + k);
+  if (accumulate) {
+    const float4 t = *o;
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+  *o = s;
+}
+
 }  // namespace
 
 long patch_wgrad_raster_workspace(long D) { return (long)WG_NWG * 2 * D * 128 * 4; }
-long patch_wgrad_raster_workspace2(long C, long D) {
-  (void)C;
-  return patch_wgrad_raster_workspace(D);
+// the XCD-sharded schedule's workgroups per XCD (0: the linear schedule)
+int pw_shard_p(long C, long Wp, long J) {
+  const long G = (C + 1) / 2;
+  if (!IVIT_PW_WS || Wp < WG_MU || G < 32 || J < 64) return 0;
+  const long R = (G + 31) / 32;  // pairs per workgroup
+  return (int)((G + R - 1) / R);
+}
+long patch_wgrad_raster_workspace2(long B, long C, long H, long W, long D) {
+  const long Np = (H / 8) * (W / 8), J = (B * Np + WG_MU - 1) / WG_MU;
+  const long lin = patch_wgrad_raster_workspace(D);
+  const long sh = pw_shard_p(C, W / 8, J) ? 8 * ((C + 1) / 2) * D * 128 * 4 : 0;
+  return lin > sh ? lin : sh;
 }
 
 bool patch_wgrad_raster_ok(long B, long C, long H, long W, long D) {
@@ -667,8 +969,21 @@ int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long 
   // diagnostic builds with the dtok chunk fixed (L2-resident) 0.988 and the raster chunk fixed
   // 1.002 ms — neither operand's source bounds the kernel by itself.
   if ((D * 128) % 256) return IVIT_ERR_UNSUPPORTED;  // the reduce's block-uniform pair
-  hipLaunchKernelGGL((patch_wgrad_kernel<3, 2>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H, (int)W, Wp,
-                     Np, M, J, slab);
+  const int P = pw_shard_p(C, Wp, J);
+  if (P > 0 && (D * 128) % 4 == 0 && ((uintptr_t)dW & 15) == 0 && (C * 64) % 4 == 0) {
+    hipLaunchKernelGGL(patch_wgrad_ws_kernel, dim3(8 * P), dim3(512), 0, st, dtok, img, (int)C, (int)H, (int)W, Wp, Np,
+                       M, J, P, slab);
+    const long tot = (long)((C + 1) / 2) * D * 128;
+    hipLaunchKernelGGL(patch_wgrad_xreduce_kernel, dim3(ivit_cdiv(tot, 1024)), dim3(256), 0, st, slab, (int)C, J,
+                       (int)D, dW, accumulate);
+    return 0;
+  }
+  if (IVIT_PW_WS && Wp >= WG_MU)  // the wave-specialised form's lane positions need Wp >= 32
+    hipLaunchKernelGGL(patch_wgrad_ws_kernel, dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H, (int)W, Wp, Np,
+                       M, J, 0, slab);
+  else
+    hipLaunchKernelGGL((patch_wgrad_kernel<3, 2>), dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H, (int)W,
+                       Wp, Np, M, J, slab);
   if ((D * 128) % 1024 == 0 && ((uintptr_t)dW & 15) == 0 && (C * 64) % 4 == 0)
     hipLaunchKernelGGL(patch_wgrad_reduce_kernel<4>, dim3(ivit_cdiv(n, 1024)), dim3(256), 0, st, slab, (int)C, J,
                        (int)D, dW, accumulate);

@@ -54,7 +54,8 @@ struct WbArgs {
 // pieces the DMA and MFMA phases ran nearly serialised (anatomy: DMA skeleton 112 us + MFMA-only
 // 105 us -> 206 us together). Both roles pass exactly one barrier per step.
 // MODE (anatomy builds: -DIVIT_WB_ANATOMY=MODE via tools/ab_build.sh): 0 product, 1 no MFMAs (the DMA / barrier
-// skeleton), 2 no DMA after the prologue (MFMAs on stale stages).
+// skeleton), 2 no DMA after the prologue (MFMAs on stale stages), 3 the product kernel without the
+// reduce launch.
 constexpr int WB_CW = 8, WB_LW = 4;  // compute / loader waves
 #ifndef IVIT_WB_ANATOMY
 #define IVIT_WB_ANATOMY 0
@@ -309,6 +310,7 @@ extern "C" int ivit_vit_block_wgrad(long M, long D, long Hd, const void* dy2, co
   hipLaunchKernelGGL(wgrad_block_kernel<IVIT_WB_ANATOMY>, dim3(args.tile_base[4] * S), dim3(64 * (WB_CW + WB_LW)), 0,
                      st, args);
   IVIT_LAUNCH_CHECK();
+  if (IVIT_WB_ANATOMY == 3) return 0;  // anatomy 3: the product kernel without its reduce (timing only)
   hipLaunchKernelGGL(wgrad_block_reduce_kernel, dim3(ivit_cdiv((off + boff) / 4, 256)), dim3(256), 0, st, args.slab,
                      args.bslab, out, S);
   IVIT_LAUNCH_CHECK();
