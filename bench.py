@@ -55,7 +55,7 @@ def step_flops(B, H, W, depth=12, D=384, C_l=290, C_m=9, planes=512, A=5, K=8, a
 # launch on the launching stream) is reported beside it: it also counts time the kernel waited
 # behind the other ViT stream's kernels.
 ATTN = {
-    "attn_bwd": {"kernels": ["attn_bwd_dq_v3_kernel", "attn_bwd_dkv_v3_kernel"], "entry": "ivit_attn_bwd_q2",
+    "attn_bwd": {"kernels": ["attn_bwd_dq_v4_kernel", "attn_bwd_dkv_v4_kernel"], "entry": "ivit_attn_bwd_q2",
                  "tags": (1, 2),
                  "flops_note": "8*B*H*N^2*64 (dQ, dK, dV, dP products; the S recompute is not counted)"},
     "attn_fwd": {"kernels": ["attn_fwd_bf16_v6_kernel"], "entry": "ivit_attn_fwd_q2", "tags": (0,),

@@ -67,8 +67,8 @@ def test_intervals_file_reproduces_the_roofline_union(tmp_path):
     iv = _FakeOps.rec[1] + _FakeOps.rec[2]
     assert abs(sum(b - a for a, b in [(1.0, 2.4)]) - 1.4) < 1e-12 and len(iv) == 4
     out = tmp_path / "u.json"
-    subprocess.run([sys.executable, os.path.join(HERE, "..", "tools", "kunion.py"), str(path), "attn_bwd_dq_v3",
-                    "attn_bwd_dkv_v3", "--flops", "7e8", "--json", str(out)], check=True, capture_output=True)
+    subprocess.run([sys.executable, os.path.join(HERE, "..", "tools", "kunion.py"), str(path), "attn_bwd_dq_v4",
+                    "attn_bwd_dkv_v4", "--flops", "7e8", "--json", str(out)], check=True, capture_output=True)
     d = json.loads(out.read_text())
     assert d["source_kind"] == "bench_intervals" and d["launches"] == 2
     assert abs(d["union_us_per_launch"] - 700.0) < 1e-6
