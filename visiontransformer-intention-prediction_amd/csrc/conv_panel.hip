@@ -36,9 +36,6 @@ constexpr int CP_PBW = CP_PB / CP_W;                        // 4 B pieces per wa
 static_assert(CP_PB % CP_W == 0 && CP_PAX > 0, "piece split");
 
 __device__ __attribute__((aligned(16))) uint4 cp_zero16[4];
-#ifndef CP_ILV
-#define CP_ILV 0
-#endif
 // anatomy builds (tools/ab_build.sh -DCP_ANAT=1 / 2; timing only, wrong results): 1 no fragment reads
 // or MFMAs (the DMA / barrier skeleton), 2 no DMA after the first K tile (MFMAs on stale stages)
 #ifndef CP_ANAT
@@ -146,13 +143,9 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
     // wave is done reading stage cur ^ 1 (tile kt-1), which tile kt+1 then refills
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    const bool more = kt + 1 < nk;
-    Tile tn1;
-    if (CP_ILV) {
-      if (more) tn1 = tile_of(kt + 1);
-    } else if (more && CP_ANAT != 2) {
-      issue(kt + 1, cur ^ 1);
-    }
+    // (the pieces issued one per MFMA group instead of this burst: 136-137 vs 138-139 us at
+    // 512 -> 512, not kept)
+    if (kt + 1 < nk && CP_ANAT != 2) issue(kt + 1, cur ^ 1);
     if (CP_ANAT == 1) continue;
     const char* ia = smem + cur * CP_STAGE;
     const char* ib = ia + CP_SA;
@@ -178,9 +171,6 @@ __global__ __launch_bounds__(512, 1) void conv_panel_kernel(CpArgs p) {
 #pragma unroll
       for (int j = 0; j < CP_NB; ++j)
         acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[t][j], fr[f % 4], acc[mb][j], 0, 0, 0);
-      // CP_ILV: the next tile's pieces one per MFMA group (from the second on) instead of a burst
-      // before the first
-      if (CP_ILV && more && f >= 1 && f - 1 < CP_PAW + CP_PBW) issue_piece(tn1, cur ^ 1, f - 1);
       __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of this stage are done

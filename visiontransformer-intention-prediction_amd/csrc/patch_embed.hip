@@ -595,9 +595,6 @@ __global__ __launch_bounds__(512, 1) void patch_wgrad_kernel(const bf16* __restr
 // Issue order per loader wave (vmcnt retires in issue order): R(0) T(0) R(1) T(1) R(2) T(2) R(3),
 // then iteration k issues T(k+3) R(k+4); before the barrier of unit i, R(i) and T(i) must have
 // landed: vmcnt = the ops issued after T(i) (R(i+1) and iterations i-2, i-1).
-#ifndef IVIT_PW_WS
-#define IVIT_PW_WS 1
-#endif
 // anatomy builds (tools/ab_build.sh -DPW_ANAT=n; timing only, wrong results): 1 no MFMAs, 2 no raster
 // loads, 3 no token-gradient DMA, 4 neither load, 5 every unit's token-gradient rows from chunk 0
 #ifndef PW_ANAT
@@ -939,7 +936,7 @@ long patch_wgrad_raster_workspace(long D) { return (long)WG_NWG * 2 * D * 128 * 
 // the XCD-sharded schedule's workgroups per XCD (0: the linear schedule)
 int pw_shard_p(long C, long Wp, long J) {
   const long G = (C + 1) / 2;
-  if (!IVIT_PW_WS || Wp < WG_MU || G < 32 || J < 64) return 0;
+  if (Wp < WG_MU || G < 32 || J < 64) return 0;
   const long R = (G + 31) / 32;  // pairs per workgroup
   return (int)((G + R - 1) / R);
 }
@@ -978,7 +975,7 @@ int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long 
                        (int)D, dW, accumulate);
     return 0;
   }
-  if (IVIT_PW_WS && Wp >= WG_MU)  // the wave-specialised form's lane positions need Wp >= 32
+  if (Wp >= WG_MU)  // the wave-specialised form's lane positions need Wp >= 32
     hipLaunchKernelGGL(patch_wgrad_ws_kernel, dim3(WG_NWG), dim3(512), 0, st, dtok, img, (int)C, (int)H, (int)W, Wp, Np,
                        M, J, 0, slab);
   else

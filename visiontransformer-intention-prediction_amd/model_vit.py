@@ -125,7 +125,8 @@ class TwoStreamViTBackbone(nn.Module):
     def _cdt(self):
         return BF16 if getattr(self, "compute_dtype", torch.float32) == torch.bfloat16 else F32
 
-    concurrent_streams = True
+    # A/B switch (IVIT_CONCURRENT_STREAMS=0): both ViTs on the caller's stream, one after the other
+    concurrent_streams = os.environ.get("IVIT_CONCURRENT_STREAMS", "1") == "1"
 
     def stream_tokens(self, lidar_bev, map_bev):
         """The LiDAR and map ViTs are independent until the fusion block: run them on two HIP
