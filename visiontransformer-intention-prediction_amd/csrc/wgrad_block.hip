@@ -10,13 +10,14 @@
 // S token splits (S = 7 at the bench shape: 252 workgroups, one per CU), reduced by one launch:
 // the partial traffic is paid once per block instead of once per GEMM, and every CU streams.
 //
-// Workgroup: 8 compute waves (2 along rows x 4 along columns, each 64 x 96 = 2 x 3 blocks of
-// v_mfma_f32_32x32x16_bf16) + 4 loader waves, K step 32 tokens, 4 LDS stages (32 KiB each: the
-// dY block's 128 columns and the X block's 384 columns as token-major 256-B-row images), three
-// steps in flight by LDS-DMA, one barrier per step. Both operands are read by transposing LDS
-// reads (frag_mn).
-// Bias: row sums of the dY block on the matrix pipe against a ones operand (tiles with tn == 0;
-// each wave adds one MFMA per step: its row block wn & 1 on substep wn >> 1).
+// Workgroup: 4 compute waves + 4 loader waves (below), K step 32 tokens, 4 LDS stages (32 KiB
+// each: the dY block's 128 columns and the X block's 384 columns as token-major 256-B-row images),
+// three steps in flight by LDS-DMA, one barrier per step. Both operands are read by transposing
+// LDS reads. Rounds 3-4 ran 8 compute waves (64 x 96 each, two per SIMD in lock step, the bias as
+// an extra MFMA against a ones operand) + 4 loaders: 175-176 us isolated vs 158-169 us for this
+// form (profiles/r05_l_*); the dedicated loader waves themselves came from the round-3 anatomy
+// (every wave issuing its own pieces: DMA skeleton 112 us + MFMA-only 105 us -> 206 us together,
+// an LDS-DMA piece costing its wave ~100-185 cycles beside MFMAs).
 #include "gemm_engine.h"
 #include "panel_common.h"
 
@@ -48,26 +49,29 @@ struct WbArgs {
   float* bslab;
 };
 
-// Roles: waves 0..7 compute (2 along rows x 4 along columns, each 64 x 96), waves 8..11 only
-// issue the LDS-DMA (8 pieces each per step): an LDS-DMA piece costs its issuing wave ~100-185
-// cycles beside MFMAs (MI355X_MICROARCH.md cycle constants), and with every wave issuing its own
-// pieces the DMA and MFMA phases ran nearly serialised (anatomy: DMA skeleton 112 us + MFMA-only
-// 105 us -> 206 us together). Both roles pass exactly one barrier per step.
-// MODE (anatomy builds: -DIVIT_WB_ANATOMY=MODE via tools/ab_build.sh): 0 product, 1 no MFMAs (the DMA / barrier
-// skeleton), 2 no DMA after the prologue (MFMAs on stale stages), 3 the product kernel without the
-// reduce launch.
-constexpr int WB_CW = 8, WB_LW = 4;  // compute / loader waves
+// MODE (anatomy builds: -DIVIT_WB_ANATOMY=MODE via tools/ab_build.sh; timing only): 0 product, 1 no
+// MFMAs (the DMA / barrier skeleton), 2 no DMA after the prologue (MFMAs on stale stages), 3 the
+// product kernel without the reduce launch.
 #ifndef IVIT_WB_ANATOMY
 #define IVIT_WB_ANATOMY 0
 #endif
+// Wave-specialised form (round 5): waves 0-3 compute, one per SIMD, each the tile's 128 rows x 96
+// columns (4 x 3 blocks of v_mfma_f32_32x32x16_bf16, 192 accumulator VGPRs); waves 4-7 load (the
+// same 32 LDS-DMA pieces per step) and also sum the dY block's columns for the bias (VALU on the
+// landed image; those waves idle otherwise), so the compute waves hold no bias accumulator.
+// Fragment reads run one substep ahead of the MFMAs across the step boundary: the step's barrier
+// sits between its two substeps' MFMA groups, after the compute waves' reads of the stage are
+// complete, so the next stage's first fragments are read while the current stage's second MFMA
+// group runs. wgrad_block_kernel's anatomy (MFMA side alone 144 us against a 64-us floor) was
+// the read latency exposed after each step's barrier, at 2 waves per SIMD in lock step.
+// Barriers: B_0 publishes step 0; B_j (j = 1 .. nk) publishes step j and certifies that every
+// compute wave has read stage j - 1 completely, which the loaders then refill with step j + 3.
 template <int MODE>
-__global__ __launch_bounds__(64 * (WB_CW + WB_LW), 1) void wgrad_block_kernel(const WbArgs args) {
+__global__ __launch_bounds__(512, 1) void wgrad_block_kernel(const WbArgs args) {
   __shared__ __attribute__((aligned(16))) char smem[WB_NS * WB_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntiles = args.tile_base[4];
-  // consecutive flat ids (same split, neighbouring tiles) on one XCD: the split's token panels
-  // are fetched into one L2 and shared by its tiles
   const int flat = xcd_remap(blockIdx.x, gridDim.x);
   const int split = flat / ntiles, tile = flat - split * ntiles;
   int gi = 0;
@@ -78,14 +82,13 @@ __global__ __launch_bounds__(64 * (WB_CW + WB_LW), 1) void wgrad_block_kernel(co
   const int tm = lt / g.tiles_n, tn = lt - tm * g.tiles_n;
   const int kbeg = split * args.kchunk, kend = min(args.M, kbeg + args.kchunk);
   const int nk = (kend - kbeg + WB_BK - 1) / WB_BK;
+  const bool dob = tn == 0 && args.bslab != nullptr;
 
-  if (wv >= WB_CW) {  // ---------------------------------------------------------------- loader
-    const bf16* Abase = g.dy + tm * WB_TM;  // the dY block's first column
-    const bf16* Bbase = g.x + tn * WB_TN;   // the X block's first column
+  if (wv >= 4) {  // ---------------------------------------------------------------- loader
+    const bf16* Abase = g.dy + tm * WB_TM;
+    const bf16* Bbase = g.x + tn * WB_TN;
     const int lda = g.N, ldb = g.K;
-    const int lw = wv - WB_CW;
-    // 32 pieces of 1 KiB per stage, 8 per loader wave: piece p < 8 -> dY image rows 4p.., else X
-    // image (p - 8) / 8; a piece is 4 token rows x 16 chunks, chunk c of row r at c ^ 4(r & 3)
+    const int lw = wv - 4;
     unsigned voff[8];
     int prow[8], pcol[8];
 #pragma unroll
@@ -98,14 +101,14 @@ __global__ __launch_bounds__(64 * (WB_CW + WB_LW), 1) void wgrad_block_kernel(co
       pcol[i] = col;
       voff[i] = 2u * (unsigned)(row * (img == 0 ? lda : ldb) + col);
     }
-    const bool isa = lw == 0;  // wave-uniform: loader 0 fills the dY image, 1..3 the X images
+    const bool isa = lw == 0;
     auto issue = [&](int stage, int k0) {
       char* st = smem + stage * WB_STAGE + lw * 8192;
       if (k0 + WB_BK <= kend) {
         const char* sb = isa ? uniform_ptr(Abase + (long)k0 * lda) : uniform_ptr(Bbase + (long)k0 * ldb);
 #pragma unroll
         for (int i = 0; i < 8; ++i) glds_s<false>(voff[i], sb, st + i * 1024);
-      } else {  // the ragged last step: token rows >= kend read the zero page
+      } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int t = k0 + prow[i];
@@ -115,86 +118,116 @@ __global__ __launch_bounds__(64 * (WB_CW + WB_LW), 1) void wgrad_block_kernel(co
         }
       }
     };
+    // bias: column 32 lw + (lane & 31) of the dY block, tokens 16 hl .. 16 hl + 15 of each step
+    const int bcol = 32 * lw + (lane & 31);
+    int boff[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = 16 * hl + r;
+      boff[r] = row * 256 + (((bcol >> 3) ^ ((row & 3) << 2)) << 4) + (bcol & 7) * 2;
+    }
+    float bsum = 0.f;
+    auto bias = [&](int stage) {
+      const char* im = smem + stage * WB_STAGE;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bsum += __uint_as_float((unsigned)*(const unsigned short*)(im + boff[r]) << 16);
+    };
+    auto wait_step = [&](int j) {  // step j landed; steps j+1, j+2 (those issued) stay in flight
+      const int after = (j + 1 < nk ? 8 : 0) + (j + 2 < nk ? 8 : 0);
+      if (after == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (after == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
 #pragma unroll
     for (int s = 0; s < WB_NS - 1; ++s)
       if (s < nk) issue(s, kbeg + s * WB_BK);
-    for (int kt = 0; kt < nk; ++kt) {
-      // this step's pieces have landed (later steps stay in flight) ...
-      static_assert(WB_NS == 4, "counted waits below assume three steps in flight");
-      if (MODE == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // ... published by the barrier, which also tells that the compute waves are done with the
-      // stage refilled next (read in step kt-1)
-      __builtin_amdgcn_s_barrier();
-      if (MODE != 2 && kt + WB_NS - 1 < nk) issue((kt + WB_NS - 1) % WB_NS, kbeg + (kt + WB_NS - 1) * WB_BK);
+    wait_step(0);
+    __builtin_amdgcn_s_barrier();  // B_0
+    if (3 < nk) issue(3, kbeg + 3 * WB_BK);
+    if (dob) bias(0);
+    for (int j = 1; j <= nk; ++j) {
+      if (j < nk) wait_step(j);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my bias reads of stage j - 1 are done
+      __builtin_amdgcn_s_barrier();  // B_j
+      if (MODE != 2 && j + 3 < nk) issue((j + 3) % WB_NS, kbeg + (j + 3) * WB_BK);
+      if (dob && j < nk) bias(j % WB_NS);
+    }
+    if (dob) {
+      float* bs = args.bslab + ((long)split * 2 + hl) * args.bias_n + g.bias_off;
+      bs[tm * WB_TM + bcol] = bsum;
     }
     return;
   }
 
   // ------------------------------------------------------------------------------------ compute
-  const int wm = wv >> 2, wn = wv & 3;
-  f32x16 acc[2][3];
+  const int cw = wv;  // columns 96 cw .. 96 cw + 95 of the X block
+  f32x16 acc[4][3];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  f32x16 accb;
+  struct Frags { bf16x8 a[4], b[3]; };
+  // frag_mn's addresses, factored: the 32-column block m of an image is at lane offset
+  // lc + 64 (m ^ q) (the row swizzle 4 (r & 3) only touches the chunk bits m covers); lc and q are
+  // laundered per load set so the compiler forms the 7 offsets there instead of holding them
+  // (at 192 accumulators + two fragment sets the held offsets spilled)
+  const int fq = (lane >> 2) & 3;
+  const int flc = (8 * (lane >> 5) + fq) * 256 + 32 * ((lane >> 4) & 1) + 16 * ((lane & 3) >> 1) + (lane & 1) * 8;
+  auto load = [&](Frags& f, int stage, int t) {
+    int q = fq, lc = flc;
+    asm volatile("" : "+v"(q), "+v"(lc));
+    const char* st = smem + stage * WB_STAGE + 4096 * t;
+    auto rd = [&](const char* img, int m) {
+      const char* a = img + lc + 64 * (m ^ q);
+      union { s16x4 s[2]; bf16x8 v; } u;
+      u.s[0] = ds_tr(a);
+      u.s[1] = ds_tr(a + 1024);
+      return u.v;
+    };
 #pragma unroll
-  for (int r = 0; r < 16; ++r) accb[r] = 0.f;
-  const bool dob = tn == 0 && args.bslab != nullptr;
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.0f;
-
-  for (int kt = 0; kt < nk; ++kt) {
-    __builtin_amdgcn_s_barrier();
-    const char* st = smem + (kt % WB_NS) * WB_STAGE;
-#pragma unroll
-    for (int t = 0; t < (MODE == 1 ? 0 : 2); ++t) {
-      bf16x8 fa[2], fb[3];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) fa[i] = frag_mn(st, 16 * t, 64 * wm + 32 * i, lane);
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int cb = 96 * wn + 32 * j;
-        fb[j] = frag_mn(st + WB_IMG * (1 + (cb >> 7)), 16 * t, cb & 127, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      if (dob && t == (wn >> 1)) {  // uniform branches: a runtime index into fa is lowered to
-        if (wn & 1)                 // per-element select chains (240 VALU per step)
-          accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], ones, accb, 0, 0, 0);
-        else
-          accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], ones, accb, 0, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // my reads of this stage are done
-  }
-
-  // partial tile -> this split's slab, in dW's own [N][K] layout (the reduce is a plain sum)
-  float* slab = args.slab + (long)split * args.slab_n + g.slab_off;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i) f.a[i] = rd(st, i);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const int col = tn * WB_TN + 96 * wn + 32 * j + (lane & 31);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = tm * WB_TM + 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        slab[(long)row * g.K + col] = acc[i][j][r];
-      }
+      const int cb = 96 * cw + 32 * j;
+      f.b[j] = rd(st + WB_IMG * (1 + (cb >> 7)), (cb & 127) >> 5);
     }
-  if (dob && (lane & 31) == 0) {  // every column of accb holds the row sum
-    float* bs = args.bslab + ((long)split * 2 + (wn >> 1)) * args.bias_n + g.bias_off;
+  };
+  auto mma = [&](const Frags& f) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) bs[tm * WB_TM + 64 * wm + 32 * (wn & 1) + (r & 3) + 8 * (r >> 2) + 4 * hl] = accb[r];
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        if (MODE != 1) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+  };
+  Frags f0, f1;
+  __builtin_amdgcn_s_barrier();  // B_0
+  load(f0, 0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    load(f1, kt % WB_NS, 1);
+    mma(f0);
+    // the scheduler must not move MFMAs across the barrier (it sank 9 of mma(f0)'s 12 below it,
+    // which left f1's reads 3 MFMAs to land before the lgkmcnt(0))
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // stage kt fully read
+    __builtin_amdgcn_s_barrier();                        // B_{kt+1}
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < nk) load(f0, (kt + 1) % WB_NS, 0);
+    mma(f1);
+    __builtin_amdgcn_sched_barrier(0);
   }
+
+  // the lane's slab offset laundered here, so that the store addresses are formed after the loop
+  int lo = 4 * hl * g.K + (lane & 31);
+  asm volatile("" : "+v"(lo));
+  float* slab = args.slab + (long)split * args.slab_n + g.slab_off + (long)(tm * WB_TM) * g.K + tn * WB_TN + 96 * cw + lo;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) slab[(long)(32 * i + (r & 3) + 8 * (r >> 2)) * g.K + 32 * j] = acc[i][j][r];
 }
 
 struct WbOut {
@@ -307,8 +340,7 @@ extern "C" int ivit_vit_block_wgrad(long M, long D, long Hd, const void* dy2, co
   args.bslab = args.slab + (long)S * off;
   hipStream_t st = ivit_stream(stream);
   // anatomy builds (tools/ab_build.sh -DIVIT_WB_ANATOMY=1 / 2) compile a diagnostic body instead
-  hipLaunchKernelGGL(wgrad_block_kernel<IVIT_WB_ANATOMY>, dim3(args.tile_base[4] * S), dim3(64 * (WB_CW + WB_LW)), 0,
-                     st, args);
+  hipLaunchKernelGGL(wgrad_block_kernel<IVIT_WB_ANATOMY>, dim3(args.tile_base[4] * S), dim3(512), 0, st, args);
   IVIT_LAUNCH_CHECK();
   if (IVIT_WB_ANATOMY == 3) return 0;  // anatomy 3: the product kernel without its reduce (timing only)
   hipLaunchKernelGGL(wgrad_block_reduce_kernel, dim3(ivit_cdiv((off + boff) / 4, 256)), dim3(256), 0, st, args.slab,
