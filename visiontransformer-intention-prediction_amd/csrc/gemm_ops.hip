@@ -498,23 +498,29 @@ extern "C" int ivit_patch_embed_wgrad(int dtype, const void* dtok, const float* 
   const long Np = (H / 8) * (W / 8);
   const long n = D * C * 64;
   const int splits = (int)wgrad_splits(D, C * 64, B * Np, bf);
-  long cw_off = (long)splits * n * 4;  // colsum workspace after the slab
-  if (bf && patch_wgrad_raster_ok(B, C, H, W, D)) {  // raster read once (patch_embed.hip)
-    cw_off = patch_wgrad_raster_workspace2(B, C, H, W, D);
-    int rc = patch_wgrad_raster((const bf16*)dtok, img, B, C, H, W, D, dW, accumulate, work, st);
+  const bool raster = bf && patch_wgrad_raster_ok(B, C, H, W, D);  // raster read once (patch_embed.hip)
+  const long cw_off = raster ? patch_wgrad_raster_workspace2(B, C, H, W, D) : (long)splits * n * 4;  // after the slab
+  // the pos / cls / bias gradients first: they are short, and after the weight gradient (whose
+  // persistent workgroups hold every CU's LDS) they waited for it and ran at the step's tail
+  // (54.6 us for the LiDAR stream in profiles/r05_j_bench_kernel_stats.csv's trace)
+  char* cw = (char*)work + cw_off;
+  int rc = patch_pos_bias_grad(dtype, dtok, B, Np, D, dbias, dpos, dcls, accumulate, cw,
+                               ivit_colsum_workspace(B * Np, D), stream);
+  if (rc) return rc;
+  if (raster) {
+    rc = patch_wgrad_raster((const bf16*)dtok, img, B, C, H, W, D, dW, accumulate, work, st);
     if (rc) return rc;
     IVIT_LAUNCH_CHECK();
   } else {
     float* slab = (float*)work;
-    int rc = bf ? patch_wgrad_t<bf16>(dtok, img, B, C, H, W, D, slab, splits, st)
-                : patch_wgrad_t<float>(dtok, img, B, C, H, W, D, slab, splits, st);
+    rc = bf ? patch_wgrad_t<bf16>(dtok, img, B, C, H, W, D, slab, splits, st)
+            : patch_wgrad_t<float>(dtok, img, B, C, H, W, D, slab, splits, st);
     if (rc) return rc;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3(ivit_cdiv(n, 256)), dim3(256), 0, st, slab, n, splits, dW,
                        accumulate);
+    IVIT_LAUNCH_CHECK();
   }
-  char* cw = (char*)work + cw_off;
-  return patch_pos_bias_grad(dtype, dtok, B, Np, D, dbias, dpos, dcls, accumulate, cw, ivit_colsum_workspace(B * Np, D),
-                             stream);
+  return 0;
 }
 
 // bf16 patch matrix. One workgroup per (b, c, gy) = 8 consecutive raster rows (8*W floats,

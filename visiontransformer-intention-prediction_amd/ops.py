@@ -846,6 +846,18 @@ def _unit_ln_params(n, dev):
     return _UNIT_LN[key]
 
 
+_ZEROS = {}
+
+
+def _zeros(n, dev):
+    """A cached all-zero f32 vector (never written)."""
+    key = (n, str(dev))
+    z = _ZEROS.get(key)
+    if z is None:
+        z = _ZEROS[key] = torch.zeros((n,), dtype=torch.float32, device=dev)
+    return z
+
+
 class NeckFn(torch.autograd.Function):
     """Everything after the ViT blocks (model_vit.py:116-142,179-185; heads.py):
     final ViT norm (eps 1e-6) → drop CLS → adapter LN(eps 1e-5) → Linear → GELU for each
@@ -880,20 +892,22 @@ class NeckFn(torch.autograd.Function):
         bns = {}
         packs = {}
         acts = []
+        nbts = []  # the BatchNorms' num_batches_tracked, advanced in one launch below
         for li in range(layers):
             p = f"fusion_block.{li}."
             w1 = pack_conv(P[p + "conv1.weight"], cdt)
             w2 = pack_conv(P[p + "conv2.weight"], cdt)
             c1, s1 = conv_bn_fwd(x, B, Hf, Wf, w1, cdt, torch.float32, P[p + "bn1.running_mean"],
-                                 P[p + "bn1.running_var"], training, nbt=P.get(p + "bn1.num_batches_tracked"))
+                                 P[p + "bn1.running_var"], training)
             r1 = bn_apply(c1, s1, P[p + "bn1.weight"], P[p + "bn1.bias"], cd, relu=True)
             c2, s2 = conv_bn_fwd(r1, B, Hf, Wf, w2, cdt, torch.float32, P[p + "bn2.running_mean"],
-                                 P[p + "bn2.running_var"], training, nbt=P.get(p + "bn2.num_batches_tracked"))
+                                 P[p + "bn2.running_var"], training)
+            nbts += [P.get(p + "bn1.num_batches_tracked"), P.get(p + "bn2.num_batches_tracked")]
             if (p + "downsample.0.weight") in P:
                 wd = pack_conv(P[p + "downsample.0.weight"], cdt)
                 dd, sd = conv_bn_fwd(x, B, Hf, Wf, wd, cdt, torch.float32, P[p + "downsample.1.running_mean"],
-                                     P[p + "downsample.1.running_var"], training,
-                                     nbt=P.get(p + "downsample.1.num_batches_tracked"))
+                                     P[p + "downsample.1.running_var"], training)
+                nbts.append(P.get(p + "downsample.1.num_batches_tracked"))
                 idn = bn_apply(dd, sd, P[p + "downsample.1.weight"], P[p + "downsample.1.bias"], cd)
                 bns[p + "ds"] = (dd, sd, idn)
                 packs[p + "ds"] = wd
@@ -903,6 +917,9 @@ class NeckFn(torch.autograd.Function):
             acts.append((x, c1, s1, r1, c2, s2, out))
             packs[p + "1"], packs[p + "2"] = w1, w2
             x = out
+        nbts = [t for t in nbts if t is not None]
+        if training and nbts:  # BatchNorm2d's num_batches_tracked += 1 (model_vit.py:24-27 via torch)
+            torch._foreach_add_(nbts, 1)
         if A == 0:  # backbone-only call (TwoStreamViTBackbone.forward): fused feature map
             ctx.st = (saved, cat, pre, acts, bns, packs, None, x, 0)
             ctx.meta, ctx.P = meta, P
@@ -911,9 +928,8 @@ class NeckFn(torch.autograd.Function):
         Cp = (Cd + Ci + 7) // 8 * 8
         wh = torch.cat([P["det_head.conv.weight"], P["intention_head.conv.weight"]], 0)
         whp = pack_conv(wh, cdt, cout_pad=Cp)
-        bh = torch.zeros((Cp,), dtype=torch.float32, device=dev)
-        bh[:Cd] = P["det_head.conv.bias"]
-        bh[Cd:Cd + Ci] = P["intention_head.conv.bias"]
+        bh = torch.cat([P["det_head.conv.bias"].float(), P["intention_head.conv.bias"].float(),
+                        _zeros(Cp - Cd - Ci, dev)])
         hout = conv_fwd(x, B, Hf, Wf, whp, bh, cdt, torch.float32)
         cls = torch.empty((B, M // B * A, 1), dtype=torch.float32, device=dev)
         box = torch.empty((B, M // B * A, 6), dtype=torch.float32, device=dev)
@@ -956,7 +972,7 @@ class NeckFn(torch.autograd.Function):
             def head_wgrad(dh, x_last):
                 gp, dbh = conv_wgrad(dh, x_last, B, Hf, Wf, Cin, Cp, 3, cdt, want_bias=True)
                 gw = unpack_conv_grad(gp, Cd + Ci, Cin, 3)
-                return gw[:Cd], gw[Cd:], dbh[:Cd].clone(), dbh[Cd:Cd + Ci].clone()
+                return gw[:Cd], gw[Cd:], dbh[:Cd], dbh[Cd:Cd + Ci]  # views: no copy launches
 
             for n_, g_ in zip(("det_head.conv.weight", "intention_head.conv.weight", "det_head.conv.bias",
                                "intention_head.conv.bias"), head_wgrad(dh, x_last)):
