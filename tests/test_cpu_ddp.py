@@ -211,3 +211,29 @@ def test_single_process_buckets_are_views():
     m.a.weight.grad = None  # replaced outside the bucket → zero_grad re-attaches the view
     gb.zero_grad()
     assert m.a.weight.grad is not None and float(m.a.weight.grad.abs().sum()) == 0.0
+
+
+def test_grad_order_interleaves_streams_and_tail_bucket():
+    """ddp.grad_order: every IntentNetViT parameter once, the two ViTs' blocks interleaved in
+    forward order (so the bucket fill order follows the interleaved backward); GradBuckets'
+    last_bucket_mb gives the last-ready parameters (the LiDAR patch embedding) a small bucket."""
+    import torch.nn as nn
+    from ddp import GradBuckets, grad_order
+    from model_vit import IntentNetViT
+    m = IntentNetViT()
+    order = grad_order(m)
+    names = {id(p): n for n, p in m.named_parameters()}
+    assert sorted(names[id(p)] for p in order) == sorted(names.values())
+    seq = [names[id(p)] for p in order]
+    i0 = seq.index("backbone.vit_lidar.blocks.0.attn.qkv.weight")
+    i1 = seq.index("backbone.vit_map.blocks.0.attn.qkv.weight")
+    i2 = seq.index("backbone.vit_lidar.blocks.1.attn.qkv.weight")
+    assert i0 < i1 < i2
+    gb = GradBuckets(order, 64.0, last_bucket_mb=32.0)
+    last = gb.buckets[-1]
+    assert "backbone.vit_lidar.patch_embed.proj.weight" in {names[id(p)] for p in last.params}
+    assert last.flat.numel() * 4 <= 32 * (1 << 20)
+    assert sum(b.flat.numel() for b in gb.buckets) >= sum(p.numel() for p in m.parameters())
+    # a model without the two-stream backbone: registration order
+    lin = nn.Linear(3, 4)
+    assert grad_order(lin) == list(lin.parameters())

@@ -52,6 +52,36 @@ def init_distributed(backend: str | None = None, force_group: bool = False):
     return rank, local, world, dev
 
 
+def grad_order(model):
+    """The model's trainable parameters in forward order with the two ViT streams interleaved
+    block by block (patch embeddings, block 0 of each stream, block 1, ..., the final norms, then
+    the rest in registration order), so that the reverse — GradBuckets' fill order — follows the
+    order the interleaved backward produces gradients (model_vit.stream_tokens). Models without
+    the two-stream backbone: registration order."""
+    bb = getattr(model, "backbone", None)
+    vl, vm = getattr(bb, "vit_lidar", None), getattr(bb, "vit_map", None)
+    if vl is None or vm is None or not hasattr(vl, "blocks") or not hasattr(vm, "blocks"):
+        return [p for p in model.parameters()]
+    order, seen = [], set()
+
+    def add(mod_or_params):
+        ps = mod_or_params.parameters() if isinstance(mod_or_params, torch.nn.Module) else mod_or_params
+        for p in ps:
+            if id(p) not in seen:
+                seen.add(id(p))
+                order.append(p)
+
+    for v in (vl, vm):
+        add(v.patch_embed)
+        add([t for t in (getattr(v, "cls_token", None), getattr(v, "pos_embed", None)) if t is not None])
+    for i in range(max(len(vl.blocks), len(vm.blocks))):
+        for v in (vl, vm):
+            if i < len(v.blocks):
+                add(v.blocks[i])
+    add(model)  # final norms, adapters, fusion block, heads (registration order)
+    return order
+
+
 # Each parameter's view starts on a 16-byte boundary of its bucket: kernels that write a gradient
 # straight into its view (GradSink: the grouped ViT weight gradient's reduce stores 16 B per lane)
 # need aligned destinations, and a 35-element bias (the detection head) would otherwise leave every
@@ -123,7 +153,8 @@ class GradBuckets:
 
     launched = 0  # collectives issued (tests)
 
-    def __init__(self, params, bucket_mb: float = 64.0, group=None, force_collectives: bool = False):
+    def __init__(self, params, bucket_mb: float = 64.0, group=None, force_collectives: bool = False,
+                 last_bucket_mb: float | None = None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         # world 1: no exchange, unless forced (the collective path exercised on one device)
@@ -132,6 +163,19 @@ class GradBuckets:
         if len({id(p) for p in ps}) != len(ps):
             raise ValueError("GradBuckets: duplicate parameters")
         cap = max(1, int(bucket_mb * (1 << 20)))
+        # last_bucket_mb: the parameters whose gradients arrive last (the end of the reversed list)
+        # get a bucket of their own of at most this size, so the collective that cannot overlap
+        # the backward is short (IntentNetViT: the LiDAR patch embedding's 28.5-MB weight gradient
+        # is the step's last kernel)
+        tail = []
+        if last_bucket_mb is not None:
+            lcap, lbytes = max(1, int(last_bucket_mb * (1 << 20))), 0
+            while ps:
+                nb = ps[0].numel() * ps[0].element_size()
+                if tail and lbytes + nb > lcap:
+                    break
+                tail.append(ps.pop(0))
+                lbytes += nb
         self.buckets: list[_Bucket] = []
         self._of, self._ptr = {}, {}
         self._fresh = set()  # ids of parameters whose bucket view is zeroed and not written yet
@@ -152,6 +196,9 @@ class GradBuckets:
             cur_bytes += nb
         if cur:
             self._add(cur)
+        if tail:
+            self._add(list(reversed(tail)))
+            ps = tail + ps
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in ps]
 
     def _add(self, params):

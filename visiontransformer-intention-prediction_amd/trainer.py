@@ -24,7 +24,7 @@ from __future__ import annotations
 
 import torch
 
-from ddp import GradBuckets, any_rank, broadcast_state, min_on_device
+from ddp import GradBuckets, any_rank, broadcast_state, grad_order, min_on_device
 from loss import device_guard
 from optim import FusedAdamW
 
@@ -39,8 +39,10 @@ class Trainer:
             # identical replicas from the first step, whatever each rank's RNG did
             broadcast_state(model)
         # force_buckets: the bucketed all-reduce path even at world 1 (tests on one GPU over RCCL)
-        self.buckets = GradBuckets(model.parameters(), bucket_mb, force_collectives=force_buckets) \
-            if world > 1 or force_buckets else None
+        # buckets in the order the interleaved backward produces gradients, the last ones in a
+        # 32-MB bucket of their own (the collective left after the backward)
+        self.buckets = GradBuckets(grad_order(model), bucket_mb, force_collectives=force_buckets,
+                                   last_bucket_mb=min(32.0, bucket_mb)) if world > 1 or force_buckets else None
         self.skipped = 0
         self.nonfinite = 0
 
