@@ -52,7 +52,7 @@ def kernel_ms(fn, tags, it=20):
     return [sum(b - a for a, b in ops.ktime_read(t)) / it for t in tags]
 
 
-VARIANTS = [v for v in os.environ.get("ATTN_VARIANTS", "").split(";") if v]  # e.g. "IVIT_ATTN_DKV16=0;IVIT_ATTN_DKV16=1"
+VARIANTS = [v for v in os.environ.get("ATTN_VARIANTS", "").split(";") if v]  # "ENV=V;ENV=V": same-call A/B of env switches
 for rep in range(2 if VARIANTS else 1):
     for var in VARIANTS or [""]:
         if var:

@@ -10,14 +10,9 @@ torch.manual_seed(0)
 qkv = torch.randn(B * N, 3 * H * 64, device="cuda").to(torch.bfloat16)
 qkv[:, : H * 64] = (qkv[:, : H * 64].float() * ops.Q2_SCALE).to(torch.bfloat16)
 dout = torch.randn(B * N, H * 64, device="cuda").to(torch.bfloat16)
-# ATTN_FORMS="000;111": each listed (dK/dV, dQ, forward) form in turn (IVIT_ATTN_DKV16 / DQ16 / FWD16 —
-# the round-5 A/B switches, removed with the losing kernels: the variable is inert on the current tree)
-for form in (os.environ.get("ATTN_FORMS") or "").split(";"):
-    if form:
-        os.environ["IVIT_ATTN_DKV16"], os.environ["IVIT_ATTN_DQ16"], os.environ["IVIT_ATTN_FWD16"] = form
-    for _ in range(3):
-        o, lse = ops.attn_fwd_q2(qkv, B, N, H)
-        if os.environ.get("FWD_ONLY") != "1":
-            ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H)
-    torch.cuda.synchronize()
+for _ in range(3):
+    o, lse = ops.attn_fwd_q2(qkv, B, N, H)
+    if os.environ.get("FWD_ONLY") != "1":
+        ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H)
+torch.cuda.synchronize()
 print("ok")
