@@ -96,21 +96,53 @@ def write_intervals(ops, path):
 
 
 def rocprof_union(name):
-    """(us per launch, source) of the newest committed rocprofv3-trace union of an ATTN entry's
-    kernels (profiles/*_<name>_union.json, written by tools/kunion.py --json from the kernel trace of
-    a profiled bench command), or (None, None)."""
+    """(us per launch, source, generated) of the newest committed rocprofv3-trace union of an ATTN
+    entry's kernels (profiles/*_<name>_union.json, written by tools/kunion.py --json from the kernel
+    trace of a profiled bench command), or (None, None, None). A file whose matched kernel names
+    (``kernel_names``) are not exactly the entry's current kernels is stale and skipped; files
+    older than that field are skipped too."""
     import glob
     files = sorted(glob.glob(os.path.join(HERE, "profiles", f"*_{name}_union.json")),
                    key=lambda p: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(p))])
+    want = ATTN[name]["kernels"]
     for f in reversed(files):
         try:
             with open(f) as fh:
                 d = json.load(fh)
-            if d.get("source_kind") == "rocprofv3":
-                return float(d["union_us_per_launch"]), os.path.relpath(f, HERE)
+            if d.get("source_kind") != "rocprofv3":
+                continue
+            got = d.get("kernel_names", [])
+            if not (got and all(any(w in k for w in want) for k in got) and all(any(w in k for k in got) for w in want)):
+                continue
+            return float(d["union_us_per_launch"]), os.path.relpath(f, HERE), d.get("generated_utc")
         except (OSError, ValueError, KeyError):
             continue
-    return None, None
+    return None, None, None
+
+
+def warm_time_ms(fn, warm_s=2.0, iters=20, reps=3):
+    """Launch time of fn the way tools/attn_bench.py and DESIGN quote isolated kernels: >= warm_s
+    seconds of back-to-back launches first (the clock ramps under sustained MFMA load,
+    MI355X_MICROARCH.md "DVFS"; one warm launch read 0.81-0.83 ms where the warm pair runs
+    0.71-0.73), then the median over ``reps`` of the mean of ``iters`` launches (HIP events).
+    -> (median ms, [ms per rep])."""
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        for _ in range(10):
+            fn()
+        torch.cuda.synchronize()
+    res = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        res.append(s.elapsed_time(e) / iters)
+    return sorted(res)[len(res) // 2], res
 
 
 def attn_flops(name, B, N, H, Dh=64):
@@ -153,8 +185,8 @@ def pmc_traffic(kernel_prefix):
     return tot, os.path.relpath(files[-1], HERE)
 
 
-def isolated_attn_ms(name, B, N, H, dev, iters=20):
-    """Mean launch time of ivit_attn_fwd_q2 / ivit_attn_bwd_q2 alone at the bench shape."""
+def isolated_attn_ms(name, B, N, H, dev):
+    """ivit_attn_fwd_q2 / ivit_attn_bwd_q2 alone at the bench shape, warm (warm_time_ms)."""
     import ops
     g = torch.Generator(device=dev).manual_seed(0)
     qkv = torch.randn(B * N, 3 * H * 64, device=dev, generator=g).to(torch.bfloat16)
@@ -163,15 +195,7 @@ def isolated_attn_ms(name, B, N, H, dev, iters=20):
     o, lse = ops.attn_fwd_q2(qkv, B, N, H)
     fn = (lambda: ops.attn_fwd_q2(qkv, B, N, H)) if name == "attn_fwd" else \
         (lambda: ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H))
-    fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters
+    return warm_time_ms(fn)
 
 
 def cpu_model_name():
@@ -540,23 +564,27 @@ def main():
     if default_cfg:
         # the same launches' device time from a committed rocprofv3 kernel trace of the profiled
         # bench command (tools/kunion.py --json): the figure the profile files reproduce
-        us, src = rocprof_union(roof)
+        us, src, gen = rocprof_union(roof)
         if us is not None:
             out["roofline"]["frac_rocprof"] = round(afl / (us * 1e-6) / 1e12 / peak, 4)
+            out["roofline"]["frac_rocprof_source"] = {"file": src, "generated_utc": gen}
             out["roofline"]["frac_rocprof_note"] = (f"{us:.1f} us per launch = the union of the kernels' intervals in "
-                                                    f"the rocprofv3 kernel trace summarised in {src} (profiled "
-                                                    f"command: the profiler lowers the clock, MI355X_MICROARCH.md "
-                                                    f"DVFS item 2)")
+                                                    f"the rocprofv3 kernel trace summarised in {src} (a committed "
+                                                    f"profile of the same kernels, not this run; profiled command: "
+                                                    f"the profiler lowers the clock, MI355X_MICROARCH.md DVFS item 2)")
     if args.intervals_out and timing:
         out["roofline"]["intervals_file"] = os.path.relpath(os.path.abspath(args.intervals_out), HERE)
     if default_cfg and world == 1:
         # the same kernel(s) alone on the same shape (outside the timed region): the frac without the
         # other ViT stream's kernels sharing the CUs
-        iso = isolated_attn_ms(roof, B, N, 6, dev)
+        iso, reps = isolated_attn_ms(roof, B, N, 6, dev)
         out["roofline"]["isolated"] = {"ms": round(iso, 4), "achieved": round(afl / (iso * 1e-3) / 1e12, 2),
                                        "frac": round(afl / (iso * 1e-3) / 1e12 / peak, 4),
-                                       "note": "mean of 20 back-to-back launches on random bf16 inputs of the "
-                                               "bench shape (prescaled Q), HIP events, nothing else running"}
+                                       "reps_ms": [round(r, 4) for r in reps],
+                                       "note": "warm: 2 s of back-to-back launches, then the median of 3 x the mean "
+                                               "of 20 launches (HIP events) on random bf16 inputs of the bench shape "
+                                               "(prescaled Q), nothing else running — the protocol of "
+                                               "tools/attn_bench.py and DESIGN's kernel table"}
     if force:
         out["collectives_world1"] = time_forced_buckets(model, opt, lf, anchors, batch, args, ms)
     if train:

@@ -361,12 +361,26 @@ int ivit_lidar_bev(const void* points, int points_f64, long ld, const float* int
 /* Batched NMS (eval_vit.py:170 for every sample of a batch, one launch per stage): sample s
  * owns rows seg[s] .. seg[s+1]-1 (int64 device offsets) of boxes / scores / keep and the mask
  * words mask_off[s] .. + n_s * ceil(n_s / 64); keep receives LOCAL kept indices in score order,
- * count[s] their number; the score order is a stable descending segmented radix sort.
- * work >= ivit_nms_batched_workspace(n_samples, total, mask_words) bytes.                      */
+ * count[s] their number; the score order is a stable descending radix sort (one workgroup per
+ * sample). n_s <= 131072. work >= ivit_nms_batched_workspace(n_samples, total, mask_words) bytes. */
 long ivit_nms_batched_workspace(long n_samples, long total, long mask_words);
 int ivit_nms_batched(const float* boxes_xywha, const float* scores, const long* seg, const long* mask_off,
                      long n_samples, long total, long max_n, long mask_words, double iou_thr, long* keep,
                      long* count, void* work, long work_bytes, void* stream);
+
+/* Eval post-processing of a batch (replaces the per-sample loop of eval_vit.py:156-176: sigmoid,
+ * torch.where(score >= CONFIDENCE_THRESHOLD), decode_box_predictions utils.py:227-257, apply_nms
+ * utils.py:259-274, argmax of the intention logits) with no host round trip. cls [B, NA] f32
+ * logits, box_rel [B, NA, 6], intent [B, NA, K], anchors [NA, 5]; NA <= 131072. Sample s's kept
+ * detections, in NMS (descending score) order, go to rows s*NA .. s*NA + out_count[s] - 1 of
+ * out_scores [B, NA], out_boxes [B, NA, 5] (decoded xywha) and out_intent [B, NA] (int64);
+ * out_count [B] int64 is the one value the caller reads back. Scores are torch's f32 GPU sigmoid,
+ * boxes ivit_decode_boxes', keep order torchvision CPU nms's (bit-exact).
+ * work >= ivit_eval_post_workspace(B, NA) bytes.                                               */
+long ivit_eval_post_workspace(long B, long NA);
+int ivit_eval_post(const float* cls, const float* box_rel, const float* intent, const float* anchors, long B, long NA,
+                   long K, float conf_thr, double iou_thr, float* out_scores, float* out_boxes, long* out_intent,
+                   long* out_count, void* work, long work_bytes, void* stream);
 
 /* ---- BEV augmentation passes ----------------------------------------
  * Replaces the raster side of utils.augment_bev (utils.py:500-517): random_flip_bev's np.flip

@@ -62,10 +62,12 @@ def test_argument_validation_without_device():
 def test_workspace_queries_are_pure_host():
     dll = _lib.lib.load()
     B, N, H = 8, 4501, 6
-    npad = (N + 63) // 64 * 64  # lse2 + delta rows, padded to the 64-row tile
-    assert dll.ivit_attn_workspace(_lib.BF16, B, N, H, 64, 1) == 2 * B * H * npad * 4
+    npad = (N + 63) // 64 * 64  # lse2 + delta rows, padded to the 64-row tile, + the prescaled Q copy
+    assert dll.ivit_attn_workspace(_lib.BF16, B, N, H, 64, 1) == 2 * B * H * npad * 4 + B * N * H * 64 * 2
     assert dll.ivit_attn_workspace(_lib.BF16, B, N, H, 64, 0) == 0
     assert dll.ivit_nms_workspace(22500) > 0
+    assert dll.ivit_eval_post_workspace(32, 22500) >= 32 * 22500 * 352 * 8  # the padded suppression masks
+    assert dll.ivit_eval_post_workspace(0, 22500) == 64
 
 
 def test_ptr_refuses_host_tensors():

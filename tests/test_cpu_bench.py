@@ -76,15 +76,26 @@ def test_intervals_file_reproduces_the_roofline_union(tmp_path):
 
 
 def test_rocprof_union_reads_newest_trace_summary(tmp_path, monkeypatch):
+    """The newest rocprofv3 union whose matched kernels are exactly the entry's current kernels;
+    a newer file of other (replaced) kernels, one without the names, and bench-interval files are skipped."""
     import json
     prof = tmp_path / "profiles"
     prof.mkdir()
-    (prof / "r05_a_attn_bwd_union.json").write_text(json.dumps({"source_kind": "rocprofv3",
+    cur = ["(anonymous namespace)::attn_bwd_dq_v4_kernel<4>(bf16 const*)",
+           "(anonymous namespace)::attn_bwd_dkv_v4_kernel<4>(bf16 const*)"]
+    old = ["(anonymous namespace)::attn_bwd_dq_v3_kernel<4>(bf16 const*)",
+           "(anonymous namespace)::attn_bwd_dkv_v4_kernel<4>(bf16 const*)"]
+    (prof / "r05_a_attn_bwd_union.json").write_text(json.dumps({"source_kind": "rocprofv3", "kernel_names": cur,
                                                                 "union_us_per_launch": 900.0}))
-    (prof / "r05_b_attn_bwd_union.json").write_text(json.dumps({"source_kind": "rocprofv3",
-                                                                "union_us_per_launch": 850.0}))
-    (prof / "r05_c_attn_bwd_union.json").write_text(json.dumps({"source_kind": "bench_intervals",
+    (prof / "r05_b_attn_bwd_union.json").write_text(json.dumps({"source_kind": "rocprofv3", "kernel_names": cur,
+                                                                "union_us_per_launch": 850.0,
+                                                                "generated_utc": "2026-10-18T00:00:00Z"}))
+    (prof / "r05_c_attn_bwd_union.json").write_text(json.dumps({"source_kind": "bench_intervals", "kernel_names": cur,
                                                                 "union_us_per_launch": 700.0}))
+    (prof / "r05_d_attn_bwd_union.json").write_text(json.dumps({"source_kind": "rocprofv3", "kernel_names": old,
+                                                                "union_us_per_launch": 600.0}))
+    (prof / "r05_e_attn_bwd_union.json").write_text(json.dumps({"source_kind": "rocprofv3",
+                                                                "union_us_per_launch": 500.0}))
     monkeypatch.setattr(bench, "HERE", str(tmp_path))
-    us, src = bench.rocprof_union("attn_bwd")
-    assert us == 850.0 and src.endswith("r05_b_attn_bwd_union.json")
+    us, src, gen = bench.rocprof_union("attn_bwd")
+    assert us == 850.0 and src.endswith("r05_b_attn_bwd_union.json") and gen == "2026-10-18T00:00:00Z"

@@ -57,6 +57,61 @@ def test_postprocess_batch_matches_oracle():
         assert torch.equal(got[b]["pred_intentions"].cpu(), torch.argmax(it[b][idx][keep], -1))
 
 
+def _post_reference(cls, box, it, anchors, conf=0.1, thr=0.2):
+    """The reference's per-sample loop (eval_vit.py:156-176) on the same device tensors: torch's
+    GPU sigmoid, torch.where, the device decode, the oracle's torchvision-CPU NMS, CPU argmax."""
+    import utils
+    out = []
+    for b in range(cls.shape[0]):
+        s = torch.sigmoid(cls[b].reshape(-1).float())
+        idx = torch.where(s >= conf)[0]
+        if idx.numel() == 0:
+            out.append((torch.empty(0), torch.empty((0, 5)), torch.empty(0, dtype=torch.long)))
+            continue
+        dec = utils.decode_box_predictions(box[b].reshape(-1, 6)[idx], anchors[idx]).cpu()
+        keep = torch.as_tensor(O.nms_numpy(dec.numpy(), s[idx].cpu().numpy(), thr), dtype=torch.long)
+        out.append((s[idx].cpu()[keep], dec[keep], torch.argmax(it[b].reshape(cls.shape[1], -1)[idx].cpu()[keep], -1)))
+    return out
+
+
+def test_postprocess_adversarial_vs_reference_loop():
+    """ivit_eval_post (one batched pass: sigmoid, threshold compaction, decode, stable score sort,
+    NMS, argmax) against the reference's per-sample loop, bit-exact, on a batch holding: random
+    logits; every logit equal (22 500 tied scores, all pass); nothing passing; logits at the
+    threshold's edge (sigmoid within an ulp of 0.1), NaN / +-inf logits and -0 / +0; quantised
+    logits (mass ties) over overlapping boxes; intention rows with tied maxima and NaN."""
+    import utils
+    g = torch.Generator().manual_seed(11)
+    anchors = O.generate_anchors(400, 720, 8)
+    NA = anchors.shape[0]
+    B = 5
+    cls = torch.randn(B, NA, generator=g) * 2.0
+    cls[1] = 0.37
+    cls[2] = -30.0
+    edge = torch.log(torch.tensor(0.1 / 0.9))
+    ulps = torch.arange(-64, 64, dtype=torch.float32) * 1.2e-7
+    cls[3] = (edge + ulps.repeat(NA // 128 + 1)[:NA]).float()
+    cls[3, :50] = float("nan")
+    cls[3, 50:60] = float("inf")
+    cls[3, 60:70] = float("-inf")
+    cls[3, 70:80] = 0.0
+    cls[3, 80:90] = -0.0
+    cls[4] = torch.round(torch.randn(NA, generator=g) * 2) / 2
+    box = torch.randn(B, NA, 6, generator=g) * 0.3
+    box[4, :, :4] = 0.05 * torch.randn(NA, 4, generator=g)  # heavy overlaps
+    it = torch.round(torch.randn(B, NA, 8, generator=g))  # tied maxima
+    it[0, :100, 3] = float("nan")
+    it[0, 100:200, 2:4] = float("nan")
+    dev_args = (cls.cuda(), box.cuda(), it.cuda(), anchors.cuda())
+    got = utils.postprocess_batch(*dev_args, 0.1, 0.2)
+    want = _post_reference(*dev_args)
+    for b, (p, (ws, wb, wi)) in enumerate(zip(got, want)):
+        assert torch.equal(p["pred_scores"].cpu(), ws), b
+        assert torch.equal(p["pred_boxes_xywha"].cpu(), wb), b
+        assert torch.equal(p["pred_intentions"].cpu(), wi), b
+    assert got[2]["pred_scores"].numel() == 0 and got[1]["pred_scores"].numel() > 0
+
+
 def test_postprocess_empty_after_threshold():
     import utils
     anchors = O.generate_anchors(32, 48, 8).cuda()

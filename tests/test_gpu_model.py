@@ -594,7 +594,7 @@ def test_config1_fp32_full_grid_train_step_vs_oracle():
 def test_config4_eval_batch32_full_grid_vs_oracle():
     """BASELINE config 4 end to end (eval_vit.py:136-187): B = 32 full-grid bf16 inference, then
     sigmoid >= 0.1, decode, NMS(0.2), intention argmax for all 32 samples through the batched
-    device post-processing (ivit_nms_batched), against the oracle: decode within 1e-5 rel of the
+    device post-processing (ivit_eval_post), against the oracle: decode within 1e-5 rel of the
     oracle's decode, NMS keep indices bit-exact (torchvision CPU semantics) per sample on the same
     boxes / scores, scores and intentions equal."""
     import model_vit

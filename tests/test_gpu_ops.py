@@ -190,6 +190,32 @@ def test_attention_q2_prescaled_path(B, N, H):
         assert _rel(d[:, i], g[:, i]) < 3e-2, ("qkv"[i], _rel(d[:, i], g[:, i]))
 
 
+@pytest.mark.parametrize("B,N,H", [(1, 64, 1), (2, 257, 3), (1, 4501, 2), (1, 33, 1)])
+def test_attention_plain_entry_is_the_v4_pair(B, N, H):
+    """The reference-facing seam (ivit_attn_bwd, bf16; INTEGRATION.md binds timm Attention to it)
+    runs the product's 16x16x32 v4 backward pair on a prescaled copy of Q: its dQ / dK / dV are
+    bitwise those of ivit_attn_bwd_q2 on qkv with the Q block holding bf16(q * log2(e)/8), and the
+    kernel-timing hook records exactly one dQ and one dK/dV v4 launch for it."""
+    import ops
+    from _lib import BF16
+    D = H * 64
+    qkv = torch.randn(B * N, 3 * D, device=DEV).to(torch.bfloat16)
+    dod = torch.randn(B * N, D, device=DEV).to(torch.bfloat16)
+    o, lse = ops.attn_fwd(qkv, B, N, H, BF16)
+    qs = qkv.clone()
+    qs[:, :D] = (qkv[:, :D].float() * ops.Q2_SCALE).to(torch.bfloat16)
+    o2, l2 = ops.attn_fwd_q2(qs, B, N, H)
+    assert torch.equal(o, o2) and torch.equal(lse, l2)  # the forward's in-kernel prescale rounds alike
+    torch.cuda.synchronize()
+    ops.ktime_arm(True)
+    d_plain = ops.attn_bwd(qkv, o, dod, lse, B, N, H, BF16)
+    ops.ktime_arm(False)
+    torch.cuda.synchronize()
+    assert len(ops.ktime_read(ops.KT_ATTN_BWD_DQ)) == 1 and len(ops.ktime_read(ops.KT_ATTN_BWD_DKV)) == 1
+    d_q2 = ops.attn_bwd_q2(qs, o, dod, lse, B, N, H)
+    assert torch.equal(d_plain, d_q2)
+
+
 def test_kernel_exec_timing_hook():
     """ivit_ktime_*: armed launches go through hipExtLaunchKernel with kernel-bound events (one
     record per kernel, outputs unchanged); the kernel intervals lie inside the stream's own span

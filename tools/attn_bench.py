@@ -20,16 +20,12 @@ dout = torch.randn(B * N, H * 64, device="cuda").to(torch.bfloat16)
 fl = 4.0 * B * H * N * N * 64
 
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import warm_time_ms  # noqa: E402  (bench.py's isolated leg: the same warm protocol)
+
+
 def timeit(fn, it=20):
-    fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(it):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / it
+    return warm_time_ms(fn, iters=it)[0]
 
 
 o, lse = ops.attn_fwd_q2(qkv, B, N, H)
@@ -38,12 +34,17 @@ print(f"fwd q2: {ms:.4f} ms  {fl / ms / 1e9:.1f} TF/s")
 d = ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H)
 ms = timeit(lambda: ops.attn_bwd_q2(qkv, o, dout, lse, B, N, H))
 print(f"bwd q2: {ms:.4f} ms  {2 * fl / ms / 1e9:.1f} TF/s algorithmic (dQ, dK, dV, dP: 8*B*H*N^2*64)")
+# the reference-facing plain entry (ivit_attn_bwd, unscaled qkv): Q prescale copy + the same v4 pair
+qkv_u = qkv.clone()
+qkv_u[:, : H * 64] = (qkv[:, : H * 64].float() / ops.Q2_SCALE).to(torch.bfloat16)
+o_u, lse_u = ops.attn_fwd(qkv_u, B, N, H, ops.BF16)
+ms_p = timeit(lambda: ops.attn_bwd(qkv_u, o_u, dout, lse_u, B, N, H, ops.BF16))
+print(f"bwd plain (ivit_attn_bwd): {ms_p:.4f} ms = {ms_p / ms:.3f} x q2")
 
 
 def kernel_ms(fn, tags, it=20):
-    """mean execution interval per kernel (ivit_ktime_*: events bound to the kernel commands)"""
-    fn()
-    torch.cuda.synchronize()
+    """mean execution interval per kernel (ivit_ktime_*: events bound to the kernel commands), warm"""
+    warm_time_ms(fn, iters=2, reps=1)
     ops.ktime_arm(True)
     for _ in range(it):
         fn()

@@ -13,17 +13,19 @@ Inputs (same columns, Kernel_Name / Start_Timestamp / End_Timestamp in ns):
 
 --flops: algorithmic flop per launch (bench.py attn_flops) -> TFLOP/s and the fraction of the
 dense bf16 MFMA peak; --json: write the summary (bench.py reads the newest committed
-profiles/*_attn_bwd_union.json of kind rocprofv3 into roofline.frac_rocprof).
+profiles/*_attn_bwd_union.json of kind rocprofv3 into roofline.frac_rocprof, only when the kernel
+names it matched are the kernels the entry point launches now, and names the file and its time).
 """
 import argparse
 import csv
 import json
+import time
 
 PEAK_BF16_TFLOPS = 2516.6
 
 
 def union(path, names):
-    iv, n_first, own = [], 0, 0
+    iv, n_first, own, matched = [], 0, 0, set()
     with open(path) as fh:
         rows = csv.DictReader(fh)
         kind = "bench_intervals" if "Launch" in (rows.fieldnames or []) else "rocprofv3"
@@ -33,6 +35,7 @@ def union(path, names):
                 s, e = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
                 iv.append((s, e))
                 own += e - s
+                matched.add(k)
                 if names[0] in k:
                     n_first += 1
     iv.sort()
@@ -46,7 +49,8 @@ def union(path, names):
             ce = max(ce, e)
     if ce is not None:
         tot += ce - cs
-    return {"source": path, "source_kind": kind, "kernels": names, "dispatches": len(iv), "launches": n_first,
+    return {"source": path, "source_kind": kind, "kernels": names, "kernel_names": sorted(matched),
+            "generated_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()), "dispatches": len(iv), "launches": n_first,
             "union_ms": tot / 1e6, "union_us_per_launch": tot / max(n_first, 1) / 1e3,
             "own_us_per_launch": own / max(n_first, 1) / 1e3}
 

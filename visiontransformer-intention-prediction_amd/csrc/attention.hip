@@ -8,9 +8,9 @@
 //             P^T straight from the S^T accumulator (no LDS round trip) and V^T by the
 //             CDNA4 transposing LDS read.
 //   backward: dQ kernel (query block, sweep keys) and dK/dV kernel (key block, sweep
-//             queries); both recompute P from the saved LSE. No atomics. The prescaled-Q
-//             (bf16 ViT block) path runs the software-pipelined 16x16x32 v4 kernels; the plain bf16
-//             entry point keeps the v2 tile loops.
+//             queries); both recompute P from the saved LSE. No atomics. Both bf16 entry points
+//             run the software-pipelined 16x16x32 v4 kernels: the ViT block path with Q prescaled
+//             in qkv (ivit_attn_bwd_q2), the plain one (ivit_attn_bwd) on a prescaled Q copy.
 // f32 path (parity): exact-f32 MFMA GEMMs through the generic engine with the score
 //             matrix materialised in the workspace, plus row-softmax kernels.
 #include "attn_common.h"
@@ -319,289 +319,25 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
   if (q < N && hl == 0) lse[(long)z * N + q] = (m + log2f(l)) * 0.69314718055994531f;
 }
 
-// ------------------------------------------------------------------------- backward v2 (bf16)
-// Row constants for the backward in a padded layout [z][Npad] (Npad = N rounded up to 64):
-// lse2 = lse * log2(e) (+1e30 on padding rows, so their probabilities are exactly 0) and
-// delta = rowsum(dO * O) (0 on padding). 8 lanes per (z, padded row), one 16-B load of O
-// and of dO each (a wave reads 8 whole 128-B row segments), reduced across the 8 lanes.
-__global__ void attn_rows_v2_kernel(const bf16* __restrict__ o, const bf16* __restrict__ dout,
-                                    const float* __restrict__ lse, int B, int N, int Npad, int H,
-                                    float* __restrict__ lse2p, float* __restrict__ deltap) {
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long i = t >> 3;  // (z, padded row)
-  const int part = (int)(t & 7);
-  if (i >= (long)B * H * Npad) return;
-  // rows ordered n-major within (b, h): consecutive i share (b, h) -> contiguous stores
-  const int z = (int)(i / Npad), n = (int)(i - (long)z * Npad);
-  float s = 0.f;
-  if (n < N) {
-    const int b = z / H, h = z - b * H, D = H * 64;
-    const long off = ((long)b * N + n) * D + h * 64 + part * 8;
-    Pack8 x, y;
-    x.u = *(const uint4*)(o + off);
-    y.u = *(const uint4*)(dout + off);
+// ------------------------------------------------------------------------- Q prescale (plain entry)
+// ivit_attn_bwd (bf16) on unscaled qkv: q' = bf16(q * c2), rounded as the forward's PRE path
+// rounds its Q fragments, into a [B*N, D] workspace the v4 kernels read Q from (ldq = D).
+__global__ void attn_prescale_q_kernel(const bf16* __restrict__ qkv, long rows, int D, float c2,
+                                       bf16* __restrict__ q2) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;  // 8 columns per thread
+  const int cpr = D / 8;
+  if (t >= rows * cpr) return;
+  const long r = t / cpr;
+  const int c = (int)(t - r * cpr) * 8;
+  Pack8 x;
+  x.u = *(const uint4*)(qkv + r * 3 * D + c);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s = fmaf(bf2f(x.h[j]), bf2f(y.h[j]), s);
-  }
-  s += __shfl_xor(s, 1, 8);
-  s += __shfl_xor(s, 2, 8);
-  s += __shfl_xor(s, 4, 8);
-  if (part == 0) {
-    deltap[i] = s;
-    lse2p[i] = n < N ? lse[(long)z * N + n] * LOG2E : 1e30f;
-  }
-}
-
-// One dQ tile step: keys kbase.. of the K/V images against this wave's 32 queries.
-// Q2: qf holds q * c2 and nl = -lse2 in every register: S' - lse2 comes straight out of the
-// MFMA chain (nl as its initial accumulator) and p = exp2 of it, no per-score FMA.
-template <bool MASK, bool Q2 = false>
-IVIT_DEV void dq_tile(const char* kimg, const char* vimg, const bf16x8 (&qf)[4], const bf16x8 (&gf)[4], f32x16& a0,
-                      f32x16& a1, float lse2, float dlt, int kbase, int N, float c2, int lane,
-                      const f32x16& nl = f32x16{}) {
-  const int hl = lane >> 5;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    f32x16 s = Q2 ? nl : zero16(), dp;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dp[r] = -dlt;  // row constant as the initial accumulator
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 ka = *(const bf16x8*)(kimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-      const bf16x8 va = *(const bf16x8*)(vimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[ks], s, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, gf[ks], dp, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float p = Q2 ? fast_exp2(s[r]) : fast_exp2(fmaf(s[r], c2, -lse2));
-      if (MASK) {
-        const int key = kbase + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        if (key >= N) p = 0.f;
-      }
-      s[r] = p * dp[r];  // dS^T[key][q]
-    }
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      const bf16x8 xa = pack_acc(s, ss);
-      const int rb = 32 * t + 16 * ss;
-      const bf16x8 kb0 = tr_acc_order(kimg, rb, 0, lane);
-      const bf16x8 kb1 = tr_acc_order(kimg, rb, 32, lane);
-      a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, kb0, a0, 0, 0, 0);
-      a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa, kb1, a1, 0, 0, 0);
-    }
-  }
-}
-
-// dQ: 4 waves x 32 queries; K/V tiles by LDS-DMA (k-invariant offsets, ragged tail guarded),
-// tile loop unrolled by two so the LDS stage is a compile-time constant.
-// (plain bf16 entry point, unscaled Q; row constants from attn_rows_v2_kernel)
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_v2_kernel(const bf16* __restrict__ qkv,
-                                                                const bf16* __restrict__ dout,
-                                                                float* __restrict__ lse2p,
-                                                                float* __restrict__ deltap, int N, int Npad,
-                                                                int H, bf16* __restrict__ dqkv, float c2,
-                                                                float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][K|V]
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int2 bid = attn_block_id();
-  const int z = bid.y, b = z / H, h = z - b * H;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
-  const int q = bid.x * AQ + wv * 32 + (lane & 31);
-  const bool qv = q < N;
-  bf16x8 qf[4], gf[4];
-  load_row_frags(Qb + (long)q * ld, qv, lane, qf);
-  load_row_frags(dout + ((long)b * N + q) * D + h * 64, qv, lane, gf);
-  const float lse2 = qv ? lse2p[(long)z * Npad + q] : 1e30f;
-  const float dlt = qv ? deltap[(long)z * Npad + q] : 0.f;
-  f32x16 a0 = zero16(), a1 = zero16();
-  const int nt = (N + AK - 1) / AK, nfull = N / AK;
-  int off[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) off[i] = dma_off<4>(i, wv, lane, ld);
-  auto issue = [&](int kt, char* kimg, char* vimg) {
-    if (kt < nfull) {
-      const bf16* kb = Kb + (long)kt * AK * ld;
-      const bf16* vb = Vb + (long)kt * AK * ld;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int piece = wv * 2 + i;
-        glds<16>((kb + off[i]), kimg + piece * 1024);
-        glds<16>((vb + off[i]), vimg + piece * 1024);
-      }
-    } else {
-      tile_glds_w<4>(Kb, ld, kt * AK, N, kimg, wv, lane);
-      tile_glds_w<4>(Vb, ld, kt * AK, N, vimg, wv, lane);
-    }
-  };
-  auto step = [&](auto stage, int kt) {
-    constexpr int S = decltype(stage)::value;
-    if (kt + 1 < nt) issue(kt + 1, smem[S ^ 1][0], smem[S ^ 1][1]);
-    if (kt < nfull)
-      dq_tile<false>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane);
-    else
-      dq_tile<true>(smem[S][0], smem[S][1], qf, gf, a0, a1, lse2, dlt, kt * AK, N, c2, lane);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  issue(0, smem[0][0], smem[0][1]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nt; kt += 2) {
-    step(std::integral_constant<int, 0>{}, kt);
-    if (kt + 1 < nt) step(std::integral_constant<int, 1>{}, kt + 1);
-  }
-  const int qw = bid.x * AQ + wv * 32;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int qq = qw + (r & 3) + 8 * (r >> 2) + 4 * hl;
-    if (qq < N) {
-      bf16* row = dqkv + ((long)b * N + qq) * ld + h * 64;
-      row[lane & 31] = (bf16)(a0[r] * scale);
-      row[32 + (lane & 31)] = (bf16)(a1[r] * scale);
-    }
-  }
-}
-
-// One dK/dV tile step: queries of the Q/dO images (rows past N are zero with lse2 = 1e30,
-// so P = 0 there and no mask is needed) against this wave's 32 keys.
-IVIT_DEV void dkv_tile(const char* qimg, const char* gimg, const float* lrow, const float* drow,
-                       const bf16x8 (&kf)[4], const bf16x8 (&vf)[4], f32x16& dk0, f32x16& dk1, f32x16& dv0,
-                       f32x16& dv1, float c2, int lane) {
-  const int hl = lane >> 5;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 qa = *(const bf16x8*)(qimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-      const bf16x8 ga = *(const bf16x8*)(gimg + t_off(32 * t + (lane & 31), 2 * ks + hl));
-      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[ks], s, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, vf[ks], dp, 0, 0, 0);
-    }
-    {
-      // row constants read after the MFMA chains are issued (off the chains' critical path)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {  // rows (r&3) + 8(r>>2) + 4h, r = 4g + j
-        const float4 l4 = *(const float4*)(lrow + 32 * t + 8 * g + 4 * hl);
-        const float4 d4 = *(const float4*)(drow + 32 * t + 8 * g + 4 * hl);
-        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-        const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float p = fast_exp2(fmaf(s[4 * g + j], c2, -lv[j]));
-          s[4 * g + j] = p;                             // P[q][key]
-          dp[4 * g + j] = p * (dp[4 * g + j] - dv[j]);  // dS[q][key]
-        }
-      }
-    }
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      const int rb = 32 * t + 16 * ss;
-      const bf16x8 pa = pack_acc(s, ss);
-      const bf16x8 g0 = tr_acc_order(gimg, rb, 0, lane);
-      const bf16x8 g1 = tr_acc_order(gimg, rb, 32, lane);
-      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, g0, dv0, 0, 0, 0);
-      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, g1, dv1, 0, 0, 0);
-      const bf16x8 da = pack_acc(dp, ss);
-      const bf16x8 q0 = tr_acc_order(qimg, rb, 0, lane);
-      const bf16x8 q1 = tr_acc_order(qimg, rb, 32, lane);
-      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, q0, dk0, 0, 0, 0);
-      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, q1, dk1, 0, 0, 0);
-    }
-  }
-}
-
-// dK/dV: 4 waves x 32 keys; Q, dO tiles and their lse2 / delta rows by LDS-DMA.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_v2_kernel(const bf16* __restrict__ qkv,
-                                                                 const bf16* __restrict__ dout,
-                                                                 const float* __restrict__ lse2p,
-                                                                 const float* __restrict__ deltap, int N, int Npad,
-                                                                 int H, bf16* __restrict__ dqkv, float c2,
-                                                                 float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2][8192];  // [stage][Q|dO]
-  __shared__ __attribute__((aligned(16))) float srow[2][2][AK];    // [stage][lse2|delta]
-  const int tid = threadIdx.x, lane = tid & 63, hl = lane >> 5;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int2 bid = attn_block_id();
-  const int z = bid.y, b = z / H, h = z - b * H;
-  const int D = H * 64;
-  const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
-  const bf16* Gb = dout + (long)b * N * D + h * 64;
-  const float* L = lse2p + (long)z * Npad;
-  const float* Dl = deltap + (long)z * Npad;
-  const int key = bid.x * AQ + wv * 32 + (lane & 31);
-  bf16x8 kf[4], vf[4];
-  load_row_frags(Kb + (long)key * ld, key < N, lane, kf);
-  load_row_frags(Vb + (long)key * ld, key < N, lane, vf);
-  retire_loads(kf, vf);
-  f32x16 dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
-  const int nt = (N + AK - 1) / AK, nfull = N / AK;
-  int offq[2], offg[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    offq[i] = dma_off<4>(i, wv, lane, ld);
-    offg[i] = dma_off<4>(i, wv, lane, D);
-  }
-  auto issue = [&](int qt, int S) {
-    char* qimg = smem[S][0];
-    char* gimg = smem[S][1];
-    if (qt < nfull) {
-      const bf16* qb = Qb + (long)qt * AK * ld;
-      const bf16* gb = Gb + (long)qt * AK * D;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int piece = wv * 2 + i;
-        glds<16>((qb + offq[i]), qimg + piece * 1024);
-        glds<16>((gb + offg[i]), gimg + piece * 1024);
-      }
-    } else {
-      tile_glds_w<4>(Qb, ld, qt * AK, N, qimg, wv, lane);
-      tile_glds_w<4>(Gb, D, qt * AK, N, gimg, wv, lane);
-    }
-    if (wv == 0) {  // 64 lse2 + 64 delta floats (the padded arrays cover every tile row)
-      glds<4>((L + qt * AK + lane), &srow[S][0][0]);
-      glds<4>((Dl + qt * AK + lane), &srow[S][1][0]);
-    }
-  };
-  auto step = [&](auto stage, int qt) {
-    constexpr int S = decltype(stage)::value;
-    if (qt + 1 < nt) issue(qt + 1, S ^ 1);
-    dkv_tile(smem[S][0], smem[S][1], srow[S][0], srow[S][1], kf, vf, dk0, dk1, dv0, dv1, c2, lane);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int qt = 0; qt < nt; qt += 2) {
-    step(std::integral_constant<int, 0>{}, qt);
-    if (qt + 1 < nt) step(std::integral_constant<int, 1>{}, qt + 1);
-  }
-  const int kw = bid.x * AQ + wv * 32;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int kk = kw + (r & 3) + 8 * (r >> 2) + 4 * hl;
-    if (kk < N) {
-      bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
-      row[D + (lane & 31)] = (bf16)(dk0[r] * scale);
-      row[D + 32 + (lane & 31)] = (bf16)(dk1[r] * scale);
-      row[2 * D + (lane & 31)] = (bf16)dv0[r];
-      row[2 * D + 32 + (lane & 31)] = (bf16)dv1[r];
-    }
-  }
+  for (int e = 0; e < 8; ++e) x.h[e] = (bf16)((float)x.h[e] * c2);
+  *(uint4*)(q2 + r * D + c) = x.u;
 }
 
 // ------------------------------------------------------------------------- backward pipeline (prescaled Q)
-// (The round-2 "v3" structure, kept by the 16x16x32 v4 kernels below.) The v2 loops were issue-bound: per 64x32 wave-tile of the dK/dV kernel ~140 VALU beside 32
+// (The round-2 "v3" structure, kept by the 16x16x32 v4 kernels below.) The round-2 v2 loops were issue-bound: per 64x32 wave-tile of the dK/dV kernel ~140 VALU beside 32
 // MFMAs (the element-wise bf16 packing re-shuffled by v_alignbit / v_perm, accumulator copies),
 // and every S / dP chain MFMA waited (lgkmcnt) on the LDS read issued just before it. v3 keeps
 // the same algorithm and data flow, software-pipelined over 32-row units u (half a 64-row tile):
@@ -635,7 +371,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
                                                                  const bf16* __restrict__ dout,
                                                                  const float* __restrict__ nlse2p,
                                                                  const float* __restrict__ ndeltap, int N, int Npad,
-                                                                 int H, bf16* __restrict__ dqkv, float scale) {
+                                                                 int H, bf16* __restrict__ dqkv, float scale,
+                                                                 const bf16* __restrict__ qsrc, int ldq) {
   __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][Q|dO]
   __shared__ __attribute__((aligned(16))) float srow[BNS][2][AK];  // [stage][-lse2|-delta]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -645,9 +382,9 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
   const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
+  const bf16* Kb = qkv + (long)b * N * ld + D + h * 64;
+  const bf16* Vb = Kb + D;
+  const bf16* Qb = qsrc + (long)b * N * ldq + h * 64;  // q' (prescaled): in qkv, or the plain entry's copy
   const bf16* Gb = dout + (long)b * N * D + h * 64;
   const char* Ls = uniform_ptr(nlse2p + (long)z * Npad);
   const char* Ds = uniform_ptr(ndeltap + (long)z * Npad);
@@ -678,13 +415,13 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
   unsigned offq[PW], offg[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) {
-    offq[i] = 2u * dma_off16<W>(i, wv, lane, ld);
+    offq[i] = 2u * dma_off16<W>(i, wv, lane, ldq);
     offg[i] = 2u * dma_off16<W>(i, wv, lane, D);
   }
   auto issue = [&](int qt, int S) {
     char* qimg = smem[S][0];
     char* gimg = smem[S][1];
-    const char* qb = uniform_ptr(Qb + (long)qt * AK * ld);
+    const char* qb = uniform_ptr(Qb + (long)qt * AK * ldq);
     const char* gb = uniform_ptr(Gb + (long)qt * AK * D);
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
@@ -693,7 +430,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
       if (qt >= nfull) {
         const int row = piece * 8 + (lane >> 3), c = (lane & 7) ^ (row & 6);
         const int r = min(qt * AK + row, N - 1) - qt * AK;
-        oq = 2u * (unsigned)(r * ld + c * 8);
+        oq = 2u * (unsigned)(r * ldq + c * 8);
         og = 2u * (unsigned)(r * D + c * 8);
       }
       glds_s<false>(oq, qb, qimg + piece * 1024);
@@ -930,7 +667,8 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
                                                                 float* __restrict__ ndeltap, int N, int Npad, int H,
                                                                 bf16* __restrict__ dqkv, float scale,
                                                                 const bf16* __restrict__ out,
-                                                                const float* __restrict__ lse) {
+                                                                const float* __restrict__ lse,
+                                                                const bf16* __restrict__ qsrc, int ldq) {
   __shared__ __attribute__((aligned(16))) char smem[BNS][2][8192];  // [stage][K|V]
   const int tid = threadIdx.x, lane = tid & 63;
   const int g = lane >> 4, c16 = lane & 15;
@@ -939,9 +677,9 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
   const int z = bid.y, b = z / H, h = z - b * H;
   const int D = H * 64;
   const long ld = 3L * D;
-  const bf16* Qb = qkv + (long)b * N * ld + h * 64;
-  const bf16* Kb = Qb + D;
-  const bf16* Vb = Qb + 2 * D;
+  const bf16* Kb = qkv + (long)b * N * ld + D + h * 64;
+  const bf16* Vb = Kb + D;
+  const bf16* Qb = qsrc + (long)b * N * ldq + h * 64;  // q' (prescaled)
   constexpr int PW = 8 / W;
   const int qw = bid.x * (32 * W) + wv * 32;
   // B operands: lane (g, c) holds Q / dO of query qw + 16i + c, dims 32s + 8g .. +7
@@ -956,7 +694,7 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
     for (int s = 0; s < 2; ++s) {
       Pack8 pq, pg, po;
       const long orow = ((long)b * N + q) * D + h * 64 + 32 * s + 8 * g;
-      pq.u = qv ? *(const uint4*)(Qb + (long)q * ld + 32 * s + 8 * g) : make_uint4(0, 0, 0, 0);
+      pq.u = qv ? *(const uint4*)(Qb + (long)q * ldq + 32 * s + 8 * g) : make_uint4(0, 0, 0, 0);
       pg.u = qv ? *(const uint4*)(dout + orow) : make_uint4(0, 0, 0, 0);
       po.u = qv ? *(const uint4*)(out + orow) : make_uint4(0, 0, 0, 0);
       qf[i][s] = pq.v;
@@ -1208,9 +946,82 @@ long ld_scores(long N) { return (N + 7) / 8 * 8; }
 
 }  // namespace
 
+// ------------------------------------------------------------------------- kernel timing
+// ivit_ktime_arm / _read (ivit.h): while armed, the q2 entry points launch through
+// hipExtLaunchKernel with an event pair bound to the kernel command, so the elapsed time is the
+// kernel's own execution interval. Events are pooled across arm() calls.
+namespace {
+struct KtRec {
+  int tag;
+  hipEvent_t start, stop;
+};
+std::mutex kt_mu;
+bool kt_on = false;
+std::vector<KtRec> kt_recs;
+std::vector<hipEvent_t> kt_pool;
+size_t kt_used = 0;
+
+hipEvent_t kt_event() {
+  if (kt_used == kt_pool.size()) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    kt_pool.push_back(e);
+  }
+  return kt_pool[kt_used++];
+}
+
+// Launch through hipExtLaunchKernelGGL with a recorded event pair when armed, else plainly.
+template <typename K, typename... Args>
+void kt_launch(int tag, K kernel, dim3 g, dim3 b, hipStream_t st, Args... args) {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(kt_mu);
+    if (kt_on) {
+      e0 = kt_event();
+      e1 = e0 ? kt_event() : nullptr;
+      if (e0 && e1) kt_recs.push_back({tag, e0, e1});
+    }
+  }
+  if (e0 && e1)
+    hipExtLaunchKernelGGL(kernel, g, b, 0, st, e0, e1, 0, args...);
+  else
+    hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
+}
+}  // namespace
+
+
+// The v4 backward pair; Q (prescaled by c2) is read from qsrc with row stride ldq: the Q block of
+// qkv (ldq = 3D) on the q2 path, the plain entry's copy (ldq = D) otherwise.
+namespace {
+void attn_bwd_v4_launch(const void* qkv, const void* out, const void* dout, const float* lse, long B, long N, long H,
+                        void* dqkv, float* nlse2p, const void* qsrc, int ldq, hipStream_t st) {
+  const float scale = 0.125f;  // 1 / sqrt(64)
+  const long Npad = (N + AK - 1) / AK * AK;
+  float* ndeltap = nlse2p + B * H * Npad;
+  // dQ also forms the row constants (-lse2, -delta) the dK/dV kernel reads: no rows kernel.
+  // 4 waves per workgroup, two workgroups per CU: 8-wave workgroups (half the L2 -> LDS bytes,
+  // one per CU) measured 0.875 vs 0.814 ms per pair (the 8-wave tile barrier, no second
+  // independent workgroup to fill its gaps)
+  constexpr int BW = 4;
+  const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
+  // the 16x16x32 forms (v4). Same-call A/B against the 32x32x16 v3 kernels they replaced (removed):
+  // dK/dV 0.441-0.445 -> 0.406 ms, dQ 0.332-0.334 -> 0.316 ms isolated, step 44.07-44.14 -> 43.29 ms
+  // with dK/dV alone (profiles/r05_b_attn_dkv16_ab.txt, r05_c_attn_dq16_ab.txt, r05_c_ab_dkv16_*.json)
+  kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+            (const bf16*)dout, nlse2p, ndeltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse,
+            (const bf16*)qsrc, ldq);
+  kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
+            (const bf16*)dout, nlse2p, ndeltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f,
+            (const bf16*)qsrc, ldq);
+}
+}  // namespace
+
+// bf16 backward: the -lse2 and -delta rows (f32, padded to whole key tiles)
+static long attn_rows_bytes(long B, long N, long H) { return 2 * B * H * ((N + AK - 1) / AK * AK) * 4; }
+
 extern "C" long ivit_attn_workspace(int dtype, long B, long N, long H, long Dh, int backward) {
-  // bf16 backward: the -lse2 and -delta rows (f32, padded to whole key tiles)
-  if (dtype == IVIT_BF16) return backward ? 2 * B * H * ((N + AK - 1) / AK * AK) * 4 : 0;
+  // bf16 backward: the row constants + the prescaled Q copy of the plain entry (ivit_attn_bwd)
+  if (dtype == IVIT_BF16) return backward ? attn_rows_bytes(B, N, H) + B * N * H * Dh * 2 : 0;
   const long one = B * H * N * ld_scores(N) * 4;
   return backward ? 2 * one : one;
 }
@@ -1257,16 +1068,13 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
   if (B * N * H == 0) return 0;
   const long D = H * Dh, ldq = 3 * D;
   if (dtype == IVIT_BF16) {
-    dim3 g(ivit_cdiv(N, AQ), B * H);
-    const long Npad = (N + AK - 1) / AK * AK;
-    float* lse2p = (float*)work;
-    float* deltap = lse2p + B * H * Npad;
-    hipLaunchKernelGGL(attn_rows_v2_kernel, dim3(ivit_cdiv(B * H * Npad * 8, 256)), dim3(256), 0, st,
-                       (const bf16*)out, (const bf16*)dout, lse, (int)B, (int)N, (int)Npad, (int)H, lse2p, deltap);
-    hipLaunchKernelGGL(attn_bwd_dq_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout, lse2p,
-                       deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
-    hipLaunchKernelGGL(attn_bwd_dkv_v2_kernel, g, dim3(256), 0, st, (const bf16*)qkv, (const bf16*)dout,
-                       lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale * LOG2E, scale);
+    // the product's v4 pair: Q prescaled by c2 = log2(e)/sqrt(Dh) into the workspace, as the
+    // forward (ivit_attn_fwd) scales its fragments, then the q2 kernels reading Q from that copy
+    float* nlse2p = (float*)work;
+    bf16* q2 = (bf16*)((char*)work + attn_rows_bytes(B, N, H));
+    hipLaunchKernelGGL(attn_prescale_q_kernel, dim3(ivit_cdiv(B * N * D / 8, 256)), dim3(256), 0, st,
+                       (const bf16*)qkv, B * N, (int)D, scale * LOG2E, q2);
+    attn_bwd_v4_launch(qkv, out, dout, lse, B, N, H, dqkv, nlse2p, q2, (int)D, st);
     IVIT_LAUNCH_CHECK();
     return 0;
   }
@@ -1316,49 +1124,6 @@ extern "C" int ivit_attn_bwd(int dtype, const void* qkv, const void* out, const 
   IVIT_LAUNCH_CHECK();
   return 0;
 }
-
-// ------------------------------------------------------------------------- kernel timing
-// ivit_ktime_arm / _read (ivit.h): while armed, the q2 entry points launch through
-// hipExtLaunchKernel with an event pair bound to the kernel command, so the elapsed time is the
-// kernel's own execution interval. Events are pooled across arm() calls.
-namespace {
-struct KtRec {
-  int tag;
-  hipEvent_t start, stop;
-};
-std::mutex kt_mu;
-bool kt_on = false;
-std::vector<KtRec> kt_recs;
-std::vector<hipEvent_t> kt_pool;
-size_t kt_used = 0;
-
-hipEvent_t kt_event() {
-  if (kt_used == kt_pool.size()) {
-    hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
-    kt_pool.push_back(e);
-  }
-  return kt_pool[kt_used++];
-}
-
-// Launch through hipExtLaunchKernelGGL with a recorded event pair when armed, else plainly.
-template <typename K, typename... Args>
-void kt_launch(int tag, K kernel, dim3 g, dim3 b, hipStream_t st, Args... args) {
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  {
-    std::lock_guard<std::mutex> lk(kt_mu);
-    if (kt_on) {
-      e0 = kt_event();
-      e1 = e0 ? kt_event() : nullptr;
-      if (e0 && e1) kt_recs.push_back({tag, e0, e1});
-    }
-  }
-  if (e0 && e1)
-    hipExtLaunchKernelGGL(kernel, g, b, 0, st, e0, e1, 0, args...);
-  else
-    hipLaunchKernelGGL(kernel, g, b, 0, st, args...);
-}
-}  // namespace
 
 extern "C" int ivit_ktime_arm(int on) {
   std::lock_guard<std::mutex> lk(kt_mu);
@@ -1414,29 +1179,14 @@ extern "C" int ivit_attn_fwd_q2(const void* qkv, long B, long N, long H, long Dh
 
 // With q' = q c2 in qkv: P = exp2(q'k - lse2) (c2 = 1 in the kernels); dQ = scale dS K as before
 // (the gradient w.r.t. the unscaled q); dK = ln2 dS^T q' = scale dS^T q.
+// With q' = q c2 in qkv: P = exp2(q'k - lse2) (c2 = 1 in the kernels); dQ = scale dS K as before
+// (the gradient w.r.t. the unscaled q); dK = ln2 dS^T q' = scale dS^T q.
 extern "C" int ivit_attn_bwd_q2(const void* qkv, const void* out, const void* dout, const float* lse, long B, long N,
                                 long H, long Dh, void* dqkv, void* work, long work_bytes, void* stream) {
   IVIT_CHECK_ARG(Dh == 64, "ivit_attn_bwd_q2: head dim must be 64 (got %ld)", Dh);
-  IVIT_CHECK_ARG(work_bytes >= ivit_attn_workspace(IVIT_BF16, B, N, H, Dh, 1), "ivit_attn_bwd_q2: workspace too small");
+  IVIT_CHECK_ARG(work_bytes >= attn_rows_bytes(B, N, H), "ivit_attn_bwd_q2: workspace too small");
   if (B * N * H == 0) return 0;
-  hipStream_t st = ivit_stream(stream);
-  const float scale = 1.0f / sqrtf((float)Dh);
-  const long Npad = (N + AK - 1) / AK * AK;
-  float* lse2p = (float*)work;
-  float* deltap = lse2p + B * H * Npad;
-  // dQ also forms the row constants (-lse2, -delta) the dK/dV kernel reads: no rows kernel.
-  // 4 waves per workgroup, two workgroups per CU: 8-wave workgroups (half the L2 -> LDS bytes,
-  // one per CU) measured 0.875 vs 0.814 ms per pair (the 8-wave tile barrier, no second
-  // independent workgroup to fill its gaps)
-  constexpr int BW = 4;
-  const dim3 gw(ivit_cdiv(N, 32 * BW), B * H);
-  // the 16x16x32 forms (v4). Same-call A/B against the 32x32x16 v3 kernels they replaced (removed):
-  // dK/dV 0.441-0.445 -> 0.406 ms, dQ 0.332-0.334 -> 0.316 ms isolated, step 44.07-44.14 -> 43.29 ms
-  // with dK/dV alone (profiles/r05_b_attn_dkv16_ab.txt, r05_c_attn_dq16_ab.txt, r05_c_ab_dkv16_*.json)
-  kt_launch(IVIT_KT_ATTN_BWD_DQ, attn_bwd_dq_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, scale, (const bf16*)out, lse);
-  kt_launch(IVIT_KT_ATTN_BWD_DKV, attn_bwd_dkv_v4_kernel<BW>, gw, dim3(64 * BW), st, (const bf16*)qkv,
-            (const bf16*)dout, lse2p, deltap, (int)N, (int)Npad, (int)H, (bf16*)dqkv, 0.69314718055994531f);
+  attn_bwd_v4_launch(qkv, out, dout, lse, B, N, H, dqkv, (float*)work, qkv, (int)(3 * H * Dh), ivit_stream(stream));
   IVIT_LAUNCH_CHECK();
   return 0;
 }

@@ -2,8 +2,6 @@
 // torchvision-CPU-exact non-maximum suppression.
 #include "geom.h"
 
-#include <rocprim/device/device_segmented_radix_sort.hpp>
-
 #include <cmath>
 #include <cstring>
 
@@ -39,18 +37,19 @@ __global__ void iou_matrix_kernel(const float* b1, long n1, const float* b2, lon
 }
 
 // utils.py:227-257
-__global__ void decode_kernel(const float* rel, const float* anchors, const long* idx, long n, float* out) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float* d = rel + i * 6;
-  const float* a = anchors + (idx ? idx[i] : i) * 5;
-  float* o = out + i * 5;
+IVIT_DEV void decode_one(const float* d, const float* a, float* o) {
   o[0] = d[0] * a[2] + a[0];
   o[1] = d[1] * a[3] + a[1];
   o[2] = expf(d[2]) * a[2];
   o[3] = expf(d[3]) * a[3];
   const float yaw = a[4] + atan2f(d[4], d[5]);
   o[4] = atan2f(sinf(yaw), cosf(yaw));
+}
+
+__global__ void decode_kernel(const float* rel, const float* anchors, const long* idx, long n, float* out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  decode_one(rel + i * 6, anchors + (idx ? idx[i] : i) * 5, out + i * 5);
 }
 
 // ---- NMS (torchvision CPU nms_kernel_impl): stable descending sort; f32 corners/areas/IoU;
@@ -192,7 +191,7 @@ __global__ __launch_bounds__(64) void nms_mask_kernel(const float* __restrict__ 
   nms_mask_body(sb, n, nw, th, mask, rb, cb0);
 }
 
-constexpr int NMS_MAXW = 1024;  // n <= 65536
+constexpr int NMS_MAXW = 2048;  // n <= 131072
 
 // The greedy walk of torchvision's nms over the suppression mask (one workgroup per sample):
 // column block c (64 sorted boxes) is settled by wave 0 on SCALAR registers (each diagonal word
@@ -220,7 +219,6 @@ IVIT_DEV void nms_scan_body(const unsigned long long* __restrict__ mask, long n,
   }
   for (int c = 0; c < nw; ++c) {
     if (threadIdx.x < 64) {
-      const long row = (long)c * 64 + lane;
       const unsigned long long diag = diag_n;
       const int ord = ord_n;
       const unsigned dlo = (unsigned)diag, dhi = (unsigned)(diag >> 32);
@@ -282,31 +280,137 @@ __global__ __launch_bounds__(256) void nms_scan_kernel(const unsigned long long*
   nms_scan_body(mask, n, nw, order, keep, count);
 }
 
-// ---- batched NMS: sample s owns rows seg[s] .. seg[s+1]-1 of every per-row array and the
-// mask words mask_off[s] .. ; blockIdx.y (rank / sorted boxes / scan) or blockIdx.z (mask)
-// selects the sample, so all samples' kernels run in one launch each (the single-workgroup
-// scan of one sample no longer serialises the batch).
-// keys / values of the segmented sort: the score (+0.0f: a -0 score ties with +0 as in torch's
-// comparison sort) and the row's local index.
-__global__ void nms_keys_b_kernel(const float* __restrict__ scores, const long* __restrict__ seg, float* __restrict__ key,
-                                  int* __restrict__ idx) {
-  const int sm = blockIdx.y;
-  const long o = seg[sm], n = seg[sm + 1] - o;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  key[o + i] = scores[o + i] + 0.0f;
-  idx[o + i] = (int)i;
+// ---- batched NMS and the fused eval post-processing -------------------------------------------
+// Sample s owns rows lo(s) .. lo(s) + n(s) - 1 of every per-row array and the mask words mo(s) ..:
+// either host prefix offsets (seg [S+1], mask_off [S]: ivit_nms_batched) or a fixed capacity per
+// sample with the row counts on the device (ivit_eval_post: nothing is read back before the NMS).
+struct SegView {
+  const long* seg;   // [S+1] row offsets, or null
+  const long* moff;  // [S] mask word offsets (with seg)
+  const int* cnt;    // [S] rows per sample (without seg)
+  long row_stride, mask_stride;
+  IVIT_DEV long lo(int s) const { return seg ? seg[s] : (long)s * row_stride; }
+  IVIT_DEV long n(int s) const { return seg ? seg[s + 1] - seg[s] : (long)cnt[s]; }
+  IVIT_DEV long mo(int s) const { return seg ? moff[s] : (long)s * mask_stride; }
+};
+
+// One sample per workgroup of PS_T threads (16 waves) for the selection and the score sort.
+constexpr int PS_T = 1024;
+constexpr int PS_D = 16;  // radix digits: 4 key bits per pass
+
+// Ascending order of the key = torch's stable descending sort of the score: the IEEE order made
+// unsigned, inverted; s + 0.0f makes -0 tie with +0 as torch's comparison sort does.
+IVIT_DEV unsigned desc_key(float s) {
+  const unsigned u = __float_as_uint(s + 0.0f);
+  return ~(u ^ ((u >> 31) ? 0xffffffffu : 0x80000000u));
 }
 
-__global__ void nms_sorted_boxes_b_kernel(const float* __restrict__ b, const int* __restrict__ order,
-                                          const long* __restrict__ seg, float* __restrict__ sb) {
-  const int sm = blockIdx.y;
-  const long o = seg[sm], n = seg[sm + 1] - o;
-  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
-  const float* q = b + (o + order[o + p]) * 5;
+// Exclusive prefix of v over the workgroup in thread order; the total goes to wsum[16].
+// wsum: 17 LDS words. The caller separates two calls by a barrier.
+IVIT_DEV unsigned block_excl_scan(unsigned v, unsigned* wsum) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  if (wid == 0) {
+    const unsigned w = lane < PS_T / 64 ? wsum[lane] : 0u;
+    unsigned z = w;
+#pragma unroll
+    for (int o = 1; o < PS_T / 64; o <<= 1) {
+      const unsigned y = __shfl_up(z, o, 64);
+      if (lane >= o) z += y;
+    }
+    if (lane < PS_T / 64) wsum[lane] = z - w;
+    if (lane == PS_T / 64 - 1) wsum[16] = z;
+  }
+  __syncthreads();
+  return wsum[wid] + x - v;
+}
+
+// Stable LSD radix sort of n (key, value) pairs by ascending key, by one workgroup. Thread t owns
+// the contiguous chunk [t*I, t*I + I), I = ceil(n / PS_T): it counts its chunk's digits into its
+// own histogram column (hist[d * PS_T + t], no atomics), the digit-major exclusive scan of the
+// columns gives every (digit, thread) its first slot, and the thread scatters its chunk in order —
+// so equal digits keep their order and the sort is stable. Thread t scans entries 16t .. 16t + 15,
+// which all belong to digit t / 64: wave d's sum is digit d's total, and a pass in which one digit
+// holds all n keys moves nothing and is skipped (the scores of one eval sample share their top
+// bits). Keys / values ping-pong between (k0, v0) and (k1, v1), global scratch that stays in L2;
+// returns which pair holds the result. n < 2^31.
+IVIT_DEV int block_radix_sort(unsigned* k0, int* v0, unsigned* k1, int* v1, int n, unsigned* hist, unsigned* wsum,
+                              int* skip) {
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int I = (n + PS_T - 1) / PS_T;
+  const int b0 = min(t * I, n), b1 = min(b0 + I, n);
+  int cur = 0;
+  for (int shift = 0; shift < 32; shift += 4) {
+    const unsigned* ki = cur ? k1 : k0;
+    const int* vi = cur ? v1 : v0;
+    unsigned* ko = cur ? k0 : k1;
+    int* vo = cur ? v0 : v1;
+#pragma unroll
+    for (int d = 0; d < PS_D; ++d) hist[d * PS_T + t] = 0u;
+    if (t == 0) *skip = 0;
+    for (int i = b0; i < b1; ++i) ++hist[((ki[i] >> shift) & 15u) * PS_T + t];
+    __syncthreads();
+    unsigned c[PS_D], run = 0;
+#pragma unroll
+    for (int j = 0; j < PS_D; ++j) {
+      c[j] = hist[t * PS_D + j];
+      run += c[j];
+    }
+    unsigned x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+      const unsigned w = lane < PS_D ? wsum[lane] : 0u;
+      unsigned z = w;
+#pragma unroll
+      for (int o = 1; o < PS_D; o <<= 1) {
+        const unsigned y = __shfl_up(z, o, 64);
+        if (lane >= o) z += y;
+      }
+      if (lane < PS_D) {
+        wsum[lane] = z - w;
+        if (w == (unsigned)n) *skip = 1;
+      }
+    }
+    __syncthreads();
+    unsigned off = wsum[wid] + x - run;
+#pragma unroll
+    for (int j = 0; j < PS_D; ++j) {
+      hist[t * PS_D + j] = off;
+      off += c[j];
+    }
+    __syncthreads();
+    if (!*skip) {
+      for (int i = b0; i < b1; ++i) {
+        const unsigned k = ki[i];
+        const unsigned slot = ((k >> shift) & 15u) * PS_T + t;
+        const unsigned p = hist[slot];
+        hist[slot] = p + 1u;
+        ko[p] = k;
+        vo[p] = vi[i];
+      }
+      cur ^= 1;
+    }
+    __syncthreads();
+  }
+  return cur;
+}
+
+// torchvision's nms input for sorted row p: corners of box[order[p]] and the area (utils.py:266-272)
+IVIT_DEV void sorted_corners(const float* q, float* d) {
   const float x1 = q[0] - q[2] / 2.f, y1 = q[1] - q[3] / 2.f, x2 = q[0] + q[2] / 2.f, y2 = q[1] + q[3] / 2.f;
-  float* d = sb + (o + p) * 5;
   d[0] = x1;
   d[1] = y1;
   d[2] = x2;
@@ -314,26 +418,135 @@ __global__ void nms_sorted_boxes_b_kernel(const float* __restrict__ b, const int
   d[4] = (x2 - x1) * (y2 - y1);
 }
 
+// ivit_nms_batched, stage 1: one workgroup per sample — keys from the scores, the stable
+// descending sort, the sorted corner boxes. k0/v0/k1/v1: [total] scratch.
+__global__ __launch_bounds__(PS_T) void nms_sort_b_kernel(const float* __restrict__ b, const float* __restrict__ scores,
+                                                          const long* __restrict__ seg, unsigned* k0, int* v0,
+                                                          unsigned* k1, int* v1, int* __restrict__ order,
+                                                          float* __restrict__ sb) {
+  __shared__ unsigned hist[PS_D * PS_T];
+  __shared__ unsigned wsum[20];
+  __shared__ int skip;
+  const int sm = blockIdx.x;
+  const long o = seg[sm];
+  const int n = (int)(seg[sm + 1] - o);
+  for (int i = threadIdx.x; i < n; i += PS_T) {
+    k0[o + i] = desc_key(scores[o + i]);
+    v0[o + i] = i;
+  }
+  __syncthreads();
+  const int r = block_radix_sort(k0 + o, v0 + o, k1 + o, v1 + o, n, hist, wsum, &skip);
+  const int* ord = (r ? v1 : v0) + o;
+  for (int p = threadIdx.x; p < n; p += PS_T) {
+    const int q = ord[p];
+    order[o + p] = q;
+    sorted_corners(b + (o + q) * 5, sb + (o + p) * 5);
+  }
+}
+
 // grid (ceil(nwmax / NMS_CB), nwmax, samples)
-__global__ __launch_bounds__(64) void nms_mask_b_kernel(const float* __restrict__ sb_all, const long* __restrict__ seg,
-                                                        const long* __restrict__ mask_off, NmsThr th,
+__global__ __launch_bounds__(64) void nms_mask_b_kernel(const float* __restrict__ sb_all, SegView sv, NmsThr th,
                                                         unsigned long long* __restrict__ mask_all) {
   const int sm = blockIdx.z;
-  const long o = seg[sm], n = seg[sm + 1] - o;
+  const long o = sv.lo(sm), n = sv.n(sm);
   const int nw = (int)((n + 63) / 64);
   const int cb0 = blockIdx.x * NMS_CB, rb = blockIdx.y;
   if (cb0 >= nw || rb >= nw || cb0 + NMS_CB <= rb) return;
-  nms_mask_body(sb_all + o * 5, n, nw, th, mask_all + mask_off[sm], rb, cb0);
+  nms_mask_body(sb_all + o * 5, n, nw, th, mask_all + sv.mo(sm), rb, cb0);
 }
 
-__global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long long* __restrict__ mask_all,
-                                                         const long* __restrict__ seg,
-                                                         const long* __restrict__ mask_off,
+__global__ __launch_bounds__(256) void nms_scan_b_kernel(const unsigned long long* __restrict__ mask_all, SegView sv,
                                                          const int* __restrict__ order_all,
                                                          long* __restrict__ keep_all, long* __restrict__ count) {
   const int sm = blockIdx.x;
-  const long o = seg[sm], n = seg[sm + 1] - o;
-  nms_scan_body(mask_all + mask_off[sm], n, (int)((n + 63) / 64), order_all + o, keep_all + o, count + sm);
+  const long o = sv.lo(sm), n = sv.n(sm);
+  nms_scan_body(mask_all + sv.mo(sm), n, (int)((n + 63) / 64), order_all + o, keep_all + o, count + sm);
+}
+
+// ---- eval post-processing (eval_vit.py:156-176) for a whole batch, capacity NA rows per sample.
+struct PostWs {
+  int* n;            // [S] rows passing the confidence threshold
+  int* anchor;       // [S*NA] anchor index of compacted row p
+  float* score;      // [S*NA]
+  float* box;        // [S*NA*5] decoded (utils.py:227-257)
+  unsigned *k0, *k1;  // sort scratch
+  int *v0, *v1;
+  int* order;        // [S*NA] stable descending score order (compacted-row indices)
+  float* sb;         // [S*NA*5] sorted corners + area
+  long* keep;        // [S*NA] kept compacted-row indices in score order
+  unsigned long long* mask;
+};
+
+// torch's f32 sigmoid on the GPU: 1 / (1 + exp(-x)), IEEE division (UnarySpecialOpsKernel.cu)
+IVIT_DEV float torch_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// eval_vit.py:159-168 for sample blockIdx.x: scores = sigmoid(cls); where(score >= conf) in anchor
+// order (a workgroup-wide exclusive scan of per-thread counts: thread t owns anchors
+// [t*I, t*I + I)); the compacted scores, anchor indices and decoded boxes; then apply_nms's stable
+// descending score order and its sorted corner boxes. NaN logits fail the threshold, as in torch.
+__global__ __launch_bounds__(PS_T) void post_select_kernel(const float* __restrict__ cls, const float* __restrict__ rel,
+                                                           const float* __restrict__ anchors, int NA, float conf,
+                                                           PostWs w) {
+  __shared__ unsigned hist[PS_D * PS_T];
+  __shared__ unsigned wsum[20];
+  __shared__ int skip;
+  const int sm = blockIdx.x, t = threadIdx.x;
+  const long base = (long)sm * NA;
+  const float* c = cls + base;
+  const float* r = rel + base * 6;
+  const int I = (NA + PS_T - 1) / PS_T;
+  const int a0 = min(t * I, NA), a1 = min(a0 + I, NA);
+  unsigned np = 0;
+  for (int a = a0; a < a1; ++a) np += torch_sigmoid(c[a]) >= conf;
+  unsigned p = block_excl_scan(np, wsum);
+  const int n = (int)wsum[16];
+  for (int a = a0; a < a1; ++a) {
+    const float s = torch_sigmoid(c[a]);
+    if (s >= conf) {
+      const long q = base + p;
+      w.anchor[q] = a;
+      w.score[q] = s;
+      w.k0[q] = desc_key(s);
+      w.v0[q] = (int)p;
+      decode_one(r + (long)a * 6, anchors + (long)a * 5, w.box + q * 5);
+      ++p;
+    }
+  }
+  if (t == 0) w.n[sm] = n;
+  __syncthreads();
+  const int res = block_radix_sort(w.k0 + base, w.v0 + base, w.k1 + base, w.v1 + base, n, hist, wsum, &skip);
+  const int* ord = (res ? w.v1 : w.v0) + base;
+  for (int i = t; i < n; i += PS_T) {
+    const int q = ord[i];
+    w.order[base + i] = q;
+    sorted_corners(w.box + (base + q) * 5, w.sb + (base + i) * 5);
+  }
+}
+
+// eval_vit.py:172-175: kept row j of sample s (blockIdx.y) -> its score, decoded box and the
+// argmax intention of its anchor (first maximum; a NaN is the maximum, the first NaN wins — torch's
+// argmax), packed at s * NA + j.
+__global__ void post_gather_kernel(const long* __restrict__ kcnt, const float* __restrict__ intent, int NA, int K,
+                                   PostWs w, float* __restrict__ out_score, float* __restrict__ out_box,
+                                   long* __restrict__ out_int) {
+  const int sm = blockIdx.y;
+  const long j = (long)blockIdx.x * 256 + threadIdx.x;
+  if (j >= kcnt[sm]) return;
+  const long base = (long)sm * NA, k = base + w.keep[base + j], q = base + j;
+  out_score[q] = w.score[k];
+#pragma unroll
+  for (int e = 0; e < 5; ++e) out_box[q * 5 + e] = w.box[k * 5 + e];
+  const float* lg = intent + (base + w.anchor[k]) * K;
+  int best = 0;
+  float bv = lg[0];
+  for (int e = 1; e < K; ++e) {
+    const float v = lg[e];
+    if (bv == bv && (v > bv || v != v)) {
+      bv = v;
+      best = e;
+    }
+  }
+  out_int[q] = best;
 }
 
 }  // namespace
@@ -411,25 +624,15 @@ extern "C" int ivit_nms(const float* boxes_xywha, const float* scores, long n, d
 // stage). seg: [S+1] int64 row offsets (device); mask_off: [S] int64 word offsets of each
 // sample's [n_s, ceil(n_s/64)] suppression mask (device). keep[seg[s] ..] receives sample s's kept
 // LOCAL indices in score order, count[s] their number. The score order is a stable descending
-// segmented radix sort (rocPRIM; ties keep the row order, as torch's stable sort). Workspace:
-// ivit_nms_batched_workspace(n_samples, total, mask_words) bytes.
+// sort (nms_sort_b_kernel: one workgroup per sample; ties keep the row order, as torch's stable
+// sort). Workspace: ivit_nms_batched_workspace(n_samples, total, mask_words) bytes.
 namespace {
-size_t nms_sort_temp_bytes(long n_samples, long total) {
-  size_t bytes = 0;
-  if (rocprim::segmented_radix_sort_pairs_desc(nullptr, bytes, (const float*)nullptr, (float*)nullptr,
-                                               (const int*)nullptr, (int*)nullptr, (unsigned)total,
-                                               (unsigned)n_samples, (const long*)nullptr, (const long*)nullptr) !=
-      hipSuccess)
-    return 0;
-  return bytes;
-}
 long al16(long b) { return (b + 15) / 16 * 16; }
 }  // namespace
 
 extern "C" long ivit_nms_batched_workspace(long n_samples, long total, long mask_words) {
   if (n_samples <= 0 || total <= 0) return 64;
-  return al16(4 * total) + al16(20 * total) + al16(8 * mask_words) + 2 * al16(4 * total) + al16(4 * total) +
-         al16((long)nms_sort_temp_bytes(n_samples, total)) + 256 + 64;
+  return al16(4 * total) + al16(20 * total) + al16(8 * mask_words) + 4 * al16(4 * total) + 64;
 }
 
 extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, const long* seg, const long* mask_off,
@@ -455,26 +658,84 @@ extern "C" int ivit_nms_batched(const float* boxes_xywha, const float* scores, c
   w += al16(20 * total);
   unsigned long long* mask = (unsigned long long*)w;
   w += al16(8 * mask_words);
-  float* key = (float*)w;
+  unsigned* k0 = (unsigned*)w;
   w += al16(4 * total);
-  float* key_sorted = (float*)w;
+  unsigned* k1 = (unsigned*)w;
   w += al16(4 * total);
-  int* idx = (int*)w;
+  int* v0 = (int*)w;
   w += al16(4 * total);
-  w = (char*)(((uintptr_t)w + 255) & ~(uintptr_t)255);
-  size_t tb = nms_sort_temp_bytes(n_samples, total);
-  const int gx = ivit_cdiv(max_n, 256);
-  hipLaunchKernelGGL(nms_keys_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, scores, seg, key, idx);
-  const hipError_t e = rocprim::segmented_radix_sort_pairs_desc(w, tb, key, key_sorted, idx, order, (unsigned)total,
-                                                               (unsigned)n_samples, seg, seg + 1, 0, 32, st);
-  if (e != hipSuccess) {
-    ivit_set_error("ivit_nms_batched: segmented sort: %s", hipGetErrorString(e));
-    return (int)e;
+  int* v1 = (int*)w;
+  const SegView sv{seg, mask_off, nullptr, 0, 0};
+  hipLaunchKernelGGL(nms_sort_b_kernel, dim3(n_samples), dim3(PS_T), 0, st, boxes_xywha, scores, seg, k0, v0, k1, v1,
+                     order, sb);
+  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(ivit_cdiv(nwmax, NMS_CB), nwmax, n_samples), dim3(64), 0, st, sb, sv,
+                     nms_thr(iou_thr), mask);
+  hipLaunchKernelGGL(nms_scan_b_kernel, dim3(n_samples), dim3(256), 0, st, mask, sv, order, keep, count);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
+// Eval post-processing for a batch (eval_vit.py:156-176): four launches, no host round trip.
+namespace {
+struct PostLayout {
+  long bytes;
+  long off[12];
+};
+PostLayout post_layout(long B, long NA) {
+  const long R = B * NA, nw = (NA + 63) / 64;
+  const long sz[12] = {4 * B, 4 * R, 4 * R, 20 * R, 4 * R, 4 * R, 4 * R, 4 * R, 4 * R, 20 * R, 8 * R, 8 * R * nw};
+  PostLayout L{0, {}};
+  for (int i = 0; i < 12; ++i) {
+    L.off[i] = L.bytes;
+    L.bytes += al16(sz[i]);
   }
-  hipLaunchKernelGGL(nms_sorted_boxes_b_kernel, dim3(gx, n_samples), dim3(256), 0, st, boxes_xywha, order, seg, sb);
-  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(ivit_cdiv(nwmax, NMS_CB), nwmax, n_samples), dim3(64), 0, st, sb, seg,
-                     mask_off, nms_thr(iou_thr), mask);
-  hipLaunchKernelGGL(nms_scan_b_kernel, dim3(n_samples), dim3(256), 0, st, mask, seg, mask_off, order, keep, count);
+  L.bytes += 16;  // alignment slack
+  return L;
+}
+}  // namespace
+
+extern "C" long ivit_eval_post_workspace(long B, long NA) {
+  if (B <= 0 || NA <= 0) return 64;
+  return post_layout(B, NA).bytes;
+}
+
+extern "C" int ivit_eval_post(const float* cls, const float* box_rel, const float* intent, const float* anchors, long B,
+                              long NA, long K, float conf_thr, double iou_thr, float* out_scores, float* out_boxes,
+                              long* out_intent, long* out_count, void* work, long work_bytes, void* stream) {
+  IVIT_CHECK_ARG(B >= 0 && B < 65536 && NA >= 0 && K >= 1, "ivit_eval_post: bad sizes (B %ld, NA %ld, K %ld)", B, NA,
+                 K);
+  IVIT_CHECK_ARG(NA <= 64L * NMS_MAXW, "ivit_eval_post: NA=%ld exceeds %d", NA, 64 * NMS_MAXW);
+  IVIT_CHECK_ARG(work_bytes >= ivit_eval_post_workspace(B, NA), "ivit_eval_post: workspace too small");
+  hipStream_t st = ivit_stream(stream);
+  if (B == 0) return 0;
+  if (NA == 0) {
+    (void)hipMemsetAsync(out_count, 0, sizeof(long) * B, st);
+    IVIT_LAUNCH_CHECK();
+    return 0;
+  }
+  const PostLayout L = post_layout(B, NA);
+  char* base = (char*)(((uintptr_t)work + 15) & ~(uintptr_t)15);
+  PostWs w;
+  w.n = (int*)(base + L.off[0]);
+  w.anchor = (int*)(base + L.off[1]);
+  w.score = (float*)(base + L.off[2]);
+  w.box = (float*)(base + L.off[3]);
+  w.k0 = (unsigned*)(base + L.off[4]);
+  w.k1 = (unsigned*)(base + L.off[5]);
+  w.v0 = (int*)(base + L.off[6]);
+  w.v1 = (int*)(base + L.off[7]);
+  w.order = (int*)(base + L.off[8]);
+  w.sb = (float*)(base + L.off[9]);
+  w.keep = (long*)(base + L.off[10]);
+  w.mask = (unsigned long long*)(base + L.off[11]);
+  const int nw = (int)((NA + 63) / 64);
+  const SegView sv{nullptr, nullptr, w.n, NA, NA * nw};
+  hipLaunchKernelGGL(post_select_kernel, dim3(B), dim3(PS_T), 0, st, cls, box_rel, anchors, (int)NA, conf_thr, w);
+  hipLaunchKernelGGL(nms_mask_b_kernel, dim3(ivit_cdiv(nw, NMS_CB), nw, B), dim3(64), 0, st, w.sb, sv,
+                     nms_thr(iou_thr), w.mask);
+  hipLaunchKernelGGL(nms_scan_b_kernel, dim3(B), dim3(256), 0, st, w.mask, sv, w.order, w.keep, out_count);
+  hipLaunchKernelGGL(post_gather_kernel, dim3(ivit_cdiv(NA, 256), B), dim3(256), 0, st, out_count, intent, (int)NA,
+                     (int)K, w, out_scores, out_boxes, out_intent);
   IVIT_LAUNCH_CHECK();
   return 0;
 }
