@@ -587,21 +587,13 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
         dk[jj][e] = mfma16(word8(ud[jj]), tq[e], dk[jj][e]);
       }
   }
-  // lane holds rows key 16j + 4g + r, column d = 16e + c16
-#pragma unroll
-  for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int kk = kw + 16 * jj + 4 * g + r;
-      if (kk < N) {
-        bf16* row = dqkv + ((long)b * N + kk) * ld + h * 64;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          row[D + 16 * e + c16] = (bf16)(dk[jj][e][r] * scale);
-          row[2 * D + 16 * e + c16] = (bf16)dv[jj][e][r];
-        }
-      }
-    }
+  // lane holds rows key 16j + 4g + r, column d = 16e + c16; stored through LDS as whole rows (2-byte
+  // stores from the C layout: pair 0.7220-0.7222 vs 0.7187-0.7190 ms, profiles/r06_b_attn_epi_ab.txt)
+  __syncthreads();  // every wave is past its last stage read: the stages become the store tiles
+  char* tl = &smem[0][0][0] + wv * 2 * 4608;
+  bf16* base = dqkv + (long)b * N * ld + h * 64;
+  wave_tile_store(tl, dk, scale, base + D, ld, kw, N, lane);
+  wave_tile_store(tl + 4608, dv, 1.0f, base + 2 * D, ld, kw, N, lane);
 }
 
 // ------------------------------------------------------------------------- dQ v4 (16x16x32)
@@ -877,18 +869,9 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
     const int S = nfull % BNS;
     dq16_tile_masked(smem[S][0], smem[S][1], qf, gf, nl, nd, dq, nfull * AK, N, lane);
   }
-  // lane holds rows q = qw + 16i + 4g + r, column d = 16e + c16
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int qq = qw + 16 * i + 4 * g + r;
-      if (qq < N) {
-        bf16* row = dqkv + ((long)b * N + qq) * ld + h * 64;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) row[16 * e + c16] = (bf16)(dq[i][e][r] * scale);
-      }
-    }
+  // lane holds rows q = qw + 16i + 4g + r, column d = 16e + c16 (stored through LDS as whole rows)
+  __syncthreads();  // every wave is past its last stage read
+  wave_tile_store(&smem[0][0][0] + wv * 4608, dq, scale, dqkv + (long)b * N * ld + h * 64, ld, qw, N, lane);
 }
 
 // ------------------------------------------------------------------------- f32 row kernels

@@ -76,6 +76,33 @@ IVIT_DEV int dma_off16(int i, int wv, int lane, long ld) {
   return (int)(row * ld) + c * 8;
 }
 
+// Epilogue of the 16x16x32 backward kernels: one wave's [32 rows][64 columns] output tile, held in
+// the C layout (lane (g, c16) holds rows 16i + 4g + r, column 16e + c16 of v[i][e][r]), goes through
+// the wave's own 4.5-KiB LDS region (rows 144 B apart: the 2-byte writes of lane groups g and g + 1
+// land 16 banks apart) and out as whole 128-B rows, 8 lanes per row, 16 B per lane: 4 stores per lane
+// instead of 32 two-byte ones. The caller has passed a barrier after the last read of the region
+// (it reuses the tile stages). Rows row0 + k < nrows are stored at dst + (row0 + k) * ld.
+IVIT_DEV void wave_tile_store(char* lds, const f32x4 (&v)[2][4], float scale, bf16* dst, long ld, int row0, int nrows,
+                              int lane) {
+  const int g = lane >> 4, c16 = lane & 15;
+  bf16* t = (bf16*)lds;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t[(16 * i + 4 * g + r) * 72 + 16 * e + c16] = (bf16)(v[i][e][r] * scale);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int row = 8 * k + (lane >> 3), ch = lane & 7;
+    const uint4 x = *(const uint4*)(lds + row * 144 + ch * 16);
+    if (row0 + row < nrows) *(uint4*)(dst + (long)(row0 + row) * ld + ch * 8) = x;
+  }
+}
+
 IVIT_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
