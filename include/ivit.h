@@ -28,8 +28,21 @@ extern "C" {
 #define IVIT_ACT_RELU 2
 #define IVIT_ACT_GELU_D 3 /* ivit_linear_fwd_panel only: GELU, second output = GELU'(pre-activation) */
 
+/* Tuning knobs (no effect on results; process-wide; defaults from the environment variable named,
+ * read once when the library loads):
+ *   IVIT_KNOB_WIDE_EPI   (IVIT_WIDE_EPI, default 0): epilogue form of the wide row-panel kernels —
+ *                        0 the LDS-tile form for every epilogue, 1 transposed accumulators for the
+ *                        Q-prescale and GELU + GELU' outputs, 2 transposed for all;
+ *   IVIT_KNOB_CONV_PANEL (IVIT_CONV_PANEL, default 1): 0 runs the stride-1 bf16 convolutions on the
+ *                        128 x 128 engine instead of the panel kernels (the tests compare the two). */
+#define IVIT_KNOB_WIDE_EPI 0
+#define IVIT_KNOB_CONV_PANEL 1
+#define IVIT_KNOB_COUNT 2
+
 const char* ivit_version(void);
 const char* ivit_last_error(void);
+int ivit_set_knob(int knob, int value);
+long ivit_get_knob(int knob);
 
 /* ---- Linear layers: timm Attention.qkv/proj, Mlp.fc1/fc2 (reached from model_vit.py:64,71,119)
  *      and the adapters nn.Linear(384,192) (model_vit.py:82-83).                              */

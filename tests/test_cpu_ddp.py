@@ -237,3 +237,103 @@ def test_grad_order_interleaves_streams_and_tail_bucket():
     # a model without the two-stream backbone: registration order
     lin = nn.Linear(3, 4)
     assert grad_order(lin) == list(lin.parameters())
+
+
+class TwoStream(nn.Module):
+    """Two independent branches (the LiDAR / map ViT streams' shape) joined by a fusion layer."""
+
+    def __init__(self):
+        super().__init__()
+        self.l0, self.l1 = nn.Linear(8, 16), nn.Linear(16, 16)
+        self.m0, self.m1 = nn.Linear(4, 16), nn.Linear(16, 16)
+        self.fuse = nn.Linear(32, 15)
+
+    def forward(self, lidar, mp):
+        hl = self.l1(torch.relu(self.l0(lidar)))
+        hm = self.m1(torch.relu(self.m0(mp)))
+        o = self.fuse(torch.cat([hl, hm], 1))
+        return o[:, :1], o[:, 1:7], o[:, 7:]
+
+
+def _interleaved_order(m):
+    """The order ddp.grad_order builds for IntentNetViT: the two streams' layers interleaved in
+    forward order (l0, m0, l1, m1), then the fusion — buckets fill from its end."""
+    return [p for mod in (m.l0, m.m0, m.l1, m.m1, m.fuse) for p in mod.parameters()]
+
+
+def _world4_worker(rank, world, port):
+    _init(rank, world, port)
+    from ddp import GradBuckets
+    torch.manual_seed(0)
+    model = TwoStream()
+    # tiny buckets (one or two parameters each) + a tail bucket for the first-registered (last-ready)
+    # parameters: several collectives per backward, launched from the hooks in fill order
+    gb = GradBuckets(_interleaved_order(model), bucket_mb=0.002, last_bucket_mb=0.0006)
+    assert len(gb.buckets) >= 4
+    assert {id(p) for p in gb.buckets[-1].params} <= {id(p) for p in model.l0.parameters()}
+    for step in range(3):
+        state = {k: v.clone() for k, v in model.state_dict().items()}
+        gb.zero_grad()
+        g = torch.Generator().manual_seed(100 * step + rank)
+        x, mm = torch.randn(6, 8, generator=g), torch.randn(6, 4, generator=g)
+        c, b, i = model(x, mm)
+        _loss(c, b, i, None, None)["loss"].backward()
+        gb.finish()
+        acc = None
+        for r in range(world):  # the mean over ranks of single-process gradients
+            ref = TwoStream()
+            ref.load_state_dict(state)
+            g = torch.Generator().manual_seed(100 * step + r)
+            xr, mr = torch.randn(6, 8, generator=g), torch.randn(6, 4, generator=g)
+            cr, br, ir = ref(xr, mr)
+            _loss(cr, br, ir, None, None)["loss"].backward()
+            gs = [p.grad for p in ref.parameters()]
+            acc = gs if acc is None else [a + q for a, q in zip(acc, gs)]
+        for p, r_ in zip(model.parameters(), acc):
+            torch.testing.assert_close(p.grad, r_ / world, rtol=1e-5, atol=1e-6)
+        with torch.no_grad():
+            for p in model.parameters():
+                p.add_(p.grad, alpha=-0.1)
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    other = flat.clone()
+    dist.broadcast(other, 0)
+    assert torch.equal(flat, other)
+    dist.destroy_process_group()
+
+
+def test_grad_buckets_world4_interleaved_order_and_tail():
+    """World 4 over gloo: the interleaved two-stream bucket order with a tail bucket — every rank
+    launches its bucket all-reduces in the same order from the post-accumulate hooks (gloo pairs
+    collectives by issue order: a mismatch gives wrong sums), the result is the mean of the four
+    ranks' gradients, and the replicas stay identical."""
+    mp.spawn(_world4_worker, args=(4, _port()), nprocs=4, join=True)
+
+
+def test_comm_stream_collectives_guard():
+    """The comm-stream form needs torch >= 2.8 and no blocking wait; otherwise GradBuckets takes the
+    asynchronous process-group-stream form."""
+    from ddp import GradBuckets, comm_stream_collectives_ok
+    assert comm_stream_collectives_ok("2.10.0+rocm7.0", {})
+    assert comm_stream_collectives_ok("2.8.0", {"TORCH_NCCL_BLOCKING_WAIT": "0"})
+    assert not comm_stream_collectives_ok("2.7.1+rocm6.3", {})
+    assert not comm_stream_collectives_ok("2.10.0", {"TORCH_NCCL_BLOCKING_WAIT": "1"})
+    assert not comm_stream_collectives_ok("2.10.0", {"NCCL_BLOCKING_WAIT": "1"})
+    gb = GradBuckets(nn.Linear(3, 4).parameters(), bucket_mb=1.0)
+    assert gb.pg_stream == (not comm_stream_collectives_ok())
+
+
+def test_tail_bucket_stops_at_dtype_change():
+    """last_bucket_mb takes parameters from the front only while device and dtype match the first
+    one: every bucket holds one dtype, and a backward through mixed dtypes fills all of them."""
+    from ddp import GradBuckets
+    a = nn.Parameter(torch.randn(5, dtype=torch.float64))
+    b = nn.Parameter(torch.randn(7))
+    c = nn.Parameter(torch.randn(3))
+    gb = GradBuckets([a, b, c], bucket_mb=1.0, last_bucket_mb=1.0)
+    for bk in gb.buckets:
+        assert all(p.dtype == bk.flat.dtype for p in bk.params)
+    assert [p for p in gb.buckets[-1].params] == [a]
+    gb.zero_grad()
+    (a.sum() * 2 + b.sum() * 3 + c.sum()).backward()
+    gb.finish()
+    assert torch.equal(a.grad, torch.full((5,), 2.0, dtype=torch.float64)) and torch.equal(b.grad, torch.full((7,), 3.0))

@@ -67,12 +67,11 @@ def test_linear_fwd_dgrad_wgrad(M, N, K, cd):
 
 
 @pytest.mark.parametrize("M,N,K", [(4133, 512, 1024), (2100, 384, 520), (4096, 1152, 768)])
-def test_linear_big_tiles(M, N, K, monkeypatch):
-    """gemm_bf16_big_kernel (256-row tiles, BN 256 / 128; KC and MN-contiguous B) through the
-    linear fwd / GELU / residual / dgrad / GELU-grad entry points, ragged M, N and K edges."""
+def test_linear_engine_ragged_shapes(M, N, K):
+    """The LDS-DMA GEMM engine (KC and MN-contiguous B) through the linear fwd / GELU / residual /
+    dgrad / GELU-grad entry points at ragged M, N and K edges and long K."""
     import ops
     from _lib import ACT_GELU, BF16
-    monkeypatch.setenv("IVIT_GEMM_BIG", "2")
     x, w, b = _lin_case(M, N, K, torch.bfloat16)
     xd, wd, bd = ops.cast(x.to(DEV), torch.bfloat16), ops.cast(w.to(DEV), torch.bfloat16), b.to(DEV)
     xr, wr = xd.float().cpu().double(), wd.float().cpu().double()
@@ -441,9 +440,10 @@ def test_conv_bn_stats_fused(B, H, W, Cin, Cout, k):
     assert _rel(s1.invstd, 1.0 / torch.sqrt(ref.var(0, unbiased=False) + 1e-5)) < 1e-5
 
 
-def test_conv_panel_fusion_shape_vs_engine(monkeypatch):
+def test_conv_panel_fusion_shape_vs_engine(request):
     """Full fusion-block shape (B = 8, 50 x 90, 512 -> 512, k = 3): panel kernel vs the 128 x 128
-    engine (IVIT_CONV_PANEL=0), forward and data gradient — same bf16 products, f32 sums."""
+    engine (ivit_set_knob(IVIT_KNOB_CONV_PANEL, 0)), forward and data gradient — same bf16 products,
+    f32 sums."""
     import ops
     from _lib import BF16
     torch.manual_seed(3)
@@ -455,7 +455,9 @@ def test_conv_panel_fusion_shape_vs_engine(monkeypatch):
     d1 = ops.conv_dgrad(xh, B, H, W, wp, BF16, torch.float32, w=w)
     dy = (torch.randn(B * H * W, C, device=DEV) * 0.5).bfloat16()
     g1, _ = ops.conv_wgrad(dy, xh, B, H, W, C, C, 3, BF16)
-    monkeypatch.setenv("IVIT_CONV_PANEL", "0")
+    from _lib import KNOB_CONV_PANEL, lib
+    lib.ivit_set_knob(KNOB_CONV_PANEL, 0)
+    request.addfinalizer(lambda: lib.ivit_set_knob(KNOB_CONV_PANEL, 1))
     y0 = ops.conv_fwd(xh, B, H, W, wp, None, BF16, torch.float32)
     d0 = ops.conv_dgrad(xh, B, H, W, wp, BF16, torch.float32, w=w)
     g0, _ = ops.conv_wgrad(dy, xh, B, H, W, C, C, 3, BF16)
@@ -628,16 +630,23 @@ def test_linear_dgrad_ln_bwd_fused(M, K, xs):
         assert _rel(dxs.float(), r2) < 4e-3
 
 
+def _set_wide_epi(epi, request):
+    """The wide row-panel epilogue form for one test (ivit_set_knob), back to 0 after it."""
+    from _lib import KNOB_WIDE_EPI, lib
+    lib.ivit_set_knob(KNOB_WIDE_EPI, int(epi))
+    request.addfinalizer(lambda: lib.ivit_set_knob(KNOB_WIDE_EPI, 0))
+
+
 @pytest.mark.parametrize("M,N,K,mode", [(36008, 1152, 384, "qs"), (36008, 1536, 384, "gelu"), (300, 768, 128, "gelu"),
                                         (145, 1536, 384, "dgelu"), (36008, 1536, 384, "dgelu"), (1, 384, 64, "qs"),
                                         (36008, 384, 384, "dgrad"), (77, 384, 384, "dgrad")])
 @pytest.mark.parametrize("epi", ["0", "2"])
-def test_panel_wide(M, N, K, mode, epi, monkeypatch):
+def test_panel_wide(M, N, K, mode, epi, request):
     """Row-panel wide GEMMs (ivit_linear_fwd_panel / ivit_linear_dgrad_gelu_panel) vs the generic
     engine on the same bf16 operands (qkv with the prescaled Q block, fc1 + GELU + pre-activation,
     fc2 dgrad x GELU'): equal up to f32 summation order and the bf16 rounding of the output. Both
-    epilogue forms: IVIT_WIDE_EPI=0 (the default LDS-tile form), 2 (transposed accumulators)."""
-    monkeypatch.setenv("IVIT_WIDE_EPI", epi)
+    epilogue forms: ivit_set_knob(IVIT_KNOB_WIDE_EPI) 0 (the default LDS-tile form), 2 (transposed accumulators)."""
+    _set_wide_epi(epi, request)
     import ops
     from _lib import ACT_GELU, BF16
     g = torch.Generator().manual_seed(M + N + K)
@@ -669,12 +678,12 @@ def test_panel_wide(M, N, K, mode, epi, monkeypatch):
 
 @pytest.mark.parametrize("M,N,K", [(36008, 1536, 384), (300, 768, 128), (145, 1536, 384), (1, 384, 64)])
 @pytest.mark.parametrize("epi", ["0", "1", "2"])
-def test_panel_gelu_derivative_pair(M, N, K, epi, monkeypatch):
+def test_panel_gelu_derivative_pair(M, N, K, epi, request):
     """fc1 with GELU' as its second output (act GELU_D: y = gelu(z), g = gelu'(z) from the f32 z =
     x W^T + b) and the fc2 dgrad that multiplies by it (ivit_linear_dgrad_mul_panel), vs torch on
     the same bf16 operands: z in f64, exact-erf GELU / GELU' (bf16-output tolerance); every
-    epilogue form (IVIT_WIDE_EPI 0: LDS tile, 1: transposed GELU_D, 2: transposed for both)."""
-    monkeypatch.setenv("IVIT_WIDE_EPI", epi)
+    epilogue form (IVIT_KNOB_WIDE_EPI 0: LDS tile, 1: transposed GELU_D, 2: transposed for both)."""
+    _set_wide_epi(epi, request)
     import ops
     from _lib import ACT_GELU_D, BF16
     g = torch.Generator().manual_seed(7 * M + N + K)
@@ -975,6 +984,29 @@ def test_nms_random_vs_oracle(thr):
         want.append(ref)
     for i, (k, w) in enumerate(zip(utils.nms_batched(bl, sl, thr), want)):
         assert np.array_equal(k.cpu().numpy(), w), i
+
+
+def test_nms_huge_areas_take_the_exact_division():
+    """Boxes with areas near FLT_MAX / 4 (decoded boxes with a huge exp(dw)): the union is >= 2^126,
+    where rcp(u) would be subnormal, so the fast IoU test must defer to the exact division — keep
+    indices bit-exact vs the oracle, single and batched."""
+    from oracle import ivit_oracle as O
+    import utils
+    g = torch.Generator().manual_seed(21)
+    n = 300
+    side = 1.0e19  # area 1e38 ~ FLT_MAX / 3.4: the union of two such boxes is past 2^126 (8.5e37)
+    cx = torch.rand(n, generator=g) * side * 2
+    cy = torch.rand(n, generator=g) * side * 2
+    w = side * (0.5 + torch.rand(n, generator=g))
+    h = side * (0.5 + torch.rand(n, generator=g)) * 0.7
+    b = torch.stack([cx, cy, w, h, torch.zeros(n)], 1).float()
+    s = torch.round(torch.rand(n, generator=g) * 16) / 16
+    for thr in (0.2, 0.05, 0.5):
+        ref = O.nms_numpy(b.numpy(), s.numpy(), thr)
+        assert np.array_equal(utils.apply_nms(b.to(DEV), s.to(DEV), thr).cpu().numpy(), ref), thr
+        k = utils.nms_batched([b.to(DEV), b[:100].to(DEV)], [s.to(DEV), s[:100].to(DEV)], thr)
+        assert np.array_equal(k[0].cpu().numpy(), ref)
+        assert np.array_equal(k[1].cpu().numpy(), O.nms_numpy(b[:100].numpy(), s[:100].numpy(), thr))
 
 
 def test_standalone_activation_and_head_modules():

@@ -1,5 +1,5 @@
 """Fusion-block convolution timings (B = 8, 50 x 90 map): forward and data gradient through the
-288 x 256 panel kernel (conv_panel.hip) and the 128 x 128 engine (IVIT_CONV_PANEL=0), alternating
+288 x 256 panel kernel (conv_panel.hip) and the 128 x 128 engine (ivit_set_knob(IVIT_KNOB_CONV_PANEL, 0)), alternating
 in one process; HIP events around 20 back-to-back launches.
 
     python tools/conv_bench.py [--panel-only]   (--panel-only: the fusion shapes on the panel kernels)
@@ -28,7 +28,7 @@ def timed(fn, reps=20):
 def main():
     panel_only = "--panel-only" in sys.argv
     import ops
-    from _lib import BF16
+    from _lib import BF16, KNOB_CONV_PANEL, lib
     dev = torch.device("cuda", 0)
     B, H, W = 8, 50, 90
     M = B * H * W
@@ -40,7 +40,7 @@ def main():
         fl = 2.0 * M * cout * cin * k * k
         for rep in range(2):
             for mode in (("1",) if panel_only else ("1", "0")):
-                os.environ["IVIT_CONV_PANEL"] = mode
+                lib.ivit_set_knob(KNOB_CONV_PANEL, int(mode))
                 tf = timed(lambda: ops.conv_fwd(x, B, H, W, wp, None, BF16, torch.float32))
                 td = timed(lambda: ops.conv_dgrad(dy, B, H, W, wp, BF16, torch.float32, w=w))
                 tw = timed(lambda: ops.conv_wgrad(dy, x, B, H, W, cin, cout, k, BF16))
@@ -48,7 +48,7 @@ def main():
                 print(f"{cin}->{cout} k{k} {name}: fwd {tf:7.1f} us ({fl / tf / 1e6:6.1f} TF/s)  "
                       f"dgrad(+pack) {td:7.1f} us ({fl / td / 1e6:6.1f} TF/s)  "
                       f"wgrad(+reduce) {tw:7.1f} us ({fl / tw / 1e6:6.1f} TF/s)", flush=True)
-    os.environ["IVIT_CONV_PANEL"] = "1"
+    lib.ivit_set_knob(KNOB_CONV_PANEL, 1)
     if panel_only:
         return
     # head conv data gradient (75 channels packed to 80): engine vs the panel kernel on rows zero-padded to 128

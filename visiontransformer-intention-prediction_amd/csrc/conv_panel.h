@@ -21,7 +21,8 @@ bool conv_wgrad_panel_ok(long M, long Cout, long Cin, long ks, long lddy);
 int conv_wgrad_panel_splits(long M, long Cout, long N);
 int conv_wgrad_panel_launch(const bf16* dY, long lddy, const bf16* X, int Bn, int H, int W, int Cin, int Cout, int ks,
                             float* slab, int splits, hipStream_t st);
-// IVIT_CONV_PANEL=0 turns the panel kernel off (A/B against the 128x128 engine); default on.
+// ivit_set_knob(IVIT_KNOB_CONV_PANEL, 0) turns the panel kernels off (the 128x128 engine instead: the
+// tests compare the two); default on.
 bool conv_panel_enabled();
 
 }  // namespace ivit

@@ -454,10 +454,7 @@ __global__ void pack_conv_t_kernel(const float* __restrict__ w, long Cout, long 
 
 }  // namespace
 
-bool conv_panel_enabled() {
-  const char* v = getenv("IVIT_CONV_PANEL");
-  return v ? atoi(v) != 0 : true;
-}
+bool conv_panel_enabled() { return ivit_knob(IVIT_KNOB_CONV_PANEL) != 0; }
 
 bool conv_panel_ok(long M, long N, long Cin, long lda, long ks) {
   return M >= CP_BM && N >= 128 && N % 8 == 0 && Cin % 64 == 0 && lda % 8 == 0 && (ks == 1 || ks == 3 || ks == 5) &&

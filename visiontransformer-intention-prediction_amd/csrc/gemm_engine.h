@@ -878,140 +878,7 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void gemm_bf16_glds_kern
   epilogue_tile((float*)smem + wv * (32 * EP_LD), acc, epi, z, split, m0 + wm * 64, n0 + wn * 64, M, N, lane);
 }
 
-// ----------------------------------------------------------------------------- 256-row bf16 kernel
-// The 128x128 tile streams 32 KiB per K step for 2.1 MFLOP: at two workgroups per CU the
-// LDS-DMA traffic (one 1-KiB global_load_lds per wave-instruction through the CU's address
-// path) is as long as the MFMA work, so long-K GEMMs stall on loads (34 % of peak at 4096^3).
-// Here a workgroup of 4 waves owns a 256 x BN tile (BN = 256 or 128), each wave 128 x BN/2
-// (4 x BN/64 MFMA blocks; the 256 accumulator registers of BN = 256 live in AGPRs), one
-// workgroup per CU: half (BN = 256) or 3/4 (BN = 128) of the load traffic per flop. MN-
-// contiguous operands are staged as 128-column halves (the frag_mn image layout).
-template <class LA, class LB, class EPI, bool A_KC, bool B_KC, int BN>
-__global__ __launch_bounds__(256, 1) void gemm_bf16_big_kernel(LA la_, LB lb_, EPI epi_, int M, int N, int K,
-                                                               int tilesM, int tilesN) {
-  constexpr int BM = 256, NJ = BN / 64;
-  constexpr int SA = BM * 128, SB = BN * 128, STAGE = SA + SB;
-  constexpr int PA = 8, PB = BN / 32;  // 1-KiB pieces per wave per K tile (A: 32, B: BN/8 in total)
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wm = wv >> 1, wn = wv & 1;
-  const int tiles = tilesM * tilesN;
-  const int flat = xcd_remap(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y);
-  const int z = flat / tiles, lin = flat - z * tiles;
-  const bool tmin = tilesN > tilesM;
-  const int tm = tmin ? lin % tilesM : lin / tilesN, tn = tmin ? lin / tilesM : lin - (lin / tilesN) * tilesN;
-  const LA la = la_.bind(z);
-  const LB lb = lb_.bind(z);
-  const EPI epi = epi_.bind(z);
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = (K + GBK16 - 1) / GBK16;
-  // per-lane DMA sources: KC images take pieces of 8 rows; MN images are 128-column halves of
-  // 16 pieces (4 k-rows each), PA / PB split evenly over the halves
-  constexpr int HA = A_KC ? 1 : 2, HB = B_KC ? 1 : BN / 128;
-  constexpr int QA = PA / HA, QB = PB / HB;  // pieces per wave per image (half)
-  typename LA::Pre preA[PA];
-  typename LB::Pre preB[PB];
-  const bool fastA = la.fast_ok(A_KC), fastB = lb.fast_ok(B_KC);
-#pragma unroll
-  for (int h = 0; h < HA; ++h)
-#pragma unroll
-    for (int i = 0; i < QA; ++i) preA[h * QA + i] = la.pre(A_KC, wv * QA + i, lane, m0 + h * 128);
-#pragma unroll
-  for (int h = 0; h < HB; ++h)
-#pragma unroll
-    for (int i = 0; i < QB; ++i) preB[h * QB + i] = lb.pre(B_KC, wv * QB + i, lane, n0 + h * 128);
-  auto issue = [&](int stage, int k0) {
-    const bool full = k0 + GBK16 <= K;
-    char* ia = smem + stage * STAGE;
-    char* ib = ia + SA;
-#pragma unroll
-    for (int h = 0; h < HA; ++h) {
-      typename LA::Pre pa[QA];
-#pragma unroll
-      for (int i = 0; i < QA; ++i) pa[i] = preA[h * QA + i];
-      glds_operand<QA>(la, z, A_KC, ia + h * (SA / HA), wv, lane, m0 + h * 128, k0, K, fastA && full, pa);
-    }
-#pragma unroll
-    for (int h = 0; h < HB; ++h) {
-      typename LB::Pre pb[QB];
-#pragma unroll
-      for (int i = 0; i < QB; ++i) pb[i] = preB[h * QB + i];
-      glds_operand<QB>(lb, z, B_KC, ib + h * (SB / HB), wv, lane, n0 + h * 128, k0, K, fastB && full, pb);
-    }
-  };
-
-  f32x16 acc[4][NJ];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  if (nk > 0) issue(0, 0);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      issue(cur ^ 1, (kt + 1) * GBK16);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PA + PB) : "memory");  // this tile's pieces landed
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    const char* ia = smem + cur * STAGE;
-    const char* ib = ia + SA;
-    // one wave per SIMD: the fragments of k-slice t+1 are read while the 4*NJ MFMAs of slice t run
-    bf16x8 fa[2][4], fb[2][NJ];
-    auto ldf = [&](int t, bf16x8 (&xa)[4], bf16x8 (&xb)[NJ]) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rb0 = wm * 128 + 32 * i;  // rows of half wm when A is MN-contiguous
-        xa[i] = A_KC ? frag_kc(ia, rb0 + (lane & 31), 2 * t + (lane >> 5))
-                     : frag_mn(ia + wm * (SA / 2), 16 * t, 32 * i, lane);
-      }
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int cb0 = wn * (BN / 2) + 32 * j;
-        xb[j] = B_KC ? frag_kc(ib, cb0 + (lane & 31), 2 * t + (lane >> 5))
-                     : frag_mn(ib + (cb0 / 128) * (SB / HB), 16 * t, cb0 % 128, lane);
-      }
-    };
-    ldf(0, fa[0], fb[0]);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t < 3) ldf(t + 1, fa[(t + 1) & 1], fb[(t + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[t & 1][i], fb[t & 1][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  // epilogue in 64 x 64 sub-tiles through the wave's LDS slice (the stages are free now)
-  float* ep = (float*)smem + wv * (32 * EP_LD);
-#pragma unroll
-  for (int ib2 = 0; ib2 < 2; ++ib2)
-#pragma unroll
-    for (int jb = 0; jb < NJ / 2; ++jb) {
-      f32x16 sub[2][2] = {{acc[2 * ib2][2 * jb], acc[2 * ib2][2 * jb + 1]},
-                          {acc[2 * ib2 + 1][2 * jb], acc[2 * ib2 + 1][2 * jb + 1]}};
-      epilogue_tile(ep, sub, epi, z, 0, m0 + wm * 128 + 64 * ib2, n0 + wn * (BN / 2) + 64 * jb, M, N, lane);
-    }
-}
-
 // ----------------------------------------------------------------------------- launcher
-// 256-row tiles (gemm_bf16_big_kernel) for single-split GEMMs: IVIT_GEMM_BIG=1 where they pay
-// (M >= 2048, K >= 1024, N % 256 == 0), 2 for every shape with N >= 256 (tests), 0 off (default:
-// this model's shapes give too few 256x256 tiles at one workgroup per CU). Read per launch so a
-// test can switch it (tests/test_gpu_ops.py covers both paths).
-inline int gemm_big_mode() {
-  const char* v = getenv("IVIT_GEMM_BIG");
-  return v ? atoi(v) : 0;
-}
 // dtype_bf16: which kernel. batch: number of z. splits: split-K factor (kchunk multiple
 // of the K tile). Grid: x = tiles (XCD-remapped), y = batch * splits.
 template <bool A_KC, bool B_KC, class LA, class LB, class EPI>
@@ -1029,25 +896,8 @@ int launch_gemm(bool bf16_path, const LA& la, const LB& lb, const EPI& epi, int 
   }
   if (bf16_path) {
     if constexpr (LA::kGlds && LB::kGlds) {
-      if constexpr (!BiasOnes<EPI>::v) {
-        // 256x256 tiles where they pay (measured, tools/gemm_bench.py): long K and N a multiple of
-        // 256 (the fusion convolutions; 4096^3 160 -> 140 us). Short-K token GEMMs and N = 384
-        // lose on the one-workgroup-per-CU quantisation (fc2 fwd 61 -> 71 us at BN = 128).
-        const int bm = gemm_big_mode();
-        if (bm && splits == 1 && ((M >= 2048 && K >= 1024 && N % 256 == 0) || bm == 2) && N >= 256) {
-          const int tM = ivit_cdiv(M, 256);
-          if (N % 256 == 0 || bm != 2) {
-            const int tN = ivit_cdiv(N, 256);
-            hipLaunchKernelGGL((gemm_bf16_big_kernel<LA, LB, EPI, A_KC, B_KC, 256>), dim3(tM * tN, batch), dim3(256),
-                               0, st, la, lb, epi, M, N, K, tM, tN);
-          } else {
-            const int tN = ivit_cdiv(N, 128);
-            hipLaunchKernelGGL((gemm_bf16_big_kernel<LA, LB, EPI, A_KC, B_KC, 128>), dim3(tM * tN, batch), dim3(256),
-                               0, st, la, lb, epi, M, N, K, tM, tN);
-          }
-          return 0;
-        }
-      }
+      // (a 256-row tile kernel, one workgroup per CU, was faster on 4096^3 only — 160 -> 140 us —
+      // and slower or level on this model's shapes at one workgroup per CU; removed in round 6)
       hipLaunchKernelGGL((gemm_bf16_glds_kernel<LA, LB, EPI, A_KC, B_KC, 2>), grid, dim3(256), 0, st, la, lb, epi, M,
                          N, K, tilesM, tilesN, splits, kchunk);
     } else

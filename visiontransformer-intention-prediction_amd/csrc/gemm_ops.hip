@@ -1,6 +1,7 @@
 // C-ABI GEMM-shaped ops: linear fwd/dgrad/wgrad, patch embedding, NHWC convolutions.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "gemm_engine.h"
 #include "conv_panel.h"
@@ -25,6 +26,23 @@ void ivit_set_error(const char* fmt, ...) {
   va_end(ap);
 }
 extern "C" const char* ivit_last_error(void) { return g_err; }
+
+// Tuning knobs: defaults, then the IVIT_WIDE_EPI / IVIT_CONV_PANEL environment variables read ONCE
+// when the library loads; ivit_set_knob changes them at run time (tests, A/B tools).
+static int knob_env(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+static int g_knobs[IVIT_KNOB_COUNT] = {knob_env("IVIT_WIDE_EPI", 0), knob_env("IVIT_CONV_PANEL", 1)};
+int ivit_knob(int knob) { return knob >= 0 && knob < IVIT_KNOB_COUNT ? g_knobs[knob] : 0; }
+extern "C" int ivit_set_knob(int knob, int value) {
+  IVIT_CHECK_ARG(knob >= 0 && knob < IVIT_KNOB_COUNT, "ivit_set_knob: unknown knob %d", knob);
+  IVIT_CHECK_ARG(knob != IVIT_KNOB_WIDE_EPI || (value >= 0 && value <= 2), "ivit_set_knob: wide epilogue form %d",
+                 value);
+  g_knobs[knob] = value;
+  return 0;
+}
+extern "C" long ivit_get_knob(int knob) { return ivit_knob(knob); }
 extern "C" const char* ivit_version(void) { return "ivit-hip 0.1 gfx950"; }
 
 // ----------------------------------------------------------------------------- reductions

@@ -130,7 +130,9 @@ IVIT_DEV bool nms_suppresses(float ix1, float iy1, float ix2, float iy2, float i
   // disjoint boxes (most pairs): inter = 0 gives 0 / u = +-0 or NaN, never above a threshold >= 0
   if (th.fast && !(inter > 0.f)) return false;
   const float u = (ia + ca) - inter;
-  if (th.fast && u >= 1.17549435e-38f && u < INFINITY && inter < INFINITY) {  // u normal: rcp(u) finite
+  // u in [2^-126, 2^126): rcp(u) is a normal float too (at u >= 2^126 it would be subnormal, flushed
+  // or imprecise, and q could land on the wrong side of the margin)
+  if (th.fast && u >= 1.17549435e-38f && u < 0x1p126f && inter < INFINITY) {
     const float q = inter * __builtin_amdgcn_rcpf(u);
     if (q >= th.hi) return true;
     if (q <= th.lo) return false;

@@ -34,6 +34,9 @@ void ivit_set_error(const char* fmt, ...);
   } while (0)
 
 static inline hipStream_t ivit_stream(void* s) { return (hipStream_t)s; }
+
+// Tuning knobs (ivit_set_knob / ivit_get_knob, ivit.h): process-wide ints read by the launchers.
+int ivit_knob(int knob);
 static inline int ivit_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // ---------------------------------------------------------------- LDS DMA

@@ -961,10 +961,13 @@ int patch_wgrad_raster(const bf16* dtok, const float* img, long B, long C, long 
   const int Wp = (int)(W / 8), Np = (int)((H / 8) * Wp), M = (int)(B * Np), J = ivit_cdiv(M, WG_MU);
   float* slab = (float*)work;
   const long n = (long)((C + 1) / 2) * D * 128;
-  // The persistent form. Measured and removed: a split-along-patches form (in-step
-  // 1.08 vs 1.01 ms, LiDAR) and an XCD-sharded persistent form (1.387 vs 1.116 ms isolated);
-  // diagnostic builds with the dtok chunk fixed (L2-resident) 0.988 and the raster chunk fixed
-  // 1.002 ms — neither operand's source bounds the kernel by itself.
+  // Dispatch: P > 0 (at least 32 channel pairs, patch rows >= 32 wide: the LiDAR raster) runs the
+  // wave-specialised kernel on the XCD-sharded schedule (each XCD's P workgroups walk the same
+  // chunk range over different channel pairs, so the token-gradient rows come from that XCD's L2)
+  // + the 8-way partial reduce; patch rows >= 32 wide otherwise (the map raster) run the
+  // wave-specialised kernel on the linear schedule + its reduce; narrower grids patch_wgrad_kernel.
+  // (Round 4 measured and removed an older all-waves XCD-sharded form, 1.387 vs 1.116 ms; the
+  // history is in DESIGN.md §8.)
   if ((D * 128) % 256) return IVIT_ERR_UNSUPPORTED;  // the reduce's block-uniform pair
   const int P = pw_shard_p(C, Wp, J);
   if (P > 0 && (D * 128) % 4 == 0 && ((uintptr_t)dW & 15) == 0 && (C * 64) % 4 == 0) {

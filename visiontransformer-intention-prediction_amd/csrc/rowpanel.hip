@@ -599,19 +599,17 @@ auto ln_kernel(bool st) {
   return st ? rowpanel_ln_kernel<BWD, true> : rowpanel_ln_kernel<BWD, false>;
 }
 // The wide kernel build for (EPI, stamps, epilogue form): EV = 1 needs 16-B aligned rows of Y
-// (and of P when the kernel writes it); IVIT_WIDE_EPI=0 forces the LDS-tile epilogue (A/B).
+// (and of P when the kernel writes it). wide_epi: 0 (default) the LDS-tile form for every
+// epilogue — in the bench step, beside the other ViT stream's attention, it beat the transposed
+// form for QS / GELUD in 6 of 7 same-call pairs (43.67-43.87 vs 43.80-44.17 ms), though alone the
+// transposed one is faster (GELUD 89.5 -> 85.8 us) and DMUL's LDS-tile form is faster either way
+// (76.2 vs 83.6 us); 1: transposed for QS / GELUD; 2: transposed for all. Set by
+// ivit_set_knob(IVIT_KNOB_WIDE_EPI) (the tests cover every form).
 template <int EPI>
 void launch_wide(dim3 g, hipStream_t st, bool ev1, u64* sb, const bf16* A, long lda, int M, int K, const u32x4* wp,
                  int N, const float* bias, int qcols, float qscale, bf16* Y, long ldy, bf16* P, long ldp) {
-  // Default (IVIT_WIDE_EPI unset or 0): the LDS-tile form for every epilogue — in the bench step,
-  // beside the other ViT stream's attention, it beat the transposed form for QS / GELUD in 6 of 7
-  // same-call pairs (43.67-43.87 vs 43.80-44.17 ms), though alone the transposed one is faster
-  // (GELUD 89.5 -> 85.8 us) and DMUL's LDS-tile form is faster either way (76.2 vs 83.6 us).
-  // IVIT_WIDE_EPI=1: transposed for QS / GELUD; 2: transposed for all.
-  const char* env = getenv("IVIT_WIDE_EPI");  // read per launch: the tests switch it in-process
-  const int mode = env ? atoi(env) : 0;
-  const bool off = mode == 0;
-  ev1 = ev1 && !off && (EPI == EPI_QS || EPI == EPI_GELUD || mode == 2);
+  const int mode = ivit_knob(IVIT_KNOB_WIDE_EPI);
+  ev1 = ev1 && mode != 0 && (EPI == EPI_QS || EPI == EPI_GELUD || mode == 2);
   auto k = ev1 ? (sb ? rowpanel_wide_kernel<EPI, 4, true, 1> : rowpanel_wide_kernel<EPI, 4, false, 1>)
                : (sb ? rowpanel_wide_kernel<EPI, 4, true, 0> : rowpanel_wide_kernel<EPI, 4, false, 0>);
   hipLaunchKernelGGL(k, g, dim3(256), 0, st, A, lda, M, K, wp, N, bias, qcols, qscale, Y, ldy, P, ldp, sb);

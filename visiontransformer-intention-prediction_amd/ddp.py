@@ -97,7 +97,7 @@ _ON_COMM = object()  # a bucket whose collective was enqueued on the comm stream
 
 
 class _Bucket:
-    __slots__ = ("params", "flat", "offs", "ready", "work", "events", "streams")
+    __slots__ = ("params", "flat", "offs", "ready", "work", "streams")
 
     def __init__(self, params, flat, offs):
         self.params = params
@@ -105,8 +105,22 @@ class _Bucket:
         self.offs = offs
         self.ready = 0
         self.work = None
-        self.events = []
         self.streams = {}  # producing streams of this bucket's gradients (stream_id -> stream)
+
+
+def comm_stream_collectives_ok(version=None, env=None):
+    """True when a synchronous-op all-reduce issued on a side stream is enqueued on that stream
+    without blocking the host: torch >= 2.8's ProcessGroupNCCL (asyncOp = false runs the collective
+    on the current stream), and no TORCH_NCCL_BLOCKING_WAIT / NCCL_BLOCKING_WAIT (wait() would then
+    block the autograd thread in every bucket's hook)."""
+    version = torch.__version__ if version is None else version
+    env = os.environ if env is None else env
+    try:
+        major, minor = (int(x) for x in version.split("+")[0].split(".")[:2])
+    except ValueError:
+        return False
+    blocking = any(env.get(k, "0") not in ("", "0") for k in ("TORCH_NCCL_BLOCKING_WAIT", "NCCL_BLOCKING_WAIT"))
+    return (major, minor) >= (2, 8) and not blocking
 
 
 class GradSink:
@@ -123,8 +137,6 @@ class GradSink:
 
     def claim(self):
         gb = self.gb
-        if not gb.direct:
-            return None
         if id(self.p) not in gb._fresh or self.p.grad is None or self.p.grad.data_ptr() != self.view.data_ptr():
             return None
         return self.view
@@ -172,7 +184,7 @@ class GradBuckets:
             lcap, lbytes = max(1, int(last_bucket_mb * (1 << 20))), 0
             while ps:
                 nb = ps[0].numel() * ps[0].element_size()
-                if tail and lbytes + nb > lcap:
+                if tail and (lbytes + nb > lcap or ps[0].device != tail[0].device or ps[0].dtype != tail[0].dtype):
                     break
                 tail.append(ps.pop(0))
                 lbytes += nb
@@ -181,11 +193,12 @@ class GradBuckets:
         self._fresh = set()  # ids of parameters whose bucket view is zeroed and not written yet
         self._seen = set()  # ids of parameters whose gradient arrived in this backward
         self._direct = set()  # ids of parameters written through their GradSink in this backward
-        self.direct = os.environ.get("IVIT_DDP_DIRECT", "1") == "1"
-        self.per_param_events = os.environ.get("IVIT_DDP_EVENTS", "stream") == "param"
-        # IVIT_DDP_PG_STREAM=1: asynchronous collectives on the process group's own stream (a fifth
-        # stream beside the step's four; kept for the A/B against the comm-stream form)
-        self.pg_stream = os.environ.get("IVIT_DDP_PG_STREAM", "0") == "1"
+        # the comm-stream form (a synchronous-op all-reduce issued inside torch.cuda.stream(comm))
+        # relies on torch >= 2.8 ProcessGroupNCCL enqueuing it on the current stream without
+        # blocking the host; otherwise (older torch, or TORCH_NCCL_BLOCKING_WAIT making wait()
+        # block) the asynchronous form on the process group's own stream keeps the all-reduces
+        # overlapping the backward
+        self.pg_stream = not comm_stream_collectives_ok()
         cur, cur_bytes = [], 0
         for p in reversed(ps):
             nb = p.numel() * p.element_size()
@@ -259,10 +272,7 @@ class GradBuckets:
             # stream recorded when the bucket fills covers all of them (a few waits per bucket
             # instead of one event + wait per parameter)
             st = torch.cuda.current_stream(b.flat.device)
-            if self.per_param_events:
-                b.events.append(st.record_event())
-            else:
-                b.streams[st.stream_id] = st
+            b.streams[st.stream_id] = st
         if b.ready == len(b.params):
             self._launch(b)
 
@@ -271,9 +281,6 @@ class GradBuckets:
             comm = self._comm_stream(b.flat.device)
             for st in b.streams.values():
                 comm.wait_event(st.record_event())
-            for ev in b.events:
-                comm.wait_event(ev)
-            b.events = []
             b.streams = {}
             with torch.cuda.stream(comm):
                 if self.pg_stream:
@@ -307,7 +314,8 @@ class GradBuckets:
         for b in self.buckets:
             if b.work is None:
                 if b.flat.is_cuda:  # unused parameters: everything queued so far is final
-                    b.events = [torch.cuda.current_stream(b.flat.device).record_event()]
+                    st = torch.cuda.current_stream(b.flat.device)
+                    b.streams[st.stream_id] = st
                 self._launch(b)
         inv = 1.0 / self.world
         for b in self.buckets:
@@ -315,7 +323,6 @@ class GradBuckets:
                 b.work.wait()
             b.work = None
             b.ready = 0
-            b.events = []
             b.streams = {}
         if getattr(self, "_comm", None) is not None:
             torch.cuda.current_stream(self._comm.device).wait_stream(self._comm)

@@ -125,7 +125,9 @@ class TwoStreamViTBackbone(nn.Module):
     def _cdt(self):
         return BF16 if getattr(self, "compute_dtype", torch.float32) == torch.bfloat16 else F32
 
-    # A/B switch (IVIT_CONCURRENT_STREAMS=0): both ViTs on the caller's stream, one after the other
+    # Profiling mode (IVIT_CONCURRENT_STREAMS=0): both ViTs on the caller's stream, one after the
+    # other — the one-stream step whose kernel trace attributes time per kernel without the other
+    # stream sharing the CUs (the concurrency is worth 3.7 ms per step)
     concurrent_streams = os.environ.get("IVIT_CONCURRENT_STREAMS", "1") == "1"
 
     def stream_tokens(self, lidar_bev, map_bev):
@@ -140,29 +142,22 @@ class TwoStreamViTBackbone(nn.Module):
         s1.wait_stream(main)
         s2.wait_stream(main)
         # block by block, alternating (vit.VisionTransformer.forward_tokens_steps): with each ViT
-        # launched whole, the backward engine enqueued the map stream's entire backward before the
-        # LiDAR stream's first kernel, and the LiDAR stream ran its last blocks alone
-        if not INTERLEAVE:  # A/B switch (IVIT_STREAM_INTERLEAVE=0): each ViT launched whole
-            with torch.cuda.stream(s1):
-                tl = self.vit_lidar.forward_tokens(lidar_bev)
-            with torch.cuda.stream(s2):
-                tm = self.vit_map.forward_tokens(map_bev)
-            live, out = [], {"l": tl, "m": tm}
-        else:
-            out = {}
-            live = [(s1, "l", self.vit_lidar.forward_tokens_steps(lidar_bev)),
-                    (s2, "m", self.vit_map.forward_tokens_steps(map_bev))]
-            # IVIT_STREAM_LEAD = k: the map stream's first k steps before the alternation, so the
-            # backward engine (newest node first) runs the LiDAR stream k blocks ahead and its long
-            # patch-embedding weight gradient overlaps the map stream's last blocks
-            with torch.cuda.stream(s2):
-                for _ in range(LEAD):  # a lead past the map ViT's depth finishes it here
-                    try:
-                        next(live[1][2])
-                    except StopIteration as stop:
-                        out["m"] = stop.value
-                        live.pop(1)
-                        break
+        # launched whole (round 3), the backward engine enqueued the map stream's entire backward
+        # before the LiDAR stream's first kernel, and the LiDAR stream ran its last blocks alone
+        out = {}
+        live = [(s1, "l", self.vit_lidar.forward_tokens_steps(lidar_bev)),
+                (s2, "m", self.vit_map.forward_tokens_steps(map_bev))]
+        # the map stream's first LEAD steps before the alternation, so the backward engine (newest
+        # node first) runs the LiDAR stream LEAD blocks ahead and its long patch-embedding weight
+        # gradient overlaps the map stream's last blocks
+        with torch.cuda.stream(s2):
+            for _ in range(LEAD):  # a lead past the map ViT's depth finishes it here
+                try:
+                    next(live[1][2])
+                except StopIteration as stop:
+                    out["m"] = stop.value
+                    live.pop(1)
+                    break
         while live:
             for item in list(live):
                 st, key, gen = item
@@ -256,8 +251,7 @@ class TwoStreamViTBackbone(nn.Module):
 
 
 _SIDE_STREAMS = {}
-INTERLEAVE = os.environ.get("IVIT_STREAM_INTERLEAVE", "1") == "1"
-LEAD = max(0, int(os.environ.get("IVIT_STREAM_LEAD", "1")))  # 44.53-44.64 vs 44.65-44.67 ms (lead 0), same call
+LEAD = 1  # 44.53-44.64 vs 44.65-44.67 ms (lead 0), lead 3 44.56-44.63, same call (round 4)
 
 
 def _side_streams(device):

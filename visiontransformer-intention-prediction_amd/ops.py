@@ -14,12 +14,11 @@ plus single-op Functions used by the standalone module forwards.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 from torch.utils.weak import WeakIdKeyDictionary
 
-from _lib import ACT_GELU, ACT_GELU_D, ACT_NONE, BF16, F32, dt, lib, ptr, stream, tdtype, workspace
+from _lib import ACT_GELU, ACT_GELU_D, ACT_NONE, BF16, F32, KNOB_CONV_PANEL, dt, lib, ptr, stream, tdtype, workspace
 
 
 def _code(dtype):
@@ -461,7 +460,8 @@ def conv_fwd(x, B, H, W, wp, bias, cdt, out_dtype):
 
 
 def conv_panel_enabled():
-    return os.environ.get("IVIT_CONV_PANEL", "1") != "0"
+    """The stride-1 bf16 convolutions on the panel kernels (ivit_get_knob(IVIT_KNOB_CONV_PANEL))."""
+    return lib.ivit_get_knob(KNOB_CONV_PANEL) != 0
 
 
 def pack_conv_t(w, cdt, cout_pad=None):
@@ -664,9 +664,6 @@ class PatchEmbedFn(torch.autograd.Function):
         return None, dw, db, dpos, dcls, None, None
 
 
-# bf16 row-panel ViT blocks: the four weight gradients as one grouped launch (ivit_vit_block_wgrad)
-# instead of four split-K engine GEMMs; IVIT_GROUP_WGRAD=0 selects the per-GEMM path (A/B runs).
-GROUP_WGRAD = os.environ.get("IVIT_GROUP_WGRAD", "1") == "1"
 class GradHandoff:
     """Backward hand-off between consecutive fused ViT blocks: block i+1's qkv-dgrad + norm1-backward
     kernel also writes bf16(dx * s2_i) — block i's DropPath-scaled MLP-branch gradient, the fc2
@@ -794,7 +791,8 @@ class ViTBlockFn(torch.autograd.Function):
             dx2s = add_act_grad(dx2, row_scale=s2, row_elems=N * D, out_dtype=cd)
         dh = panel_dgrad_mul(dx2s, f2w, h) if ctx.panel else linear_dgrad(dx2s, w2, cdt, cd, gelu_pre=h)
         # bf16 row-panel blocks: the four weight gradients in one grouped launch after the dgrads
-        group = ctx.panel and GROUP_WGRAD
+        # (ivit_vit_block_wgrad) instead of four split-K engine GEMMs (-1.5 ms per step, round 3)
+        group = ctx.panel
         # DDP: the twelve parameter gradients straight into their bucket views (no autograd add)
         direct = grad_sinks(ctx.params) if group else None
         dv = direct[1] if direct is not None else [None] * 12

@@ -4,15 +4,11 @@ over device pointer tables instead of torch's per-tensor foreach kernels."""
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 
 import ops
 from _lib import lib, ptr, stream
-
-
-CHUNKED = os.environ.get("IVIT_ADAMW_CHUNKED", "1") == "1"
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -112,13 +108,6 @@ class FusedAdamW(torch.optim.Optimizer):
                 if pack is not None:
                     jobs.append((p.data_ptr(), pack.data_ptr(), rows, cols, tr))
                     big = max(big, rows * cols)
-        if not CHUNKED:  # A/B switch (IVIT_ADAMW_CHUNKED=0): the 2D-grid launch
-            lib.ivit_adamw_guarded(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(self._table_ptrs(shadows, dev)),
-                                   ptr(sizes), max(p.numel() for p in ps), group["lr"], b1, b2, group["eps"],
-                                   group["weight_decay"], bc1, bc2s, ptr(finite), ptr(sin), ptr(sout), stream())
-            if jobs:
-                lib.ivit_weight_pack_multi(len(jobs), ptr(self._pack_jobs(jobs, dev)), big, stream())
-            return
         chunks, nch = self._table_chunks(ps, dev)
         lib.ivit_adamw_chunked(len(ps), ptr(tp), ptr(tg), ptr(tm), ptr(tv), ptr(self._table_ptrs(shadows, dev)),
                                ptr(sizes), ptr(chunks), nch, group["lr"], b1, b2, group["eps"],
