@@ -363,6 +363,9 @@ def main():
     ap.add_argument("--intervals-out", type=str, default=None,
                     help="write the attention kernels' recorded execution intervals of the timed region (the "
                          "roofline's device time) as a kernel-trace CSV; tools/kunion.py recomputes the union")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the isolated attention leg (profiled runs: its warm-up launches would enter the "
+                         "kernel trace's union and averages)")
     ap.add_argument("--bucket-mb", type=float, default=64)
     ap.add_argument("--ddp", choices=["buckets", "torch"], default="buckets",
                     help="gradient exchange: ddp.GradBuckets (default) or torch DistributedDataParallel")
@@ -574,7 +577,7 @@ def main():
                                                     f"the profiler lowers the clock, MI355X_MICROARCH.md DVFS item 2)")
     if args.intervals_out and timing:
         out["roofline"]["intervals_file"] = os.path.relpath(os.path.abspath(args.intervals_out), HERE)
-    if default_cfg and world == 1:
+    if default_cfg and world == 1 and not args.no_isolated:
         # the same kernel(s) alone on the same shape (outside the timed region): the frac without the
         # other ViT stream's kernels sharing the CUs
         iso, reps = isolated_attn_ms(roof, B, N, 6, dev)

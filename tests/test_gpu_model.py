@@ -2,6 +2,7 @@
 from the reference's own code and against the CPU oracle. f32 path: within 1e-3 rel
 (north_star); bf16 path: bf16-appropriate tolerances; NMS indices bit-exact."""
 import json
+import os
 
 import numpy as np
 import pytest
@@ -325,19 +326,24 @@ def test_drop_path_injected_vs_oracle():
     assert all(v == 0.0 or abs(v - 1.0 / (1.0 - p11)) < 1e-6 for v in vals), vals
 
 
-def _oracle_step(cfg, lidar, mp, gts, keep, sc, attn, checkpoint, autocast):
+def _oracle_step(cfg, lidar, mp, gts, keep, sc, attn, checkpoint, autocast, dtype=torch.float32):
     """The oracle's train step (forward, loss, backward) on the GPU with torch's own kernels:
-    f32, or under torch.autocast(bf16) — the reference's mixed-precision form (timm's fused
-    SDPA + bf16 linears / convs, f32 LayerNorm / softmax stats / loss)."""
-    sd = {k: (v.clone().to(DEV).requires_grad_(True) if v.is_floating_point() and "running" not in k
-              else v.clone().to(DEV)) for k, v in make_state_dict(cfg, seed=0).items()}
-    scd = None if sc is None else tuple([(a.to(DEV), b_.to(DEV)) for a, b_ in s] for s in sc)
+    f32 (or f64: the conditioning reference of the config-1 test), or under torch.autocast(bf16) —
+    the reference's mixed-precision form (timm's fused SDPA + bf16 linears / convs, f32 LayerNorm /
+    softmax stats / loss)."""
+    fl = lambda v: v.to(dtype) if v.is_floating_point() else v  # noqa: E731
+    sd = {k: (fl(v.clone().to(DEV)).requires_grad_(True) if v.is_floating_point() and "running" not in k
+              else fl(v.clone().to(DEV))) for k, v in make_state_dict(cfg, seed=0).items()}
+    scd = None if sc is None else tuple([(fl(a.to(DEV)), fl(b_.to(DEV))) for a, b_ in s] for s in sc)
     with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
-        rc, rb, ri = O.intentnet_forward(sd, lidar.to(DEV), mp.to(DEV), cfg, training=True, drop_path_scales=scd,
-                                         attn=attn, checkpoint=checkpoint)
-    rc, rb, ri = rc.float(), rb.float(), ri.float()
-    anchors = O.generate_anchors(*cfg["img_size"])
-    rd = O.detection_loss(rc.cpu(), rb.cpu(), ri.cpu(), anchors, gts, downsampling=True, keep=keep)
+        rc, rb, ri = O.intentnet_forward(sd, fl(lidar.to(DEV)), fl(mp.to(DEV)), cfg, training=True,
+                                         drop_path_scales=scd, attn=attn, checkpoint=checkpoint)
+    if dtype == torch.float32:
+        rc, rb, ri = rc.float(), rb.float(), ri.float()
+    anchors = fl(O.generate_anchors(*cfg["img_size"]))
+    gts_ = [{k: fl(v) for k, v in g.items()} for g in gts]
+    rd = O.detection_loss(rc.cpu(), rb.cpu(), ri.cpu(), anchors, gts_, downsampling=True,
+                          keep=None if keep is None else fl(keep))
     rd["loss"].backward()
     return (rc.detach(), rb.detach(), ri.detach()), rd, {k: v.grad for k, v in sd.items() if v.grad is not None}
 
@@ -554,9 +560,13 @@ def test_config1_fp32_full_grid_train_step_vs_oracle():
     (factors injected into both), forward + DetectionIntentionLoss (downsampling keep mask
     injected) + backward (train_vit.py:29,151-173) against the oracle's f32 step (plain PyTorch f32,
     explicit attention, run on the GPU with torch's kernels: the CPU oracle step takes minutes).
-    Bars: outputs and loss terms 1e-3 relative (north_star); every parameter gradient 1e-3
-    relative L2 where it holds, 5e-3 for any (the train-mode BN + ReLU kink argument of
-    test_medium_grid_fp32_vs_oracle)."""
+    Bars: outputs and loss terms 1e-3 relative (north_star). Parameter gradients, per tensor
+    (relative L2): within 1e-3 of the f32 oracle, or — where train-mode BatchNorm + ReLU make the
+    step ill-conditioned in f32 (an activation within f32 rounding of a ReLU kink lands on either
+    side in two correct f32 implementations, and the BN batch-statistic terms carry the O(1) change
+    to every upstream gradient) — no further from the same oracle computed in f64 than 2x the f32
+    oracle's own distance from it (+1e-4): the HIP f32 step is then as exact as the reference's own
+    f32 arithmetic allows. The per-parameter table goes to gpurun_out/config1_grads.txt."""
     import loss as L
     import utils
     torch.backends.cuda.matmul.allow_tf32 = False
@@ -574,21 +584,37 @@ def test_config1_fp32_full_grid_train_step_vs_oracle():
     d["loss"].backward()
     ours = {k: p.grad.detach().double().cpu() for k, p in m.named_parameters()}
     outs = (c.detach(), b.detach(), i.detach())
-    del m
+    d = {k: float(v.detach()) for k, v in d.items() if k != "num_pos_anchors"} | {"num_pos_anchors": int(d["num_pos_anchors"])}
+    del m, c, b, i
     (rc, rb, ri), rd, rg = _oracle_step(cfg, lidar, mp, gts, keep, sc, "explicit", False, autocast=False)
+    rg = {k: v.double().cpu() for k, v in rg.items()}
     e_out = {k: _rel(x, y) for k, x, y in zip(("cls", "box", "int"), outs, (rc, rb, ri))}
     for k in ("loss", "cls_loss", "box_loss", "intent_loss"):
-        e_out[k] = abs(float(d[k]) - float(rd[k])) / max(abs(float(rd[k])), 1e-12)
-    assert int(d["num_pos_anchors"]) == int(rd["num_pos_anchors"])
-    worst = sorted(((float((ours[k] - r.double().cpu()).norm() / (r.double().norm() + 1e-30)), k)
-                    for k, r in rg.items()), reverse=True)
-    n_strict = sum(1 for e, _ in worst if e < 1e-3)
-    print("config 1 fp32 400x720 B=1: outputs / losses", e_out, "\n  worst grad rel-L2:", worst[:6],
-          f"\n  {n_strict} of {len(worst)} parameter gradients within 1e-3")
-    assert len(worst) == len(ours)
+        e_out[k] = abs(d[k] - float(rd[k])) / max(abs(float(rd[k])), 1e-12)
+    assert d["num_pos_anchors"] == int(rd["num_pos_anchors"])
+    del rc, rb, ri, rd
+    torch.cuda.empty_cache()
+    _, _, r64 = _oracle_step(cfg, lidar, mp, gts, keep, sc, "explicit", False, autocast=False, dtype=torch.float64)
+    r64 = {k: v.double().cpu() for k, v in r64.items()}
+    l2 = lambda a, r: float((a - r).norm() / (r.norm() + 1e-30))  # noqa: E731
+    rows = sorted(((l2(ours[k], rg[k]), l2(ours[k], r64[k]), l2(rg[k], r64[k]), k) for k in rg), reverse=True)
+    n_strict = sum(1 for e, _, _, _ in rows if e < 1e-3)
+    bad = [r for r in rows if not (r[0] < 1e-3 or r[1] <= 2 * r[2] + 1e-4)]
+    lines = [f"config 1: IntentNetViT fp32, B = 1, 400x720, train mode (DropPath 0.1 injected), loss + backward; "
+             f"HIP f32 step vs the oracle's f32 step (o32) and the oracle in f64 (o64), torch kernels on the GPU",
+             f"outputs / loss terms (relative; bar 1e-3): " + ", ".join(f"{k} {v:.2e}" for k, v in e_out.items()),
+             f"parameter gradients within 1e-3 (relative L2) of o32: {n_strict} of {len(rows)}",
+             f"bar for the rest: |ours - o64| <= 2 |o32 - o64| + 1e-4; failing: {len(bad)}",
+             f"{'ours-o32':>10} {'ours-o64':>10} {'o32-o64':>10}  parameter"]
+    lines += [f"{a:10.3e} {b_:10.3e} {c_:10.3e}  {k}" for a, b_, c_, k in rows]
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "config1_grads.txt"), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    print("\n".join(lines[:10]))
+    assert len(rows) == len(ours)
     for k, e in e_out.items():
         assert e < 1e-3, (k, e_out)
-    assert worst[0][0] < 5e-3, worst[:6]
+    assert not bad, bad[:6]
 
 
 def test_config4_eval_batch32_full_grid_vs_oracle():

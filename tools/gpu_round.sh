@@ -15,15 +15,15 @@ fi
 timeout -k 10 400 python bench.py --intervals-out gpurun_out/${TAG}_attn_intervals.csv > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.err
 rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python -c "import json; d=json.load(open('gpurun_out/${TAG}_bench_default.json')); r=d['roofline']; print(d['ms_per_step'], d['value'], r['frac'], r.get('frac_rocprof'), d['cpu_baseline']['value'])"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-isolated > gpurun_out/${TAG}_prof.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python tools/kunion.py gpurun_out/${TAG}_prof/run_kernel_trace.csv attn_bwd_dq attn_bwd_dkv --flops 4.979e11 --json gpurun_out/${TAG}_attn_bwd_union.json
 python tools/kunion.py gpurun_out/${TAG}_attn_intervals.csv attn_bwd_dq attn_bwd_dkv --flops 4.979e11 --json gpurun_out/${TAG}_attn_bwd_intervals_union.json
 # HBM bytes per kernel: one FETCH_SIZE and one WRITE_SIZE pass (separate runs), summarised with the
 # gfx950 corrections (tools/pmc_summary.py); bench.py reads the newest profiles/*_pmc_hbm.json
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_pmcf -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_pmcf.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_pmcf -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-isolated > gpurun_out/${TAG}_pmcf.log 2>&1
 rc=$?; echo "pmc fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_pmcw -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_pmcw.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_pmcw -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-isolated > gpurun_out/${TAG}_pmcw.log 2>&1
 rc=$?; echo "pmc write rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 tools/pmc_summary.py gpurun_out/${TAG}_pmcf gpurun_out/${TAG}_pmcw "patch_wgrad|attn_bwd" > gpurun_out/${TAG}_pmc_hbm.json
 timeout -k 10 300 python bench.py --mode eval --steps 10 --warmup 2 > gpurun_out/${TAG}_bench_eval_config4.json 2>gpurun_out/${TAG}_eval.err
