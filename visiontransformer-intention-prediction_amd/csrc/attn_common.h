@@ -48,6 +48,7 @@ IVIT_DEV f32x16 zero16() {
 // over all 8 XCDs and every attention launch read its operands ~5x from HBM (PMC FETCH_SIZE).
 IVIT_DEV int2 attn_block_id() {
   const int nb = gridDim.x;
+
   const int flat = xcd_remap(blockIdx.x + blockIdx.y * nb, nb * gridDim.y);
   return make_int2(flat % nb, flat / nb);
 }
