@@ -257,6 +257,10 @@ long ivit_bn_workspace(long M, long C);
 int ivit_bn_stats(const void* X, int x_dtype, long M, long C, float* mean, float* invstd, float* run_mean,
                   float* run_var, float momentum, float eps, void* work, long work_bytes, void* stream);
 /* Y = [relu]( (X - mean) * invstd * g + b  [+ R] ), Y/R in y_dtype. */
+/* eval-mode statistics of nn.BatchNorm2d (model_vit.py:19-34 in eval): mean = running_mean,
+ * invstd = rsqrt(running_var + eps), as torch computes them on the device. */
+int ivit_bn_eval_stats(const float* run_mean, const float* run_var, long C, float eps, float* mean, float* invstd,
+                       void* stream);
 int ivit_bn_apply(const void* X, int x_dtype, long M, long C, const float* mean, const float* invstd,
                   const float* g, const float* b, const void* R, int relu, void* Y, int y_dtype, void* stream);
 /* Backward of Y = relu?(BN(X) + R): dYin masked by (Y > 0) if relu; dR = masked dY;

@@ -650,6 +650,28 @@ extern "C" int ivit_bn_stats(const void* X, int x_dtype, long M, long C, float* 
   return 0;
 }
 
+namespace {
+// eval-mode BatchNorm statistics from the running buffers: mean = running_mean, invstd =
+// rsqrtf(running_var + eps) — the values torch.rsqrt(rvar + eps) gives on the device
+__global__ void bn_eval_stats_kernel(const float* __restrict__ rmean, const float* __restrict__ rvar, int C, float eps,
+                                     float* __restrict__ mean, float* __restrict__ invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = rmean[c];
+  invstd[c] = rsqrtf(rvar[c] + eps);
+}
+}  // namespace
+
+extern "C" int ivit_bn_eval_stats(const float* run_mean, const float* run_var, long C, float eps, float* mean,
+                                  float* invstd, void* stream) {
+  IVIT_CHECK_ARG(C >= 0 && C < (1L << 30), "ivit_bn_eval_stats: bad channel count %ld", C);
+  if (C == 0) return 0;
+  hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(ivit_cdiv(C, 256)), dim3(256), 0, ivit_stream(stream), run_mean,
+                     run_var, (int)C, eps, mean, invstd);
+  IVIT_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int ivit_bn_apply(const void* X, int x_dtype, long M, long C, const float* mean, const float* invstd,
                              const float* g, const float* b, const void* R, int relu, void* Y, int y_dtype,
                              void* stream) {

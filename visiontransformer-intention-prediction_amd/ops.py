@@ -446,6 +446,17 @@ def pack_conv(w, cdt, cout_pad=None):
     return out
 
 
+def pack_conv_pair(w0, w1, cdt, cout_pad):
+    """pack_conv of torch.cat([w0, w1], 0) without the concatenation: w0's rows, then w1's rows
+    zero-padded to cout_pad (two ivit_pack_conv_weight launches into one buffer)."""
+    C0, Cin, k, _ = w0.shape
+    C1 = w1.shape[0]
+    out = torch.empty((cout_pad, k, k, Cin), dtype=tdtype(cdt), device=w0.device)
+    lib.ivit_pack_conv_weight(cdt, ptr(w0), C0, Cin, k, C0, ptr(out), stream())
+    lib.ivit_pack_conv_weight(cdt, ptr(w1), C1, Cin, k, cout_pad - C0, ptr(out[C0:]), stream())
+    return out
+
+
 def unpack_conv_grad(gp, Cout, Cin, k):
     out = torch.empty((Cout, Cin, k, k), dtype=torch.float32, device=gp.device)
     lib.ivit_unpack_conv_grad(ptr(gp), Cout, Cin, k, ptr(out), 0, stream())
@@ -542,8 +553,9 @@ def bn_forward(x, g, b, rmean, rvar, training, momentum=0.1, eps=1e-5, nbt=None)
         if nbt is not None:
             nbt.add_(1)
     else:
-        mean = rmean.clone()
-        invstd = torch.rsqrt(rvar + eps)
+        mean = torch.empty((C,), dtype=torch.float32, device=x.device)
+        invstd = torch.empty_like(mean)
+        lib.ivit_bn_eval_stats(ptr(rmean), ptr(rvar), C, eps, ptr(mean), ptr(invstd), stream())
     return _BNState(mean, invstd)
 
 
@@ -924,10 +936,13 @@ class NeckFn(torch.autograd.Function):
             return (cast(x, torch.float32) if x.dtype != torch.float32 else x.clone(),)
         Cd, Ci = A * 7, A * K
         Cp = (Cd + Ci + 7) // 8 * 8
-        wh = torch.cat([P["det_head.conv.weight"], P["intention_head.conv.weight"]], 0)
-        whp = pack_conv(wh, cdt, cout_pad=Cp)
-        bh = torch.cat([P["det_head.conv.bias"].float(), P["intention_head.conv.bias"].float(),
-                        _zeros(Cp - Cd - Ci, dev)])
+        wd_, wi_ = P["det_head.conv.weight"], P["intention_head.conv.weight"]
+        wh = (wd_, wi_)  # both heads as one conv: packed into one [Cp][3][3][Cin] weight, rows Cd.. the intention head
+        whp = pack_conv_pair(wd_, wi_, cdt, Cp)
+        bh = torch.empty((Cp,), dtype=torch.float32, device=dev)
+        bh[:Cd].copy_(P["det_head.conv.bias"])
+        bh[Cd:Cd + Ci].copy_(P["intention_head.conv.bias"])
+        bh[Cd + Ci:].copy_(_zeros(Cp - Cd - Ci, dev))
         hout = conv_fwd(x, B, Hf, Wf, whp, bh, cdt, torch.float32)
         cls = torch.empty((B, M // B * A, 1), dtype=torch.float32, device=dev)
         box = torch.empty((B, M // B * A, 6), dtype=torch.float32, device=dev)
@@ -975,7 +990,8 @@ class NeckFn(torch.autograd.Function):
             for n_, g_ in zip(("det_head.conv.weight", "intention_head.conv.weight", "det_head.conv.bias",
                                "intention_head.conv.bias"), head_wgrad(dh, x_last)):
                 G[n_] = g_
-            dx = conv_dgrad(dh, B, Hf, Wf, whp, cdt, torch.float32, w=wh, dy_zero_pad=True)
+            # the transposed pack of both heads' weights (the forward packs them without a concatenation)
+            dx = conv_dgrad(dh, B, Hf, Wf, whp, cdt, torch.float32, w=torch.cat(wh, 0), dy_zero_pad=True)
         for li in reversed(range(layers)):
             p = f"fusion_block.{li}."
             x, c1, s1, r1, c2, s2, out = acts[li]
