@@ -457,8 +457,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
 
   bf16x8 qa[2][2], ga[2][2];   // A(u) fragments [i][s]
   f32x4 sn[2], dn[2];          // A(u+1)'s initial accumulators (-lse2 / -delta of its rows), [i]
-  f32x4 sc[2][2], dc[2][2];    // A(u) results [i][j]: S' - lse2, dP - delta
-  unsigned up[2][4], ud[2][4];  // packed P / dS of the pending B, [j][word]
   bf16x8 tg[4], tq[4];         // transposed dO / Q fragments of the pending B, [e]
   auto read_frag = [&](const char* qimg, const char* gimg, int t, int i, int s) {
     qa[i][s] = *(const bf16x8*)(qimg + ro[s] + 4096 * t + 2048 * i);
@@ -467,13 +465,6 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
   auto read_rows = [&](const float* lr, const float* dr, int t, int i) {
     sn[i] = *(const f32x4*)(lr + 32 * t + 16 * i + 4 * g);
     dn[i] = *(const f32x4*)(dr + 32 * t + 16 * i + 4 * g);
-  };
-  // E pair k (j = k >> 2, i = (k >> 1) & 1, half hh = k & 1): word 2i + hh of up[j] / ud[j]
-  auto e_pair = [&](int k) {
-    const int j = k >> 2, i = (k >> 1) & 1, hh = k & 1;
-    const float p0 = fast_exp2(sc[i][j][2 * hh]), p1 = fast_exp2(sc[i][j][2 * hh + 1]);
-    up[j][2 * i + hh] = pk_bf16(p0, p1);
-    ud[j][2 * i + hh] = pk_bf16(p0 * dc[i][j][2 * hh], p1 * dc[i][j][2 * hh + 1]);
   };
   auto word8 = [&](const unsigned (&w)[4]) { return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3])); };
   auto read_b = [&](const char* qimg, const char* gimg, int t, int e) {
@@ -485,12 +476,47 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
     tg[e] = a.v;
     tq[e] = c.v;
   };
-  // body: A(u) on (SA, tA) || E(u-1); B(u-1) on (SB, tB) || reads of A(u+1) on (SN, tN).
+  // E (exp2, dS = P dP, bf16 packing) of one unit is 8 pairs of elements — 16 exp, 16 mul, 16 cvt,
+  // ~264 issue cycles against the 256 the unit's 32 MFMA gaps leave free — so it is spread over
+  // BOTH halves of the body instead of the A half alone (where it took ~34 cycles per 2 MFMAs and
+  // stalled the matrix pipe whenever the SIMD's other wave was in its A half too): the key-block-0
+  // half of E(u) runs beside B(u-1)'s products, right after A(u), the key-block-1 half beside
+  // A(u+1). One pair (i, hh) is four sub-steps, one per MFMA gap: exp, exp, two multiplies, two
+  // conversions (8-9 issue cycles each).
+  float ep0, ep1, et0, et1;
+  // (each result is pinned where it is computed by an empty asm that "modifies" it: the pure
+  // arithmetic would otherwise be sunk past the body's branches to its first use)
+  auto e_sub = [&](const f32x4& S, const f32x4& DP, int hh, int ph, unsigned& wu, unsigned& wd) {
+    if (ph == 0) {
+      ep0 = fast_exp2(S[2 * hh]);
+      asm volatile("" : "+v"(ep0));
+    }
+    if (ph == 1) {
+      ep1 = fast_exp2(S[2 * hh + 1]);
+      asm volatile("" : "+v"(ep1));
+    }
+    if (ph == 2) {
+      et0 = ep0 * DP[2 * hh];
+      et1 = ep1 * DP[2 * hh + 1];
+      asm volatile("" : "+v"(et0), "+v"(et1));
+    }
+    if (ph == 3) {
+      wu = pk_bf16(ep0, ep1);
+      wd = pk_bf16(et0, et1);
+      asm volatile("" : "+v"(wu), "+v"(wd));
+    }
+  };
+  f32x4 sc1[2], dc1[2];        // A(u-1)'s key-block-1 results [i] (their E half runs beside A(u))
+  unsigned upA[4], udA[4];     // key block 0 of the pending B: packed P / dS words
+  unsigned up1[4], ud1[4];     // key block 1 of the pending B
+  // body: A(u) on (SA, tA) || E(u-1) key block 1; B(u-1) on (SB, tB) || E(u) key block 0, reads of
+  // A(u+1) on (SN, tN).
   auto body = [&](auto sa, auto ta, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
     constexpr int SA = decltype(sa)::value, TA = decltype(ta)::value, SB = decltype(sb)::value;
     constexpr int TB = decltype(tb)::value, SN = decltype(sn_)::value, TN = decltype(tn)::value;
     constexpr bool BAR = decltype(bar)::value;
     f32x4 s[2][2], dp[2][2];
+    unsigned upN[4], udN[4];
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
       const int ks = m >> 3, i = (m >> 2) & 1, j = (m >> 1) & 1;
@@ -498,7 +524,10 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
       else dp[i][j] = mfma16(ga[i][ks], vf[j][ks], ks == 0 ? dn[i] : dp[i][j]);
       if (m == 0) read_frag(smem[SA][0], smem[SA][1], TA, 0, 1);
       if (m == 2) read_frag(smem[SA][0], smem[SA][1], TA, 1, 1);
-      if ((m & 1) == 0) e_pair(m >> 1);
+      {  // E(u-1), key block 1: pair q = m / 4 (i = q >> 1, hh = q & 1), sub-step m % 4
+        const int q = m >> 2, ie = q >> 1, hh = q & 1;
+        e_sub(sc1[ie], dc1[ie], hh, m & 3, up1[2 * ie + hh], ud1[2 * ie + hh]);
+      }
       if (m == 9) read_b(smem[SB][0], smem[SB][1], TB, 0);
       if (m == 12) read_b(smem[SB][0], smem[SB][1], TB, 1);
       __builtin_amdgcn_sched_barrier(0);
@@ -513,8 +542,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
       const int e = m >> 2, j = (m >> 1) & 1;
       if (m == 0) read_b(smem[SB][0], smem[SB][1], TB, 2);
       if (m == 2) read_b(smem[SB][0], smem[SB][1], TB, 3);
-      if ((m & 1) == 0) dv[j][e] = mfma16(word8(up[j]), tg[e], dv[j][e]);
-      else dk[j][e] = mfma16(word8(ud[j]), tq[e], dk[j][e]);
+      if ((m & 1) == 0) dv[j][e] = mfma16(word8(j ? up1 : upA), tg[e], dv[j][e]);
+      else dk[j][e] = mfma16(word8(j ? ud1 : udA), tq[e], dk[j][e]);
+      {  // E(u), key block 0 (A(u)'s s[i][0] / dp[i][0], complete since its MFMA 13)
+        const int q = m >> 2, ie = q >> 1, hh = q & 1;
+        e_sub(s[ie][0], dp[ie][0], hh, m & 3, upN[2 * ie + hh], udN[2 * ie + hh]);
+      }
       if (more) {
         if (m == 5) read_rows(srow[SN][0], srow[SN][1], TN, 0);
         if (m == 7) read_rows(srow[SN][0], srow[SN][1], TN, 1);
@@ -524,12 +557,15 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i) {
+      sc1[i] = s[i][1];
+      dc1[i] = dp[i][1];
+    }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        sc[i][j] = s[i][j];
-        dc[i][j] = dp[i][j];
-      }
+    for (int w = 0; w < 4; ++w) {
+      upA[w] = upN[w];
+      udA[w] = udN[w];
+    }
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -551,12 +587,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
     read_frag(smem[0][0], smem[0][1], 0, i, 0);
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    sc1[i] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};  // exp2 -> 0: B(-1) adds zeros
+    dc1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      sc[i][j] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};  // exp2 -> 0
-      dc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+  for (int w = 0; w < 4; ++w) upA[w] = udA[w] = 0u;
   auto tile = [&](auto st, int j) {
     constexpr int S = decltype(st)::value;
     using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
@@ -573,19 +609,21 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
   }
   if (j < nt) tile(I0{}, j);
   if (j + 1 < nt) tile(I1{}, j + 1);
-  {  // drain: E and B of the last unit (tile nt-1, rows 32..63)
+  {  // drain: the key-block-1 half of E and all of B for the last unit (tile nt-1, rows 32..63)
     const int S = (nt - 1) % BNS;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) e_pair(k);
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) e_sub(sc1[q >> 1], dc1[q >> 1], q & 1, ph, up1[q], ud1[q]);
 #pragma unroll
     for (int e = 0; e < 4; ++e) read_b(smem[S][0], smem[S][1], 1, e);
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int jj = 0; jj < 2; ++jj) {
-        dv[jj][e] = mfma16(word8(up[jj]), tg[e], dv[jj][e]);
-        dk[jj][e] = mfma16(word8(ud[jj]), tq[e], dk[jj][e]);
-      }
+    for (int e = 0; e < 4; ++e) {
+      dv[0][e] = mfma16(word8(upA), tg[e], dv[0][e]);
+      dk[0][e] = mfma16(word8(udA), tq[e], dk[0][e]);
+      dv[1][e] = mfma16(word8(up1), tg[e], dv[1][e]);
+      dk[1][e] = mfma16(word8(ud1), tq[e], dk[1][e]);
+    }
   }
   // lane holds rows key 16j + 4g + r, column d = 16e + c16; stored through LDS as whole rows (2-byte
   // stores from the C layout: pair 0.7220-0.7222 vs 0.7187-0.7190 ms, profiles/r06_b_attn_epi_ab.txt)
