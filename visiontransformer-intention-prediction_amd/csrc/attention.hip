@@ -796,19 +796,10 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
 #pragma unroll
     for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(tro[e]));
     bf16x8 ka[2][2], va[2][2];  // A(u) fragments [j][ks]
-    f32x4 sc[2][2], dc[2][2];   // A(u) results [j][i]
-    unsigned pdq[2][4];         // packed dS of the pending B, [i][word]
     bf16x8 tk[4];               // transposed K fragments of the pending B, [e]
     auto read_a = [&](const char* kimg, const char* vimg, int t, int j, int ks) {
       ka[j][ks] = *(const bf16x8*)(kimg + ro[ks] + 4096 * t + 2048 * j);
       va[j][ks] = *(const bf16x8*)(vimg + ro[ks] + 4096 * t + 2048 * j);
-    };
-    // E pair k (i = k >> 2, j = (k >> 1) & 1, half hh = k & 1): word 2j + hh of pdq[i]
-    auto e_pair = [&](int k) {
-      const int i = k >> 2, j = (k >> 1) & 1, hh = k & 1;
-      const float d0 = fast_exp2(sc[j][i][2 * hh]) * dc[j][i][2 * hh];
-      const float d1 = fast_exp2(sc[j][i][2 * hh + 1]) * dc[j][i][2 * hh + 1];
-      pdq[i][2 * j + hh] = pk_bf16(d0, d1);
     };
     auto read_b = [&](const char* kimg, int t, int e) {
       union { s16x4 s[2]; bf16x8 v; } u;
@@ -817,11 +808,38 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
       tk[e] = u.v;
     };
     auto word8 = [&](const unsigned (&w)[4]) { return __builtin_bit_cast(bf16x8, make_uint4(w[0], w[1], w[2], w[3])); };
+    // E (exp2, dS = P dP, bf16 packing) spread over both halves of the body as in the dK/dV kernel:
+    // the query-block-0 half of E(u) beside B(u-1)'s 8 products (two sub-steps per gap), the
+    // query-block-1 half beside A(u+1) (one per gap); results pinned where they are computed.
+    float ep0, ep1, et0, et1;
+    auto e_sub = [&](const f32x4& S, const f32x4& DP, int hh, int ph, unsigned& w) {
+      if (ph == 0) {
+        ep0 = fast_exp2(S[2 * hh]);
+        asm volatile("" : "+v"(ep0));
+      }
+      if (ph == 1) {
+        ep1 = fast_exp2(S[2 * hh + 1]);
+        asm volatile("" : "+v"(ep1));
+      }
+      if (ph == 2) {
+        et0 = ep0 * DP[2 * hh];
+        et1 = ep1 * DP[2 * hh + 1];
+        asm volatile("" : "+v"(et0), "+v"(et1));
+      }
+      if (ph == 3) {
+        w = pk_bf16(et0, et1);
+        asm volatile("" : "+v"(w));
+      }
+    };
+    f32x4 sc1[2], dc1[2];  // A(u-1)'s query-block-1 results [j]
+    unsigned pdqA[4];      // query block 0 of the pending B: packed dS words
+    unsigned pdq1[4];      // query block 1 of the pending B
     auto body = [&](auto sa, auto ta, auto sb, auto tb, auto sn_, auto tn, auto bar, int jn, bool more) {
       constexpr int SA = decltype(sa)::value, TA = decltype(ta)::value, SB = decltype(sb)::value;
       constexpr int TB = decltype(tb)::value, SN = decltype(sn_)::value, TN = decltype(tn)::value;
       constexpr bool BAR = decltype(bar)::value;
       f32x4 s[2][2], dp[2][2];
+      unsigned pdqN[4];
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
         const int ks = m >> 3, j = (m >> 2) & 1, i = (m >> 1) & 1;
@@ -829,7 +847,10 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
         else dp[j][i] = mfma16(va[j][ks], gf[i][ks], ks == 0 ? nd[i] : dp[j][i]);
         if (m == 0) read_a(smem[SA][0], smem[SA][1], TA, 0, 1);
         if (m == 2) read_a(smem[SA][0], smem[SA][1], TA, 1, 1);
-        if ((m & 1) == 0) e_pair(m >> 1);
+        {  // E(u-1), query block 1: pair q = m / 4 (j = q >> 1, hh = q & 1), sub-step m % 4
+          const int q = m >> 2, je = q >> 1, hh = q & 1;
+          e_sub(sc1[je], dc1[je], hh, m & 3, pdq1[2 * je + hh]);
+        }
         if (m == 8) read_b(smem[SB][0], TB, 0);
         if (m == 10) read_b(smem[SB][0], TB, 1);
         if (m == 12) read_b(smem[SB][0], TB, 2);
@@ -844,7 +865,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         const int e = m >> 1, i = m & 1;
-        dq[i][e] = mfma16(word8(pdq[i]), tk[e], dq[i][e]);
+        dq[i][e] = mfma16(word8(i ? pdq1 : pdqA), tk[e], dq[i][e]);
+        {  // E(u), query block 0 (A(u)'s s[j][0] / dp[j][0], complete since its MFMA 13): 2 sub-steps
+          const int q = m >> 1, je = q >> 1, hh = q & 1;
+          e_sub(s[je][0], dp[je][0], hh, 2 * (m & 1), pdqN[2 * je + hh]);
+          e_sub(s[je][0], dp[je][0], hh, 2 * (m & 1) + 1, pdqN[2 * je + hh]);
+        }
         if (more) {
           if (m == 1) read_a(smem[SN][0], smem[SN][1], TN, 0, 0);
           if (m == 3) read_a(smem[SN][0], smem[SN][1], TN, 1, 0);
@@ -852,12 +878,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 2; ++j) {
+        sc1[j] = s[j][1];
+        dc1[j] = dp[j][1];
+      }
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          sc[j][i] = s[j][i];
-          dc[j][i] = dp[j][i];
-        }
+      for (int w = 0; w < 4; ++w) pdqA[w] = pdqN[w];
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -867,12 +893,12 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
 #pragma unroll
     for (int j = 0; j < 2; ++j) read_a(smem[0][0], smem[0][1], 0, j, 0);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
+      sc1[j] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};  // B(-1) adds zeros
+      dc1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        sc[j][i] = f32x4{NEG_BIG, NEG_BIG, NEG_BIG, NEG_BIG};
-        dc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+    for (int w = 0; w < 4; ++w) pdqA[w] = 0u;
     auto tile = [&](auto st, int j) {
       constexpr int S = decltype(st)::value;
       using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
@@ -889,16 +915,19 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
     }
     if (j < nfull) tile(I0{}, j);
     if (j + 1 < nfull) tile(I1{}, j + 1);
-    {  // drain: E and B of the last unit (tile nfull-1, keys 32..63)
+    {  // drain: the query-block-1 half of E and all of B for the last unit (tile nfull-1, keys 32..63)
       const int S = (nfull - 1) % BNS;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) e_pair(k);
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) e_sub(sc1[q >> 1], dc1[q >> 1], q & 1, ph, pdq1[q]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) read_b(smem[S][0], 1, e);
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) dq[i][e] = mfma16(word8(pdq[i]), tk[e], dq[i][e]);
+      for (int e = 0; e < 4; ++e) {
+        dq[0][e] = mfma16(word8(pdqA), tk[e], dq[0][e]);
+        dq[1][e] = mfma16(word8(pdq1), tk[e], dq[1][e]);
+      }
     }
   }
   if (nt > nfull) {  // ragged last key tile (DMA issued one tile ahead, or in the prologue)
