@@ -118,8 +118,17 @@ IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8
                                 const f32x16& negm, int lane, int kbase, int N, const FwdLdsOff& lo) {
   const int hl = lane >> 5;
   auto kfrag = [&](int i) { return *(const bf16x8*)(kimg + lo.k[i & 3] + 4096 * (i >> 2)); };
-  bf16x8 p[4];
-  auto ex = [&](int i) { p[i >> 3][i & 7] = (bf16)fast_exp2(cur[i >> 4][i & 15]); };
+  // P of this tile as 16 packed words (word w = elements 2w, 2w + 1: two exp2 + one cvt_pk, ~21 issue
+  // cycles, inside one 32x32x16 gap's 24 free), each pinned in the gap it is computed in: left to
+  // the compiler, the exps of later words were sunk to their conversions and piled up in a few gaps
+  unsigned pw[16];
+  auto exw = [&](int w) {
+    pw[w] = pk_bf16(fast_exp2(cur[(2 * w) >> 4][(2 * w) & 15]), fast_exp2(cur[(2 * w + 1) >> 4][(2 * w + 1) & 15]));
+    asm volatile("" : "+v"(pw[w]));
+  };
+  auto pfrag = [&](int g) {
+    return __builtin_bit_cast(bf16x8, make_uint4(pw[4 * g], pw[4 * g + 1], pw[4 * g + 2], pw[4 * g + 3]));
+  };
   bf16x8 ka[8];
   ka[0] = kfrag(0);
   ka[1] = kfrag(1);
@@ -128,8 +137,7 @@ IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8
     if (i + 2 < 8) ka[i + 2] = kfrag(i + 2);
     const int t = i >> 2, ks = i & 3;
     nxt[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[i], qf[ks], ks == 0 ? negm : nxt[t], 0, 0, 0);
-    ex(2 * i);
-    ex(2 * i + 1);
+    exw(i);
     __builtin_amdgcn_sched_barrier(0);
   }
   bf16x8 vf[8];
@@ -142,7 +150,8 @@ IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8
   vread(0);
   vread(1);
   __builtin_amdgcn_sched_barrier(0);
-  constexpr int e0[7] = {16, 19, 22, 25, 28, 30, 32};
+  // words 8 .. 13 beside the first six P.V / row-sum MFMAs (words 8-11 are P[2], needed at k = 6),
+  // words 14, 15 beside the next two (P[3], needed at k = 9)
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     const int g = k / 3, which = k % 3;
@@ -150,11 +159,10 @@ IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8
     if (k == 1) vread(3);
     if (k == 3) vread(4);
     if (k == 4) vread(5);
-    if (which == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g], p[g], o0, 0, 0, 0);
-    else if (which == 1) o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g + 1], p[g], o1, 0, 0, 0);
-    else lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[g], lacc, 0, 0, 0);
-#pragma unroll
-    for (int i = e0[k]; i < e0[k + 1]; ++i) ex(i);
+    if (which == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g], pfrag(g), o0, 0, 0, 0);
+    else if (which == 1) o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g + 1], pfrag(g), o1, 0, 0, 0);
+    else lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pfrag(g), lacc, 0, 0, 0);
+    exw(8 + k);
     __builtin_amdgcn_sched_barrier(0);
   }
   float a = NEG_BIG, bm = NEG_BIG;
@@ -172,9 +180,11 @@ IVIT_DEV float fwd_step_fenced6(const char* kimg, const char* vimg, const bf16x8
     const int g = k / 3, which = k % 3;
     if (k == 6) vread(6);
     if (k == 7) vread(7);
-    if (which == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g], p[g], o0, 0, 0, 0);
-    else if (which == 1) o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g + 1], p[g], o1, 0, 0, 0);
-    else lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p[g], lacc, 0, 0, 0);
+    if (which == 0) o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g], pfrag(g), o0, 0, 0, 0);
+    else if (which == 1) o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[2 * g + 1], pfrag(g), o1, 0, 0, 0);
+    else lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pfrag(g), lacc, 0, 0, 0);
+    if (k == 6) exw(14);
+    if (k == 7) exw(15);
     const int v0 = 6 * (k - 6);
 #pragma unroll
     for (int v = v0; v < v0 + 6 && v < 32; v += 2) {
