@@ -357,7 +357,17 @@ IVIT_DEV int block_radix_sort(unsigned* k0, int* v0, unsigned* k1, int* v1, int 
 #pragma unroll
     for (int d = 0; d < PS_D; ++d) hist[d * PS_T + t] = 0u;
     if (t == 0) *skip = 0;
-    for (int i = b0; i < b1; ++i) ++hist[((ki[i] >> shift) & 15u) * PS_T + t];
+    // the chunk in groups of 8 keys, each group's loads issued together (one L2 latency per group,
+    // not per key: the LDS counter updates after them are a dependent chain the compiler cannot
+    // overlap with the next key's load)
+    for (int g0 = b0; g0 < b1; g0 += 8) {
+      unsigned kr[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) kr[e] = g0 + e < b1 ? ki[g0 + e] : 0u;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (g0 + e < b1) ++hist[((kr[e] >> shift) & 15u) * PS_T + t];
+    }
     __syncthreads();
     unsigned c[PS_D], run = 0;
 #pragma unroll
@@ -395,13 +405,24 @@ IVIT_DEV int block_radix_sort(unsigned* k0, int* v0, unsigned* k1, int* v1, int 
     }
     __syncthreads();
     if (!*skip) {
-      for (int i = b0; i < b1; ++i) {
-        const unsigned k = ki[i];
-        const unsigned slot = ((k >> shift) & 15u) * PS_T + t;
-        const unsigned p = hist[slot];
-        hist[slot] = p + 1u;
-        ko[p] = k;
-        vo[p] = vi[i];
+      for (int g0 = b0; g0 < b1; g0 += 8) {
+        unsigned kr[8];
+        int vr[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          kr[e] = g0 + e < b1 ? ki[g0 + e] : 0u;
+          vr[e] = g0 + e < b1 ? vi[g0 + e] : 0;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (g0 + e < b1) {
+            const unsigned slot = ((kr[e] >> shift) & 15u) * PS_T + t;
+            const unsigned p = hist[slot];
+            hist[slot] = p + 1u;
+            ko[p] = kr[e];
+            vo[p] = vr[e];
+          }
+        }
       }
       cur ^= 1;
     }
@@ -499,19 +520,32 @@ __global__ __launch_bounds__(PS_T) void post_select_kernel(const float* __restri
   const int I = (NA + PS_T - 1) / PS_T;
   const int a0 = min(t * I, NA), a1 = min(a0 + I, NA);
   unsigned np = 0;
-  for (int a = a0; a < a1; ++a) np += torch_sigmoid(c[a]) >= conf;
+  for (int g0 = a0; g0 < a1; g0 += 8) {  // the logits of 8 anchors loaded together
+    float lr[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) lr[e] = g0 + e < a1 ? c[g0 + e] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) np += g0 + e < a1 && torch_sigmoid(lr[e]) >= conf;
+  }
   unsigned p = block_excl_scan(np, wsum);
   const int n = (int)wsum[16];
-  for (int a = a0; a < a1; ++a) {
-    const float s = torch_sigmoid(c[a]);
-    if (s >= conf) {
-      const long q = base + p;
-      w.anchor[q] = a;
-      w.score[q] = s;
-      w.k0[q] = desc_key(s);
-      w.v0[q] = (int)p;
-      decode_one(r + (long)a * 6, anchors + (long)a * 5, w.box + q * 5);
-      ++p;
+  for (int g0 = a0; g0 < a1; g0 += 8) {
+    float lr[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) lr[e] = g0 + e < a1 ? c[g0 + e] : 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int a = g0 + e;
+      const float s = torch_sigmoid(lr[e]);
+      if (a < a1 && s >= conf) {
+        const long q = base + p;
+        w.anchor[q] = a;
+        w.score[q] = s;
+        w.k0[q] = desc_key(s);
+        w.v0[q] = (int)p;
+        decode_one(r + (long)a * 6, anchors + (long)a * 5, w.box + q * 5);
+        ++p;
+      }
     }
   }
   if (t == 0) w.n[sm] = n;
