@@ -266,7 +266,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ X
 
 
 // ---------------------------------------------------------------- BatchNorm (NHWC [M, C])
-constexpr int BN_ROWS = 128;
+// 32-row partial blocks: 1125 workgroups for the neck's 36 000 x 512 maps (128-row blocks gave 282,
+// ~4 waves per CU, latency-bound: mode-2 partials 50.4 -> 41.0 us; profiles/r06_m_*)
+constexpr int BN_ROWS = 32;
 
 // mode 0: partial column sums of x; mode 1: sums of (x - mean)^2; mode 2: bwd sums of dz, dz*xhat
 __global__ __launch_bounds__(256) void bn_partial_kernel(int mode, const void* X, int xdt, const void* Y, int ydt,
@@ -394,22 +396,30 @@ static void launch_bn_partial(hipStream_t st, int mode, const void* X, int xdt, 
                        dydt, M, (int)C, mean, invstd, relu, part);
 }
 
-// Column sums of the per-block partials, 64 columns x 16 row phases per 1024-thread block
-// (the partial lists are hundreds of rows long: one thread per column left them latency-bound).
-IVIT_DEV float bn_colsum16(const float* __restrict__ part, int nb, long pstride, long off, int c, bool valid,
-                           float (*red)[64]) {
-  const int ph = threadIdx.x >> 6, lc = threadIdx.x & 63;
+// Column sums of the per-block partials, BN_NC columns x BN_PH row phases per 1024-thread block
+// (the partial lists are hundreds of rows long: one thread per column left them latency-bound);
+// each phase's rows with eight loads in flight, summed in row order, then the phases in order.
+constexpr int BN_PH = 64, BN_NC = 1024 / BN_PH;  // 16 columns x 64 phases: C / 16 workgroups
+IVIT_DEV float bn_colsum(const float* __restrict__ part, int nb, long pstride, long off, int c, bool valid,
+                         float (*red)[BN_NC]) {
+  const int ph = threadIdx.x / BN_NC, lc = threadIdx.x % BN_NC;
   float s = 0.f;
   if (valid) {
-#pragma unroll 4
-    for (int k = ph; k < nb; k += 16) s += part[(long)k * pstride + off + c];
+    for (int k0 = ph; k0 < nb; k0 += 8 * BN_PH) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = k0 + i * BN_PH < nb ? part[(long)(k0 + i * BN_PH) * pstride + off + c] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (k0 + i * BN_PH < nb) s += v[i];
+    }
   }
   red[ph][lc] = s;
   __syncthreads();
   float t = 0.f;
   if (ph == 0) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) t += red[k][lc];
+#pragma unroll 8
+    for (int k = 0; k < BN_PH; ++k) t += red[k][lc];
   }
   __syncthreads();
   return t;
@@ -417,19 +427,19 @@ IVIT_DEV float bn_colsum16(const float* __restrict__ part, int nb, long pstride,
 
 __global__ __launch_bounds__(1024) void bn_mean_kernel(const float* __restrict__ part, int nb, long M, int C,
                                                        float* mean) {
-  __shared__ float red[16][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float s = bn_colsum16(part, nb, 2L * C, 0, c, c < C, red);
-  if (threadIdx.x < 64 && c < C) mean[c] = s / (float)M;
+  __shared__ float red[BN_PH][BN_NC];
+  const int c = blockIdx.x * BN_NC + (threadIdx.x % BN_NC);
+  const float s = bn_colsum(part, nb, 2L * C, 0, c, c < C, red);
+  if (threadIdx.x < BN_NC && c < C) mean[c] = s / (float)M;
 }
 
 __global__ __launch_bounds__(1024) void bn_var_kernel(const float* __restrict__ part, int nb, long M, int C,
                                                       const float* mean, float* invstd, float* run_mean,
                                                       float* run_var, float mom, float eps) {
-  __shared__ float red[16][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float s = bn_colsum16(part, nb, 2L * C, 0, c, c < C, red);
-  if (threadIdx.x < 64 && c < C) {
+  __shared__ float red[BN_PH][BN_NC];
+  const int c = blockIdx.x * BN_NC + (threadIdx.x % BN_NC);
+  const float s = bn_colsum(part, nb, 2L * C, 0, c, c < C, red);
+  if (threadIdx.x < BN_NC && c < C) {
     const float var = s / (float)M;
     invstd[c] = 1.0f / sqrtf(var + eps);
     if (run_mean) run_mean[c] = (1.f - mom) * run_mean[c] + mom * mean[c];
@@ -453,7 +463,7 @@ __global__ void bn_apply_kernel(const void* X, int xdt, long M, int C, const flo
 // parameters are loaded once per thread (per element they were 4x the bytes of the data), rows
 // strided by C; the same per-element arithmetic as bn_apply_kernel / bn_bwd_apply_kernel (bitwise
 // the same results), 16-B accesses. Thread t: chunk t % (C / 8), rows (t / (C / 8)) * BN8_R + 0..
-constexpr int BN8_R = 8;
+constexpr int BN8_R = 2;  // (8 rows per thread: 4.4 workgroups per CU on the neck's maps)
 __global__ __launch_bounds__(256) void bn_apply8_kernel(const void* X, int xdt, long M, int C,
                                                        const float* __restrict__ mean,
                                                        const float* __restrict__ invstd,
@@ -547,11 +557,11 @@ __global__ void bn_bwd_apply_kernel(const void* X, int xdt, const void* Y, int y
 
 __global__ __launch_bounds__(1024) void bn_bwd_final_kernel(const float* __restrict__ part, int nb, int C,
                                                             float* sums, float* dg, float* db, int acc) {
-  __shared__ float red[16][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const float s = bn_colsum16(part, nb, 2L * C, 0, c, c < C, red);
-  const float t = bn_colsum16(part, nb, 2L * C, C, c, c < C, red);
-  if (threadIdx.x < 64 && c < C) {
+  __shared__ float red[BN_PH][BN_NC];
+  const int c = blockIdx.x * BN_NC + (threadIdx.x % BN_NC);
+  const float s = bn_colsum(part, nb, 2L * C, 0, c, c < C, red);
+  const float t = bn_colsum(part, nb, 2L * C, C, c, c < C, red);
+  if (threadIdx.x < BN_NC && c < C) {
     sums[c] = s;
     sums[C + c] = t;
     if (db) db[c] = acc ? db[c] + s : s;
@@ -642,9 +652,9 @@ extern "C" int ivit_bn_stats(const void* X, int x_dtype, long M, long C, float* 
   const int nb = ivit_cdiv(M, BN_ROWS);
   float* part = (float*)work;
   launch_bn_partial(st, 0, X, x_dtype, nullptr, 0, nullptr, 0, M, C, nullptr, nullptr, 0, part);
-  hipLaunchKernelGGL(bn_mean_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, M, (int)C, mean);
+  hipLaunchKernelGGL(bn_mean_kernel, dim3(ivit_cdiv(C, BN_NC)), dim3(1024), 0, st, part, nb, M, (int)C, mean);
   launch_bn_partial(st, 1, X, x_dtype, nullptr, 0, nullptr, 0, M, C, mean, nullptr, 0, part);
-  hipLaunchKernelGGL(bn_var_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, M, (int)C, mean, invstd,
+  hipLaunchKernelGGL(bn_var_kernel, dim3(ivit_cdiv(C, BN_NC)), dim3(1024), 0, st, part, nb, M, (int)C, mean, invstd,
                      run_mean, run_var, momentum, eps);
   IVIT_LAUNCH_CHECK();
   return 0;
@@ -698,7 +708,7 @@ extern "C" int ivit_bn_bwd(const void* X, int x_dtype, const void* Y, int y_dtyp
   float* part = (float*)work;
   float* sums = part + (long)nb * 2 * C;
   launch_bn_partial(st, 2, X, x_dtype, Y, y_dtype, dY, dy_dtype, M, C, mean, invstd, relu, part);
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ivit_cdiv(C, 64)), dim3(1024), 0, st, part, nb, (int)C, sums, dg, db,
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(ivit_cdiv(C, BN_NC)), dim3(1024), 0, st, part, nb, (int)C, sums, dg, db,
                      accumulate);
   const bool v8 = C % 8 == 0 && hal16(X) && (!relu || hal16(Y)) && hal16(dY) && hal16(dX) && (!dR || hal16(dR)) &&
                   hal16(mean) && hal16(invstd) && hal16(g) && hal16(sums);
