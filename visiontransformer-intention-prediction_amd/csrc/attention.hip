@@ -250,6 +250,17 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_fwd_bf16_v6_kernel(const b
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (nt > 1) issue1(Kb, 1, smem[1][0]);
+  if (bid.x * (32 * W) + wv * 32 >= N) {
+    // a wave whose 32 queries are all past N (the ragged last row tile: at N = 4501 three of its four
+    // waves) only keeps the workgroup's DMA / barrier cadence
+    for (int j = 0; j < nt; ++j) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (j + 2 < nt) issue1(Kb, j + 2, smem[j & 1][0]);
+      if (j + 1 < nt) issue1(Vb, j + 1, smem[(j & 1) ^ 1][1]);
+    }
+    return;
+  }
   f32x16 sc[2], sn[2];
   qk_tile_c(smem[0][0], qf, zero16(), sc, lane);
   float m = nfull > 0 ? tile_rowmax<false>(sc, 0, N, lane) : tile_rowmax<true>(sc, 0, N, lane);
@@ -603,6 +614,15 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dkv_v4_kernel(const bf
   }
 #pragma unroll
   for (int w = 0; w < 4; ++w) upA[w] = udA[w] = 0u;
+  if (kw >= N) {  // all 32 keys past N (ragged last key tile): the DMA / barrier cadence only
+    for (int j = 0; j < nt; ++j) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (j + 2 < nt) issue(j + 2, (j + 2) % BNS);
+    }
+    __syncthreads();  // the store phase's barrier
+    return;
+  }
   auto tile = [&](auto st, int j) {
     constexpr int S = decltype(st)::value;
     using SP = std::integral_constant<int, (S + BNS - 1) % BNS>;
@@ -792,6 +812,19 @@ __global__ __launch_bounds__(64 * W, 8 / W) void attn_bwd_dq_v4_kernel(const bf1
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
+  if (qw >= N) {  // all 32 queries past N (ragged last row tile): the DMA / barrier cadence only
+    for (int j = 0; j < nfull; ++j) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (j + 2 < nt) issue(j + 2, (j + 2) % BNS);
+    }
+    if (nt > nfull) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    __syncthreads();  // the store phase's barrier
+    return;
+  }
   if (nfull > 0) {
     unsigned ro[2], tro[4];
 #pragma unroll
