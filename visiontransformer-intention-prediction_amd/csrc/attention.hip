@@ -678,6 +678,7 @@ IVIT_DEV void dq16_tile_masked(const char* kimg, const char* vimg, const bf16x8 
   const int g = lane >> 4, c16 = lane & 15, q = (lane >> 2) & 3, p = lane & 3;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
+    if (kbase + 32 * t >= N) break;  // a 32-key unit wholly past N adds nothing (N = 4501: the second)
     f32x4 s[2][2], dp[2][2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
