@@ -68,6 +68,10 @@ def test_workspace_queries_are_pure_host():
     assert dll.ivit_nms_workspace(22500) > 0
     assert dll.ivit_eval_post_workspace(32, 22500) >= 32 * 22500 * 352 * 8  # the padded suppression masks
     assert dll.ivit_eval_post_workspace(0, 22500) == 64
+    # BatchNorm partials: 32-row blocks, doubled past 65 535 blocks (the grid's y dimension)
+    assert dll.ivit_bn_workspace(36000, 512) == (1125 * 2 + 2) * 512 * 4
+    m = 8 * 400 * 720
+    assert dll.ivit_bn_workspace(m, 64) == (-(-m // 64) * 2 + 2) * 64 * 4
 
 
 def test_ptr_refuses_host_tensors():

@@ -717,9 +717,11 @@ def test_patch_im2col_bitexact():
     assert torch.equal(cols.cpu(), ref.to(torch.bfloat16).cpu())
 
 
-def test_batchnorm_train():
+@pytest.mark.parametrize("M,C", [(1000, 96), (2_200_007, 16)])
+def test_batchnorm_train(M, C):
+    """Training-mode BatchNorm forward / backward vs f64 torch; 2.2 M rows is past 32 x 65 535, where
+    the partial-sum blocks grow to 64 rows (a full-grid B = 8 CNN map has 2.3 M)."""
     import ops
-    M, C = 1000, 96
     x = torch.randn(M, C) * 3 + 1
     g, b = 1 + 0.1 * torch.randn(C), 0.1 * torch.randn(C)
     rm, rv = torch.zeros(C), torch.ones(C)

@@ -266,24 +266,29 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ X
 
 
 // ---------------------------------------------------------------- BatchNorm (NHWC [M, C])
-// 32-row partial blocks: 1125 workgroups for the neck's 36 000 x 512 maps (128-row blocks gave 282,
-// ~4 waves per CU, latency-bound: mode-2 partials 50.4 -> 41.0 us; profiles/r06_m_*)
-constexpr int BN_ROWS = 32;
+// Rows per partial block: 32 (1125 workgroups for the neck's 36 000 x 512 maps; 128-row blocks gave
+// 282, ~4 waves per CU, latency-bound: mode-2 partials 50.4 -> 41.0 us, profiles/r06_m_*), doubled
+// until the blocks fit the grid's y dimension (a B = 8 full-grid CNN map has 2.3 M rows)
+static int bn_rows(long M) {
+  long r = 32;
+  while ((M + r - 1) / r > 65535) r *= 2;
+  return (int)r;
+}
 
 // mode 0: partial column sums of x; mode 1: sums of (x - mean)^2; mode 2: bwd sums of dz, dz*xhat
 __global__ __launch_bounds__(256) void bn_partial_kernel(int mode, const void* X, int xdt, const void* Y, int ydt,
                                                          const void* dY, int dydt, long M, int C,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ invstd, int relu,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part, int rows) {
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int ph = threadIdx.x >> 6;
-  const long r0 = (long)blockIdx.y * BN_ROWS;
+  const long r0 = (long)blockIdx.y * rows;
   float s = 0.f, t = 0.f;
   if (col < C) {
     const float mu = mode ? mean[col] : 0.f;
     const float is = mode == 2 ? invstd[col] : 0.f;
-    for (long r = r0 + ph; r < min(M, r0 + BN_ROWS); r += 4) {
+    for (long r = r0 + ph; r < min(M, r0 + rows); r += 4) {
       const long i = r * C + col;
       const float x = ldv(X, xdt, i);
       if (mode == 0) s += x;
@@ -320,10 +325,10 @@ __global__ __launch_bounds__(256) void bn_partial8_kernel(int mode, const void* 
                                                           const void* dY, int dydt, long M, int C,
                                                           const float* __restrict__ mean,
                                                           const float* __restrict__ invstd, int relu,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part, int rows) {
   const int lc = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int col = (blockIdx.x * 64 + lc) * 8;
-  const long r0 = (long)blockIdx.y * BN_ROWS;
+  const long r0 = (long)blockIdx.y * rows;
   float s[8], t[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s[e] = t[e] = 0.f;
@@ -334,7 +339,7 @@ __global__ __launch_bounds__(256) void bn_partial8_kernel(int mode, const void* 
       mu[e] = mode ? mean[col + e] : 0.f;
       is[e] = mode == 2 ? invstd[col + e] : 0.f;
     }
-    const long rend = min(M, r0 + BN_ROWS);
+    const long rend = min(M, r0 + rows);
 #pragma unroll 4
     for (long r = r0 + ph; r < rend; r += 4) {
       const long i = r * C + col;
@@ -387,13 +392,13 @@ __global__ __launch_bounds__(256) void bn_partial8_kernel(int mode, const void* 
 static void launch_bn_partial(hipStream_t st, int mode, const void* X, int xdt, const void* Y, int ydt,
                               const void* dY, int dydt, long M, long C, const float* mean, const float* invstd,
                               int relu, float* part) {
-  const int nb = ivit_cdiv(M, BN_ROWS);
+  const int rows = bn_rows(M), nb = ivit_cdiv(M, rows);
   if (C % 8 == 0)
     hipLaunchKernelGGL(bn_partial8_kernel, dim3(ivit_cdiv(C, 512), nb), dim3(256), 0, st, mode, X, xdt, Y, ydt, dY,
-                       dydt, M, (int)C, mean, invstd, relu, part);
+                       dydt, M, (int)C, mean, invstd, relu, part, rows);
   else
     hipLaunchKernelGGL(bn_partial_kernel, dim3(ivit_cdiv(C, 64), nb), dim3(256), 0, st, mode, X, xdt, Y, ydt, dY,
-                       dydt, M, (int)C, mean, invstd, relu, part);
+                       dydt, M, (int)C, mean, invstd, relu, part, rows);
 }
 
 // Column sums of the per-block partials, BN_NC columns x BN_PH row phases per 1024-thread block
@@ -643,13 +648,13 @@ extern "C" int ivit_layernorm_bwd(const float* X, long ldx, long rpb, long rstri
   return 0;
 }
 
-extern "C" long ivit_bn_workspace(long M, long C) { return ((long)ivit_cdiv(M, BN_ROWS) * 2 + 2) * C * 4; }
+extern "C" long ivit_bn_workspace(long M, long C) { return ((long)ivit_cdiv(M, bn_rows(M)) * 2 + 2) * C * 4; }
 
 extern "C" int ivit_bn_stats(const void* X, int x_dtype, long M, long C, float* mean, float* invstd, float* run_mean,
                              float* run_var, float momentum, float eps, void* work, long work_bytes, void* stream) {
   IVIT_CHECK_ARG(work_bytes >= ivit_bn_workspace(M, C), "ivit_bn_stats: workspace too small");
   hipStream_t st = ivit_stream(stream);
-  const int nb = ivit_cdiv(M, BN_ROWS);
+  const int nb = ivit_cdiv(M, bn_rows(M));
   float* part = (float*)work;
   launch_bn_partial(st, 0, X, x_dtype, nullptr, 0, nullptr, 0, M, C, nullptr, nullptr, 0, part);
   hipLaunchKernelGGL(bn_mean_kernel, dim3(ivit_cdiv(C, BN_NC)), dim3(1024), 0, st, part, nb, M, (int)C, mean);
@@ -704,7 +709,7 @@ extern "C" int ivit_bn_bwd(const void* X, int x_dtype, const void* Y, int y_dtyp
                            void* stream) {
   IVIT_CHECK_ARG(work_bytes >= ivit_bn_workspace(M, C), "ivit_bn_bwd: workspace too small");
   hipStream_t st = ivit_stream(stream);
-  const int nb = ivit_cdiv(M, BN_ROWS);
+  const int nb = ivit_cdiv(M, bn_rows(M));
   float* part = (float*)work;
   float* sums = part + (long)nb * 2 * C;
   launch_bn_partial(st, 2, X, x_dtype, Y, y_dtype, dY, dy_dtype, M, C, mean, invstd, relu, part);
