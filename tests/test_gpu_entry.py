@@ -112,6 +112,41 @@ def test_postprocess_adversarial_vs_reference_loop():
     assert got[2]["pred_scores"].numel() == 0 and got[1]["pred_scores"].numel() > 0
 
 
+def test_post_pipeline_equals_per_batch_postprocess():
+    """utils.PostPipeline (batch k's post-processing on its own stream beside batch k+1's work, counts
+    read one batch late) returns, batch by batch, exactly what postprocess_batch returns; the
+    producer stream reuses memory between pushes (the inputs are freed after each push), so a missing
+    stream hand-off would show as corrupted results. Includes an empty batch and a flush."""
+    import utils
+    g = torch.Generator().manual_seed(5)
+    anchors = O.generate_anchors(400, 720, 8).cuda()
+    NA = anchors.shape[0]
+    batches = []
+    for k in range(4):
+        B = 0 if k == 2 else 3
+        batches.append((torch.randn(B, NA, generator=g) * 2.0, torch.randn(B, NA, 6, generator=g) * 0.3,
+                        torch.round(torch.randn(B, NA, 8, generator=g))))
+    want = [utils.postprocess_batch(c.cuda(), b.cuda(), i.cuda(), anchors) for c, b, i in batches]
+    want = [[{k: v.cpu() for k, v in p.items()} for p in w] for w in want]
+    pipe = utils.PostPipeline(anchors)
+    got = []
+    for c, b, i in batches:
+        cd, bd, idv = c.cuda(), b.cuda(), i.cuda()
+        prev = pipe.push(cd, bd, idv)
+        del cd, bd, idv  # freed on the producer stream while the pipeline's kernels may still read them
+        junk = torch.full((3, NA, 8), float("nan"), device="cuda")  # likely lands in the freed blocks
+        if prev is not None:
+            got.append([{k: v.cpu() for k, v in p.items()} for p in prev])
+        del junk
+    got.append([{k: v.cpu() for k, v in p.items()} for p in pipe.flush()])
+    assert pipe.flush() is None and len(got) == len(want)
+    for k, (gb, wb) in enumerate(zip(got, want)):
+        assert len(gb) == len(wb), k
+        for p, q in zip(gb, wb):
+            for key in q:
+                assert torch.equal(p[key], q[key]), (k, key)
+
+
 def test_postprocess_empty_after_threshold():
     import utils
     anchors = O.generate_anchors(32, 48, 8).cuda()

@@ -9,7 +9,7 @@ Differences, none in the numerics: ``--synthetic`` evaluates seeded synthetic BE
 (random-init weights when no checkpoint exists, which makes every anchor pass the threshold
 — the worst case for NMS); checkpoints load with ``torch.load(weights_only=True)`` (the
 pickled ``BasicBlock`` class in ``backbone_cfg`` is allow-listed by name); post-processing runs
-on the device for the whole batch (utils.postprocess_batch); the mAP / intention matching
+on the device for the whole batch (utils.postprocess_batch, pipelined by utils.PostPipeline); the mAP / intention matching
 walk runs on the device for all samples in one launch (metrics.match_device, ivit_det_match). The reference's undefined names (eval_vit.py:12-13,39,196,219)
 come from constants.py / utils.py.
 """
@@ -28,7 +28,7 @@ from constants import (ANCHOR_CONFIGS_PAPER, DETECTION_IOU_THRESHOLDS, EVAL_USE_
 from metrics import detection_map_device as detection_map, intention_matches_device as intention_matches
 from model_vit import IntentNetViT
 from synthetic import SyntheticBEVLoader
-from utils import generate_anchors, postprocess_batch
+from utils import PostPipeline, generate_anchors
 
 VAL_DATA_DIR = "./data/argoverse2/sensor/val"
 MODEL_SAVE_PATH_VIT = "./trained_models_vit/vit_model.pth"
@@ -77,17 +77,31 @@ def parse_args(argv=None):
 
 
 def run_inference(model, loader, anchors, conf=CONFIDENCE_THRESHOLD, nms=NMS_IOU_THRESHOLD):
+    """eval_vit.py:136-180: forward + post-processing per batch, in loader order. The
+    post-processing of a batch (utils.PostPipeline) runs beside the next batch's forward; results
+    are the per-batch postprocess_batch ones, appended in the same order."""
     results = []
+    pipe = PostPipeline(anchors, conf, nms)
+    gts = []
+
+    def emit(preds):
+        for p, gt in zip(preds, gts.pop(0)):
+            results.append({**{k: v.cpu() for k, v in p.items()},
+                            "gt_boxes_xywha": gt.get("boxes_xywha", torch.empty((0, 5))),
+                            "gt_intentions": gt.get("intentions", torch.empty(0, dtype=torch.long))})
+
     with torch.inference_mode():
         for batch in loader:
             dev = anchors.device
             cls, box, it = model(batch["lidar_bev"].to(dev, non_blocking=True),
                                  batch["map_bev"].to(dev, non_blocking=True))
-            preds = postprocess_batch(cls, box, it, anchors, conf, nms)
-            for p, gt in zip(preds, batch["gt_list"]):
-                results.append({**{k: v.cpu() for k, v in p.items()},
-                                "gt_boxes_xywha": gt.get("boxes_xywha", torch.empty((0, 5))),
-                                "gt_intentions": gt.get("intentions", torch.empty(0, dtype=torch.long))})
+            gts.append(batch["gt_list"])
+            prev = pipe.push(cls, box, it)
+            if prev is not None:
+                emit(prev)
+        last = pipe.flush()
+        if last is not None:
+            emit(last)
     return results
 
 

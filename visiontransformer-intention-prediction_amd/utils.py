@@ -118,18 +118,10 @@ def nms_batched(boxes_list, scores_list, iou_threshold: float = 0.2):
     return [keep[seg[i]: seg[i] + cnt[i]] for i in range(S)]
 
 
-def postprocess_batch(cls_logits: torch.Tensor, box_preds_rel: torch.Tensor, intent_logits: torch.Tensor,
-                      anchors: torch.Tensor, conf_threshold: float = 0.1, nms_threshold: float = 0.2):
-    """eval_vit.py:156-176 for a whole batch on hand-written kernels (ivit_eval_post): sigmoid →
-    score >= conf in anchor order → decode → NMS → argmax intention, every sample at once, four
-    launches and ONE host read (the kept counts). Returns [{'pred_scores', 'pred_boxes_xywha',
-    'pred_intentions'}] per sample as device tensors (views of the packed outputs; the caller
-    moves them to the host when it needs them)."""
+def _post_launch(cls_logits, box_preds_rel, intent_logits, anchors, conf_threshold, nms_threshold):
+    """ivit_eval_post for a batch on the current stream; returns what _post_collect needs."""
     B, NA = cls_logits.shape[0], anchors.shape[0]
     dev = cls_logits.device
-    if NA == 0 or B == 0:
-        return [{"pred_scores": torch.empty((0,), device=dev), "pred_boxes_xywha": torch.empty((0, 5), device=dev),
-                 "pred_intentions": torch.empty((0,), dtype=torch.long, device=dev)} for _ in range(B)]
     cls = cls_logits.reshape(B, NA).float().contiguous()  # no copy for the model's f32 outputs
     box = box_preds_rel.reshape(B, NA, 6).float().contiguous()
     it = intent_logits.reshape(B, NA, -1).float().contiguous()
@@ -142,9 +134,79 @@ def postprocess_batch(cls_logits: torch.Tensor, box_preds_rel: torch.Tensor, int
     ws = workspace(lib.ivit_eval_post_workspace(B, NA), dev)
     lib.ivit_eval_post(ptr(cls), ptr(box), ptr(it), ptr(anc), B, NA, K, float(conf_threshold), float(nms_threshold),
                        ptr(sc), ptr(bx), ptr(ii), ptr(cnt), ptr(ws), ws.numel(), stream())
+    return sc, bx, ii, cnt
+
+
+def _post_collect(launched):
+    sc, bx, ii, cnt = launched
     n = cnt.cpu().tolist()  # the one host synchronisation
     return [{"pred_scores": sc[b, : n[b]], "pred_boxes_xywha": bx[b, : n[b]], "pred_intentions": ii[b, : n[b]]}
-            for b in range(B)]
+            for b in range(len(n))]
+
+
+def _post_empty(B, dev):
+    return [{"pred_scores": torch.empty((0,), device=dev), "pred_boxes_xywha": torch.empty((0, 5), device=dev),
+             "pred_intentions": torch.empty((0,), dtype=torch.long, device=dev)} for _ in range(B)]
+
+
+def postprocess_batch(cls_logits: torch.Tensor, box_preds_rel: torch.Tensor, intent_logits: torch.Tensor,
+                      anchors: torch.Tensor, conf_threshold: float = 0.1, nms_threshold: float = 0.2):
+    """eval_vit.py:156-176 for a whole batch on hand-written kernels (ivit_eval_post): sigmoid →
+    score >= conf in anchor order → decode → NMS → argmax intention, every sample at once, four
+    launches and ONE host read (the kept counts). Returns [{'pred_scores', 'pred_boxes_xywha',
+    'pred_intentions'}] per sample as device tensors (views of the packed outputs; the caller
+    moves them to the host when it needs them)."""
+    B, NA = cls_logits.shape[0], anchors.shape[0]
+    if NA == 0 or B == 0:
+        return _post_empty(B, cls_logits.device)
+    return _post_collect(_post_launch(cls_logits, box_preds_rel, intent_logits, anchors, conf_threshold,
+                                      nms_threshold))
+
+
+class PostPipeline:
+    """postprocess_batch over consecutive batches, one batch deep (the eval loop, config 4): batch
+    k's post-processing runs on its own HIP stream beside batch k+1's forward, and its kept counts
+    are read once batch k+1's forward is enqueued — so the post-processing (sort, NMS mask and walk,
+    ~4 ms of mostly serial kernels per B = 32 batch) no longer idles the ViT streams.
+    ``push(cls, box, intent)`` returns the previous batch's predictions (None for the first);
+    ``flush()`` returns the last one's. Same kernels and results as postprocess_batch."""
+
+    def __init__(self, anchors, conf_threshold=0.1, nms_threshold=0.2):
+        self.anchors, self.conf, self.nms = anchors, conf_threshold, nms_threshold
+        self.stream = torch.cuda.Stream(anchors.device) if anchors.is_cuda else None
+        if self.stream is not None:
+            anchors.record_stream(self.stream)
+        self.pending = None
+
+    def _collect(self):
+        if self.pending is None:
+            return None
+        p, self.pending = self.pending, None
+        if isinstance(p, list):  # empty batch
+            return p
+        if self.stream is None:
+            return _post_collect(p)
+        with torch.cuda.stream(self.stream):  # the count read waits for this batch's kernels only
+            return _post_collect(p)
+
+    def push(self, cls_logits, box_preds_rel, intent_logits):
+        prev = self._collect()  # batch k-1: its post-processing ran beside this batch's forward
+        B, NA = cls_logits.shape[0], self.anchors.shape[0]
+        if NA == 0 or B == 0:
+            self.pending = _post_empty(B, cls_logits.device)
+            return prev
+        if self.stream is None:
+            self.pending = _post_launch(cls_logits, box_preds_rel, intent_logits, self.anchors, self.conf, self.nms)
+            return prev
+        self.stream.wait_stream(torch.cuda.current_stream(cls_logits.device))  # this batch's forward
+        for t in (cls_logits, box_preds_rel, intent_logits):
+            t.record_stream(self.stream)
+        with torch.cuda.stream(self.stream):
+            self.pending = _post_launch(cls_logits, box_preds_rel, intent_logits, self.anchors, self.conf, self.nms)
+        return prev
+
+    def flush(self):
+        return self._collect()
 
 
 def calculate_ap(recall: np.ndarray, precision: np.ndarray) -> float:
