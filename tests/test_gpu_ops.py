@@ -988,6 +988,26 @@ def test_nms_random_vs_oracle(thr):
         assert np.array_equal(k.cpu().numpy(), w), i
 
 
+def test_nms_past_the_held_words_and_many_kept_per_column():
+    """n = 26 000 (407 mask words: the scan's later-word update past its two held words per thread)
+    with dense overlaps and scores in descending blocks, so columns keep more than 8 boxes (the
+    update's synchronous path): keep indices bit-exact vs the oracle, single and batched."""
+    from oracle import ivit_oracle as O
+    import utils
+    g = torch.Generator().manual_seed(17)
+    n = 26000
+    b = torch.stack([60 * torch.rand(n, generator=g), 60 * torch.rand(n, generator=g),
+                     0.3 + 1.5 * torch.rand(n, generator=g), 0.3 + 1.5 * torch.rand(n, generator=g),
+                     torch.zeros(n)], 1)
+    s = torch.round(torch.rand(n, generator=g) * 64) / 64
+    ref = O.nms_numpy(b.numpy(), s.numpy(), 0.2)
+    assert len(ref) > 700  # many columns keep more than 8
+    assert np.array_equal(utils.apply_nms(b.to(DEV), s.to(DEV), 0.2).cpu().numpy(), ref)
+    k = utils.nms_batched([b.to(DEV), b[:5000].to(DEV)], [s.to(DEV), s[:5000].to(DEV)], 0.2)
+    assert np.array_equal(k[0].cpu().numpy(), ref)
+    assert np.array_equal(k[1].cpu().numpy(), O.nms_numpy(b[:5000].numpy(), s[:5000].numpy(), 0.2))
+
+
 def test_nms_huge_areas_take_the_exact_division():
     """Boxes with areas near FLT_MAX / 4 (decoded boxes with a huge exp(dw)): the union is >= 2^126,
     where rcp(u) would be subnormal, so the fast IoU test must defer to the exact division — keep
