@@ -200,7 +200,12 @@ int ivit_unpack_conv_grad(const float* gp, long Cout, long Cin, long ks, float* 
 
 /* ---- Multi-head self-attention core: timm Attention -> F.scaled_dot_product_attention
  *      (softmax(Q K^T / sqrt(Dh)) V, no mask, no dropout). qkv: [B, N, 3, H, Dh] rows of 3*H*Dh;
- *      out: [B, N, H*Dh]; lse: [B, H, N] f32 (natural-log-sum-exp of the scaled scores).        */
+ *      out: [B, N, H*Dh]; lse: [B, H, N] f32 (natural-log-sum-exp of the scaled scores).
+ *      IVIT_BF16 is flash-style (no N x N buffer: the workspace holds the backward's row
+ *      constants and a prescaled Q copy). IVIT_F32, the exact parity path, materialises the scores:
+ *      its workspace is 4 B*H*N*ldS bytes (ldS >= N; twice that for the backward) — 0.49 GB per
+ *      sample at N = 4501, H = 6, and 7.8 GB at N = 18 001: sized for the parity tests and
+ *      config 1 (B = 1), not for training at scale.                                           */
 long ivit_attn_workspace(int dtype, long B, long N, long H, long Dh, int backward);
 int ivit_attn_fwd(int dtype, const void* qkv, long B, long N, long H, long Dh, void* out, float* lse, void* work,
                   long work_bytes, void* stream);
