@@ -153,3 +153,28 @@ def test_train_eval_entry_points_parse():
     assert e.batch == 32
     full = eval_vit.default_cfg({}, (400, 720))
     assert full["vit_model_name_map"] == "vit_tiny_patch8_224"  # eval_vit.py:77 default
+
+
+def test_post_pipeline_order_and_flush(monkeypatch):
+    """utils.PostPipeline's host logic (no kernels: launch / collect stubbed): push k returns batch k-1's
+    predictions in order, an empty batch passes through as an empty list, flush returns the last one
+    and then None."""
+    import utils
+    launched = []
+
+    def fake_launch(cls, box, it, anchors, conf, nms):
+        launched.append(int(cls[0, 0]))
+        return ("batch", int(cls[0, 0]))
+
+    monkeypatch.setattr(utils, "_post_launch", fake_launch)
+    monkeypatch.setattr(utils, "_post_collect", lambda p: [{"id": p[1]}])
+    anchors = torch.zeros(4, 5)
+    pipe = utils.PostPipeline(anchors)
+    assert pipe.stream is None  # CPU anchors: no side stream
+    out = []
+    for k in range(3):
+        out.append(pipe.push(torch.full((2, 4), float(k)), torch.zeros(2, 4, 6), torch.zeros(2, 4, 8)))
+    out.append(pipe.push(torch.zeros(0, 4), torch.zeros(0, 4, 6), torch.zeros(0, 4, 8)))  # empty batch
+    out.append(pipe.flush())
+    assert out == [None, [{"id": 0}], [{"id": 1}], [{"id": 2}], []]
+    assert pipe.flush() is None and launched == [0, 1, 2]
